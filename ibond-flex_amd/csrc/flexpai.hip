@@ -1,0 +1,530 @@
+// flexpai: host context + C ABI for the MI355X Paillier engine (see include/flexpai.h).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "flexpai.h"
+#include "host_bignum.hpp"
+#include "kernels.hpp"
+
+using namespace fpai;
+
+static thread_local std::string g_last_error;
+
+static int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+#define HIPCHK(expr)                                                                    \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) return fail(PAI_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+struct pai_ctx {
+  int device = 0;
+  int nb = 0;
+  int tpi_e = 0, S_e = 0;
+  int tpi_d = 0, S_d = 0;
+  int ct_words = 0, pt_words = 0;
+  HBig n, N;
+  uint32_t mprime_N = 0;
+  uint32_t *d_N = nullptr, *d_R2 = nullptr, *d_nl = nullptr;
+  uint16_t* d_sched = nullptr;
+  int nsched = 0, first = 0;
+  // private key material
+  bool has_priv = false;
+  DecHalf* d_halves = nullptr;
+  uint32_t *d_qinvR = nullptr, *d_nlimb = nullptr, *d_qRn = nullptr, *d_maxint = nullptr;
+  uint32_t nprime_d = 0;
+  int nwin = 0, n_limbs = 0;
+  std::vector<void*> allocs;
+  // scratch (exponent tables), grown on demand
+  void* d_scratch = nullptr;
+  size_t scratch_bytes = 0;
+  int cus = 0;
+  ~pai_ctx() {
+    hipSetDevice(device);
+    for (void* p : allocs) hipFree(p);
+    if (d_scratch) hipFree(d_scratch);
+  }
+};
+
+template <typename T>
+static int upload(pai_ctx* c, const std::vector<T>& v, T** out) {
+  void* p = nullptr;
+  HIPCHK(hipMalloc(&p, std::max<size_t>(v.size(), 1) * sizeof(T)));
+  c->allocs.push_back(p);
+  if (!v.empty()) HIPCHK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  *out = (T*)p;
+  return 0;
+}
+
+static int tpi_for_bits(size_t need_bits) {
+  for (int t : {2, 4, 8, 16})
+    if ((size_t)27 * 19 * t >= need_bits) return t;
+  return 0;
+}
+
+// left-to-right sliding window (k = 5) over the fixed public exponent n
+static void sliding_schedule(const HBig& e, std::vector<uint16_t>& ops, int& first) {
+  const int K = 5;
+  int i = (int)e.bits() - 1;
+  auto window = [&](int hi, int& lo, uint32_t& val) {
+    lo = std::max(hi - K + 1, 0);
+    while (!e.bit(lo)) ++lo;
+    val = 0;
+    for (int b = hi; b >= lo; --b) val = (val << 1) | (uint32_t)e.bit(b);
+  };
+  int lo;
+  uint32_t v;
+  window(i, lo, v);
+  first = (int)(v - 1) / 2;
+  i = lo - 1;
+  int nsq = 0;
+  while (i >= 0) {
+    if (!e.bit(i)) {
+      ++nsq;
+      --i;
+      continue;
+    }
+    window(i, lo, v);
+    nsq += i - lo + 1;
+    ops.push_back((uint16_t)nsq);
+    ops.push_back((uint16_t)((v - 1) / 2));
+    nsq = 0;
+    i = lo - 1;
+  }
+  if (nsq) {
+    ops.push_back((uint16_t)nsq);
+    ops.push_back(0xFFFF);
+  }
+}
+
+template <typename K>
+static int grid_for(pai_ctx* c, K kernel, size_t lds, long long units, int per_block) {
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, BLOCK, lds) != hipSuccess || occ < 1) occ = 1;
+  long long want = (units + per_block - 1) / per_block;
+  long long cap = (long long)occ * c->cus;
+  return (int)std::max<long long>(1, std::min(want, cap));
+}
+
+static int ensure_scratch(pai_ctx* c, size_t bytes) {
+  if (bytes <= c->scratch_bytes) return 0;
+  if (c->d_scratch) HIPCHK(hipFree(c->d_scratch));
+  c->d_scratch = nullptr;
+  c->scratch_bytes = 0;
+  HIPCHK(hipMalloc(&c->d_scratch, bytes));
+  c->scratch_bytes = bytes;
+  return 0;
+}
+
+// C-linkage comes from the declarations in flexpai.h.
+const char* pai_last_error(void) { return g_last_error.c_str(); }
+
+int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** out) {
+  if (!n_le || !out || n_bytes == 0) return fail(PAI_ERR_ARG, "pai_ctx_create: null argument");
+  HBig n = HBig::from_le_bytes(n_le, n_bytes);
+  if (!n.is_odd() || n.bits() < 64) return fail(PAI_ERR_KEY, "pai_ctx_create: n must be odd and >= 64 bits");
+  auto* c = new pai_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess) {
+    delete c;
+    return fail(PAI_ERR_HIP, "pai_ctx_create: hipSetDevice failed");
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+    delete c;
+    return fail(PAI_ERR_HIP, "pai_ctx_create: hipGetDeviceProperties failed");
+  }
+  c->cus = prop.multiProcessorCount;
+  c->n = n;
+  c->nb = (int)n.bits();
+  c->N = mul(n, n);
+  c->tpi_e = tpi_for_bits(2 * (size_t)c->nb + 2);
+  c->tpi_d = tpi_for_bits((size_t)c->nb + 3);
+  if (!c->tpi_e || !c->tpi_d) {
+    delete c;
+    return fail(PAI_ERR_KEY, "pai_ctx_create: key size not supported (max 4096 bits)");
+  }
+  c->S_e = 19 * c->tpi_e;
+  c->S_d = 19 * c->tpi_d;
+  c->ct_words = (2 * c->nb + 31) / 32;
+  c->pt_words = (c->nb + 31) / 32;
+  c->mprime_N = mont_prime27(c->N);
+  const size_t Rbits = (size_t)27 * c->S_e;
+  HBig R2 = mul_pow2_mod(HBig(1), 2 * Rbits, c->N);
+  std::vector<uint16_t> sched;
+  sliding_schedule(n, sched, c->first);
+  c->nsched = (int)sched.size() / 2;
+  int rc;
+  if ((rc = upload(c, c->N.limbs27(c->S_e), &c->d_N)) || (rc = upload(c, R2.limbs27(c->S_e), &c->d_R2)) ||
+      (rc = upload(c, n.limbs27(c->S_e), &c->d_nl)) || (rc = upload(c, sched, &c->d_sched))) {
+    delete c;
+    return rc;
+  }
+  *out = c;
+  return 0;
+}
+
+int pai_ctx_set_private(pai_ctx* c, const uint8_t* p_le, const uint8_t* q_le, size_t half_bytes) {
+  if (!c || !p_le || !q_le) return fail(PAI_ERR_ARG, "pai_ctx_set_private: null argument");
+  HIPCHK(hipSetDevice(c->device));
+  HBig p = HBig::from_le_bytes(p_le, half_bytes), q = HBig::from_le_bytes(q_le, half_bytes);
+  if (cmp(mul(p, q), c->n) != 0) return fail(PAI_ERR_KEY, "given public key does not match the given p and q");
+  if (cmp(p, q) == 0) return fail(PAI_ERR_KEY, "p and q have to be different");
+  if (cmp(q, p) < 0) std::swap(p, q);   // keypair.py:57-62
+  const int S = c->S_d;
+  const size_t Rbits = (size_t)27 * S;
+  HBig hp, hq;
+  {
+    HBig qi = inv_mod(q, p), pi = inv_mod(p, q);
+    if (qi.is_zero() || pi.is_zero()) return fail(PAI_ERR_KEY, "p, q not coprime");
+    hp = sub(p, qi);   // (-q)^-1 mod p == L(g^(p-1) mod p^2, p)^-1 (keypair.py:81-90, g = n + 1)
+    hq = sub(q, pi);
+  }
+  HBig primes[2] = {p, q}, hs[2] = {hp, hq};
+  size_t ebits = std::max(sub(p, HBig(1)).bits(), sub(q, HBig(1)).bits());
+  c->nwin = (int)((ebits + 4) / 5);
+  DecHalf hh[2];
+  int rc;
+  for (int h = 0; h < 2; ++h) {
+    const HBig& ph = primes[h];
+    HBig m = mul(ph, ph);
+    HBig e = sub(ph, HBig(1));
+    std::vector<uint8_t> dig(c->nwin);
+    for (int w = 0; w < c->nwin; ++w) {
+      int v = 0;
+      for (int b = 4; b >= 0; --b) v = (v << 1) | e.bit((size_t)(c->nwin - 1 - w) * 5 + b);
+      dig[w] = (uint8_t)v;
+    }
+    uint32_t *dm, *dR3, *done, *dpneg, *dph, *dhR;
+    uint8_t* ddig;
+    HBig pneg = sub(pow2(Rbits), ph);
+    if ((rc = upload(c, m.limbs27(S), &dm)) ||
+        (rc = upload(c, mul_pow2_mod(HBig(1), 3 * Rbits, m).limbs27(S), &dR3)) ||
+        (rc = upload(c, mul_pow2_mod(HBig(1), Rbits, m).limbs27(S), &done)) ||
+        (rc = upload(c, pneg.limbs27(S), &dpneg)) || (rc = upload(c, ph.limbs27(S), &dph)) ||
+        (rc = upload(c, mul_pow2_mod(hs[h], Rbits, ph).limbs27(S), &dhR)) || (rc = upload(c, dig, &ddig)))
+      return rc;
+    hh[h] = DecHalf{dm, dR3, done, dpneg, dph, dhR, ddig, mont_prime27(m), mont_prime27(pneg), mont_prime27(ph), 0u};
+  }
+  std::vector<DecHalf> hv(hh, hh + 2);
+  if ((rc = upload(c, hv, &c->d_halves))) return rc;
+  HBig qinv = inv_mod(q, p);
+  HBig maxint = sub(div_small(c->n, 3), HBig(1));   // keypair.py:29
+  if ((rc = upload(c, mul_pow2_mod(qinv, Rbits, p).limbs27(S), &c->d_qinvR)) ||
+      (rc = upload(c, c->n.limbs27(S), &c->d_nlimb)) ||
+      (rc = upload(c, mul_pow2_mod(mod(q, c->n), Rbits, c->n).limbs27(S), &c->d_qRn)) ||
+      (rc = upload(c, maxint.limbs27(S), &c->d_maxint)))
+    return rc;
+  c->nprime_d = mont_prime27(c->n);
+  c->n_limbs = (int)((c->n.bits() + 26) / 27);
+  c->has_priv = true;
+  return 0;
+}
+
+void pai_ctx_destroy(pai_ctx* c) { delete c; }
+
+int pai_ctx_info(const pai_ctx* c, int* key_bits, int* ct_words, int* pt_words) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (key_bits) *key_bits = c->nb;
+  if (ct_words) *ct_words = c->ct_words;
+  if (pt_words) *pt_words = c->pt_words;
+  return 0;
+}
+
+// ------------------------------------------------------------------ device entry points
+template <int TPI>
+static int launch_encrypt(pai_ctx* c, EncParams& p, hipStream_t st) {
+  constexpr int S = TPI * L;
+  constexpr int GPB = BLOCK / TPI;
+  const size_t lds = (size_t)GPB * S * 4;
+  const int grid = grid_for(c, k_encrypt<TPI>, lds, p.n, GPB);
+  int rc = ensure_scratch(c, (size_t)grid * GPB * TABLE_ODD * S * 4);
+  if (rc) return rc;
+  p.scratch = (uint32_t*)c->d_scratch;
+  hipLaunchKernelGGL(k_encrypt<TPI>, dim3(grid), dim3(BLOCK), lds, st, p);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int pai_encrypt_dev(pai_ctx* c, int dtype, const void* d_x, size_t N, int exp_mode, int32_t fixed_exp, int obf_mode,
+                    const uint32_t* d_r_words, size_t r_stride_words, size_t r_words, const uint8_t* rng_key32,
+                    uint64_t index_base, uint32_t* d_ct, int32_t* d_exp, int32_t* d_status, void* stream) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (N == 0) return 0;
+  if (dtype < 0 || dtype > 2 || !d_x || !d_ct || !d_exp) return fail(PAI_ERR_ARG, "pai_encrypt_dev: bad arguments");
+  if (obf_mode == PAI_OBF_GIVEN && (!d_r_words || r_words == 0 || r_words > (size_t)c->ct_words))
+    return fail(PAI_ERR_ARG, "pai_encrypt_dev: r must be given with 0 < r_words <= ct_words");
+  if (obf_mode == PAI_OBF_RNG && !rng_key32) return fail(PAI_ERR_ARG, "pai_encrypt_dev: rng key required");
+  if (obf_mode < 0 || obf_mode > 2) return fail(PAI_ERR_ARG, "pai_encrypt_dev: bad obf_mode");
+  HIPCHK(hipSetDevice(c->device));
+  EncParams p{};
+  p.x = d_x;
+  p.dtype = dtype;
+  p.exp_mode = exp_mode;
+  p.fexp = fixed_exp;
+  p.obf = obf_mode;
+  p.r = d_r_words;
+  p.r_stride = (long long)r_stride_words;
+  p.r_words = (int)r_words;
+  p.rng_words = (c->nb + 64 + 31) / 32;
+  if (rng_key32)
+    for (int i = 0; i < 8; ++i) std::memcpy(&p.rng_key[i], rng_key32 + 4 * i, 4);
+  p.index_base = index_base;
+  p.ct = d_ct;
+  p.exp = d_exp;
+  p.status = d_status;
+  p.n = (long long)N;
+  p.N = c->d_N;
+  p.R2 = c->d_R2;
+  p.nl = c->d_nl;
+  p.mprime = c->mprime_N;
+  p.sched = c->d_sched;
+  p.nsched = c->nsched;
+  p.first = c->first;
+  p.ct_words = c->ct_words;
+  hipStream_t st = (hipStream_t)stream;
+  switch (c->tpi_e) {
+    case 2: return launch_encrypt<2>(c, p, st);
+    case 4: return launch_encrypt<4>(c, p, st);
+    case 8: return launch_encrypt<8>(c, p, st);
+    case 16: return launch_encrypt<16>(c, p, st);
+  }
+  return fail(PAI_ERR_KEY, "unsupported group size");
+}
+
+template <int TPI>
+static int launch_add(pai_ctx* c, AddParams& p, hipStream_t st) {
+  constexpr int S = TPI * L;
+  constexpr int GPB = BLOCK / TPI;
+  const size_t lds = (size_t)GPB * S * 4;
+  const int grid = grid_for(c, k_add<TPI>, lds, p.n, GPB);
+  hipLaunchKernelGGL(k_add<TPI>, dim3(grid), dim3(BLOCK), lds, st, p);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int pai_add_dev(pai_ctx* c, const uint32_t* d_cts, const int32_t* d_exps, int k, size_t N, uint32_t* d_out,
+                int32_t* d_exp_out, void* stream) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (N == 0) return 0;
+  if (k < 1 || !d_cts || !d_exps || !d_out || !d_exp_out) return fail(PAI_ERR_ARG, "pai_add_dev: bad arguments");
+  HIPCHK(hipSetDevice(c->device));
+  AddParams p{d_cts, d_exps, k, d_out, d_exp_out, (long long)N, c->d_N, c->d_R2, c->mprime_N, c->ct_words};
+  hipStream_t st = (hipStream_t)stream;
+  switch (c->tpi_e) {
+    case 2: return launch_add<2>(c, p, st);
+    case 4: return launch_add<4>(c, p, st);
+    case 8: return launch_add<8>(c, p, st);
+    case 16: return launch_add<16>(c, p, st);
+  }
+  return fail(PAI_ERR_KEY, "unsupported group size");
+}
+
+template <int TPI>
+static int launch_decrypt(pai_ctx* c, DecParams& p, hipStream_t st) {
+  constexpr int S = TPI * L;
+  constexpr int EPB = BLOCK / (2 * TPI);
+  const size_t lds = (size_t)EPB * 4 * S * 4;
+  const int grid = grid_for(c, k_decrypt<TPI>, lds, p.n, EPB);
+  int rc = ensure_scratch(c, (size_t)grid * EPB * 2 * TABLE_FIX * S * 4);
+  if (rc) return rc;
+  p.scratch = (uint32_t*)c->d_scratch;
+  hipLaunchKernelGGL(k_decrypt<TPI>, dim3(grid), dim3(BLOCK), lds, st, p);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int pai_decrypt_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t N, double* d_val, int64_t* d_mant,
+                    int32_t* d_status, uint32_t* d_raw, void* stream) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (!c->has_priv) return fail(PAI_ERR_NOPRIV, "pai_decrypt: context has no private key");
+  if (N == 0) return 0;
+  if (!d_ct || !d_exp || !d_val || !d_status) return fail(PAI_ERR_ARG, "pai_decrypt_dev: bad arguments");
+  HIPCHK(hipSetDevice(c->device));
+  DecParams p{};
+  p.ct = d_ct;
+  p.exp = d_exp;
+  p.n = (long long)N;
+  p.val = d_val;
+  p.mant = d_mant;
+  p.status = d_status;
+  p.raw = d_raw;
+  p.halves = c->d_halves;
+  p.qinvR = c->d_qinvR;
+  p.nlimb = c->d_nlimb;
+  p.qRn = c->d_qRn;
+  p.maxint = c->d_maxint;
+  p.nprime = c->nprime_d;
+  p.nwin = c->nwin;
+  p.ct_words = c->ct_words;
+  p.pt_words = c->pt_words;
+  p.n_limbs = c->n_limbs;
+  hipStream_t st = (hipStream_t)stream;
+  switch (c->tpi_d) {
+    case 2: return launch_decrypt<2>(c, p, st);
+    case 4: return launch_decrypt<4>(c, p, st);
+    case 8: return launch_decrypt<8>(c, p, st);
+    case 16: return launch_decrypt<16>(c, p, st);
+  }
+  return fail(PAI_ERR_KEY, "unsupported group size");
+}
+
+// ------------------------------------------------------------------ host-buffer entry points
+struct DevScope {
+  std::vector<void*> ptrs;
+  ~DevScope() {
+    for (void* p : ptrs) hipFree(p);
+  }
+  template <typename T>
+  T* alloc(size_t n) {
+    void* p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) return nullptr;
+    ptrs.push_back(p);
+    return (T*)p;
+  }
+};
+
+int pai_encrypt(pai_ctx* c, int dtype, const void* x, size_t N, int exp_mode, int32_t fixed_exp, int obf_mode,
+                const uint8_t* r_le, size_t r_stride_bytes, size_t r_bytes, const uint8_t* rng_key32,
+                uint64_t index_base, uint32_t* ct_out, int32_t* exp_out, int32_t* status_out) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (N == 0) return 0;
+  if (!x || !ct_out || !exp_out) return fail(PAI_ERR_ARG, "pai_encrypt: null buffer");
+  HIPCHK(hipSetDevice(c->device));
+  const size_t esz = dtype == PAI_F32 ? 4 : 8;
+  DevScope ds;
+  void* dx = ds.alloc<uint8_t>(N * esz);
+  uint32_t* dct = ds.alloc<uint32_t>(N * c->ct_words);
+  int32_t* dexp = ds.alloc<int32_t>(N);
+  int32_t* dst = ds.alloc<int32_t>(N);
+  if (!dx || !dct || !dexp || !dst) return fail(PAI_ERR_HIP, "pai_encrypt: device allocation failed");
+  HIPCHK(hipMemcpy(dx, x, N * esz, hipMemcpyHostToDevice));
+  uint32_t* dr = nullptr;
+  size_t r_words = 0, r_stride_words = 0;
+  if (obf_mode == PAI_OBF_GIVEN) {
+    if (!r_le || r_bytes == 0) return fail(PAI_ERR_ARG, "pai_encrypt: r required");
+    r_words = (r_bytes + 3) / 4;
+    const size_t cnt = r_stride_bytes ? N : 1;
+    std::vector<uint32_t> hr(cnt * r_words, 0);
+    for (size_t i = 0; i < cnt; ++i) {
+      const uint8_t* src = r_le + i * r_stride_bytes;
+      std::memcpy(&hr[i * r_words], src, r_bytes);
+    }
+    dr = ds.alloc<uint32_t>(hr.size());
+    if (!dr) return fail(PAI_ERR_HIP, "pai_encrypt: device allocation failed");
+    HIPCHK(hipMemcpy(dr, hr.data(), hr.size() * 4, hipMemcpyHostToDevice));
+    r_stride_words = r_stride_bytes ? r_words : 0;
+  }
+  int rc = pai_encrypt_dev(c, dtype, dx, N, exp_mode, fixed_exp, obf_mode, dr, r_stride_words, r_words, rng_key32,
+                           index_base, dct, dexp, dst, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(ct_out, dct, N * c->ct_words * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(exp_out, dexp, N * 4, hipMemcpyDeviceToHost));
+  if (status_out) HIPCHK(hipMemcpy(status_out, dst, N * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int pai_add(pai_ctx* c, const uint32_t* const* cts, const int32_t* const* exps, int k, size_t N, uint32_t* ct_out,
+            int32_t* exp_out) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (N == 0) return 0;
+  if (k < 1 || !cts || !exps || !ct_out || !exp_out) return fail(PAI_ERR_ARG, "pai_add: bad arguments");
+  HIPCHK(hipSetDevice(c->device));
+  DevScope ds;
+  const size_t W = c->ct_words;
+  uint32_t* dcts = ds.alloc<uint32_t>((size_t)k * N * W);
+  int32_t* dexps = ds.alloc<int32_t>((size_t)k * N);
+  uint32_t* dout = ds.alloc<uint32_t>(N * W);
+  int32_t* dexp = ds.alloc<int32_t>(N);
+  if (!dcts || !dexps || !dout || !dexp) return fail(PAI_ERR_HIP, "pai_add: device allocation failed");
+  for (int j = 0; j < k; ++j) {
+    if (!cts[j] || !exps[j]) return fail(PAI_ERR_ARG, "pai_add: null operand");
+    HIPCHK(hipMemcpy(dcts + (size_t)j * N * W, cts[j], N * W * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dexps + (size_t)j * N, exps[j], N * 4, hipMemcpyHostToDevice));
+  }
+  int rc = pai_add_dev(c, dcts, dexps, k, N, dout, dexp, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(ct_out, dout, N * W * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(exp_out, dexp, N * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int pai_decrypt(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, double* val_out, int64_t* mant_out,
+                int32_t* status_out, uint32_t* raw_out) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (!c->has_priv) return fail(PAI_ERR_NOPRIV, "pai_decrypt: context has no private key");
+  if (N == 0) return 0;
+  if (!ct || !exp || !val_out || !status_out) return fail(PAI_ERR_ARG, "pai_decrypt: null buffer");
+  HIPCHK(hipSetDevice(c->device));
+  DevScope ds;
+  uint32_t* dct = ds.alloc<uint32_t>(N * c->ct_words);
+  int32_t* dexp = ds.alloc<int32_t>(N);
+  double* dval = ds.alloc<double>(N);
+  int64_t* dmant = ds.alloc<int64_t>(N);
+  int32_t* dst = ds.alloc<int32_t>(N);
+  uint32_t* draw = raw_out ? ds.alloc<uint32_t>(N * c->pt_words) : nullptr;
+  if (!dct || !dexp || !dval || !dmant || !dst || (raw_out && !draw))
+    return fail(PAI_ERR_HIP, "pai_decrypt: device allocation failed");
+  HIPCHK(hipMemcpy(dct, ct, N * c->ct_words * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dexp, exp, N * 4, hipMemcpyHostToDevice));
+  int rc = pai_decrypt_dev(c, dct, dexp, N, dval, dmant, dst, draw, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(val_out, dval, N * 8, hipMemcpyDeviceToHost));
+  if (mant_out) HIPCHK(hipMemcpy(mant_out, dmant, N * 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(status_out, dst, N * 4, hipMemcpyDeviceToHost));
+  if (raw_out) HIPCHK(hipMemcpy(raw_out, draw, N * c->pt_words * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+
+// ------------------------------------------------------------------ engine unit-test hook
+template <int TPI>
+static int launch_debug(pai_ctx* c, DbgParams& p) {
+  constexpr int S = TPI * L;
+  constexpr int GPB = BLOCK / TPI;
+  const size_t lds = (size_t)GPB * S * 4;
+  const int grid = (int)((p.n + GPB - 1) / GPB);
+  int rc = ensure_scratch(c, (size_t)grid * GPB * TABLE_ODD * S * 4);
+  if (rc) return rc;
+  p.scratch = (uint32_t*)c->d_scratch;
+  hipLaunchKernelGGL(k_debug<TPI>, dim3(grid), dim3(BLOCK), lds, (hipStream_t)0, p);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int pai_debug_engine(pai_ctx* c, int op, const uint32_t* a, const uint32_t* b, size_t N, uint32_t* out,
+                                int32_t* flag) {
+  if (!c || N == 0) return fail(PAI_ERR_ARG, "pai_debug_engine: bad args");
+  HIPCHK(hipSetDevice(c->device));
+  DevScope ds;
+  const size_t W = c->ct_words;
+  uint32_t* da = ds.alloc<uint32_t>(N * W);
+  uint32_t* db = ds.alloc<uint32_t>(N * W);
+  uint32_t* dout = ds.alloc<uint32_t>(N * W);
+  int32_t* dflag = ds.alloc<int32_t>(N);
+  HIPCHK(hipMemcpy(da, a, N * W * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(db, b, N * W * 4, hipMemcpyHostToDevice));
+  DbgParams p{op, da, db, dout, dflag, (long long)N, (int)W, c->d_N, c->d_R2, c->d_nl, c->mprime_N,
+              c->d_sched, c->nsched, c->first, nullptr};
+  int rc = 0;
+  switch (c->tpi_e) {
+    case 2: rc = launch_debug<2>(c, p); break;
+    case 4: rc = launch_debug<4>(c, p); break;
+    case 8: rc = launch_debug<8>(c, p); break;
+    case 16: rc = launch_debug<16>(c, p); break;
+  }
+  if (rc) return rc;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(out, dout, N * W * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(flag, dflag, N * 4, hipMemcpyDeviceToHost));
+  return 0;
+}

@@ -1,0 +1,602 @@
+// Paillier array kernels for gfx950. One element per lane group (encrypt / add) or per
+// pair of lane groups (CRT decrypt: p-half and q-half side by side in one wavefront).
+#pragma once
+#include "bn_group.hpp"
+#include "device_ops.hpp"
+
+namespace fpai {
+
+constexpr int BLOCK = 256;
+constexpr int TABLE_ODD = 16;   // sliding window k=5: odd powers x^1..x^31
+constexpr int TABLE_FIX = 32;   // fixed window k=5: x^0..x^31
+
+struct EncParams {
+  const void* x;
+  int dtype, exp_mode, fexp, obf;
+  const uint32_t* r;
+  long long r_stride;   // words
+  int r_words;
+  int rng_words;
+  uint32_t rng_key[8];
+  unsigned long long index_base;
+  uint32_t* ct;
+  int32_t* exp;
+  int32_t* status;
+  long long n;
+  const uint32_t* N;    // n^2, 27-bit limbs (S)
+  const uint32_t* R2;   // R^2 mod n^2
+  const uint32_t* nl;   // n limbs (S, zero padded)
+  uint32_t mprime;
+  const uint16_t* sched;
+  int nsched, first;
+  uint32_t* scratch;
+  int ct_words;
+};
+
+struct AddParams {
+  const uint32_t* cts;    // k x n x ct_words
+  const int32_t* exps;    // k x n
+  int k;
+  uint32_t* out;
+  int32_t* out_exp;
+  long long n;
+  const uint32_t* N;
+  const uint32_t* R2;
+  uint32_t mprime;
+  int ct_words;
+};
+
+// Per-half (p: h=0, q: h=1) constants for CRT decryption; all 27-bit limb arrays of S limbs.
+// Lives in device memory (indexed per lane by the half a lane works on).
+struct DecHalf {
+  const uint32_t* m;      // p^2
+  const uint32_t* R3;     // R^3 mod p^2
+  const uint32_t* one;    // R mod p^2
+  const uint32_t* pneg;   // 2^(27S) - p
+  const uint32_t* ph;     // p
+  const uint32_t* hR;     // hp * R mod p
+  const uint8_t* digits;  // exponent p-1 in 5-bit windows, most significant first
+  uint32_t mprime, dprime, pprime, pad;
+};
+
+struct DecParams {
+  const uint32_t* ct;
+  const int32_t* exp;
+  long long n;
+  double* val;
+  int64_t* mant;
+  int32_t* status;
+  uint32_t* raw;
+  const DecHalf* halves;   // device array [2]
+  const uint32_t* qinvR;   // q^-1 * R mod p
+  const uint32_t* nlimb;   // n
+  const uint32_t* qRn;     // q * R mod n
+  const uint32_t* maxint;  // n // 3 - 1
+  uint32_t nprime;
+  int nwin;
+  int ct_words, pt_words;
+  int n_limbs;             // limbs actually used by n (<= S)
+  uint32_t* scratch;
+};
+
+// ---------------------------------------------------------------- small helpers
+template <int TPI>
+__device__ __forceinline__ void load_limbs_g(const uint32_t* __restrict__ g, uint32_t (&x)[L], int tig) {
+#pragma unroll
+  for (int i = 0; i < L; ++i) x[i] = g[tig * L + i];
+}
+template <int TPI>
+__device__ __forceinline__ void store_limbs_g(uint32_t* __restrict__ g, const uint32_t (&x)[L], int tig) {
+#pragma unroll
+  for (int i = 0; i < L; ++i) g[tig * L + i] = x[i];
+}
+template <int TPI>
+__device__ __forceinline__ void copy_g_to_lds(uint32_t* slot, const uint32_t* __restrict__ g, int tig) {
+  uint32_t t[L];
+  load_limbs_g<TPI>(g, t, tig);
+  write_limbs_lds<TPI>(slot, t, tig);
+}
+template <int TPI>
+__device__ __forceinline__ void write_limbs_lds_if(uint32_t* slot, const uint32_t (&x)[L], int tig, bool pred) {
+  wave_lds_fence();
+  if (pred) {
+#pragma unroll
+    for (int i = 0; i < L; ++i) slot[tig * L + i] = x[i];
+  }
+  wave_lds_fence();
+}
+template <int TPI>
+__device__ __forceinline__ void write_one_lds(uint32_t* slot, int tig) {
+  uint32_t t[L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) t[i] = (tig == 0 && i == 0) ? 1u : 0u;
+  write_limbs_lds<TPI>(slot, t, tig);
+}
+
+// c0 = 1 + n*M mod n^2 (raw_encrypt.py:37-45; the "sneaky inverse" branch yields the same
+// value). Branch-free across groups: both signs are computed and selected per group.
+template <int TPI>
+__device__ __forceinline__ void make_c0(int64_t M, const uint32_t* __restrict__ nl, const uint32_t (&m)[L],
+                                        uint32_t (&c0)[L], int lane, int tig) {
+  const bool neg = M < 0;
+  const uint64_t mag = neg ? (uint64_t)0 - (uint64_t)M : (uint64_t)M;
+  const uint32_t M0 = (uint32_t)mag & LMASK, M1 = (uint32_t)(mag >> LB) & LMASK, M2 = (uint32_t)(mag >> (2 * LB));
+  uint64_t P[L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int k = tig * L + i;
+    const uint64_t a0 = nl[k];
+    const uint64_t a1 = k >= 1 ? nl[k - 1] : 0u;
+    const uint64_t a2 = k >= 2 ? nl[k - 2] : 0u;
+    P[i] = a0 * M0 + a1 * M1 + a2 * M2;
+  }
+  uint32_t X[L], D[L];
+  normalize<TPI>(P, X, lane, tig);
+  (void)sub_limbs<TPI>(m, X, D, lane, tig);   // n^2 - n|M| (only used when M < 0)
+#pragma unroll
+  for (int i = 0; i < L; ++i) P[i] = (uint64_t)(neg ? D[i] : X[i]) + ((tig == 0 && i == 0) ? 1u : 0u);
+  normalize<TPI>(P, c0, lane, tig);
+}
+
+// acc = x^E mod m in the Montgomery domain, sliding window k=5 over the fixed public exponent
+// E = n (host-built schedule), odd-power table in global scratch.
+template <int TPI>
+__device__ __forceinline__ void modexp_sliding(uint32_t (&acc)[L], const uint32_t (&xt)[L], uint32_t* slot,
+                                               uint32_t* __restrict__ table, const uint16_t* __restrict__ sched,
+                                               int nsched, int first, const uint32_t (&m)[L], uint32_t mprime,
+                                               int lane, int tig) {
+  constexpr int S = TPI * L;
+  uint32_t cur[L];
+  store_limbs_g<TPI>(table, xt, tig);
+  write_limbs_lds<TPI>(slot, xt, tig);
+  uint32_t x2[L];
+  montmul<TPI>(x2, xt, slot, TPI, m, mprime, lane, tig);
+  write_limbs_lds<TPI>(slot, x2, tig);
+#pragma unroll
+  for (int i = 0; i < L; ++i) cur[i] = xt[i];
+  for (int k = 1; k < TABLE_ODD; ++k) {
+    montmul<TPI>(cur, cur, slot, TPI, m, mprime, lane, tig);
+    store_limbs_g<TPI>(table + k * S, cur, tig);
+  }
+  load_limbs_g<TPI>(table + first * S, acc, tig);
+  for (int op = 0; op < nsched; ++op) {
+    const int nsq = sched[2 * op];
+    const int idx = sched[2 * op + 1];
+    for (int t = 0; t < nsq; ++t) {
+      write_limbs_lds<TPI>(slot, acc, tig);
+      montmul<TPI>(acc, acc, slot, TPI, m, mprime, lane, tig);
+    }
+    if (idx != 0xFFFF) {
+      write_limbs_lds<TPI>(slot, acc, tig);
+      load_limbs_g<TPI>(table + idx * S, cur, tig);
+      montmul<TPI>(acc, cur, slot, TPI, m, mprime, lane, tig);
+    }
+  }
+}
+
+// Write canonical limbs (S of them) of the group's result to LDS and emit `nwords` 32-bit
+// little-endian words to global memory (lanes of the group interleave -> coalesced).
+template <int TPI>
+__device__ __forceinline__ void emit_words(uint32_t* slot, const uint32_t (&x)[L], uint32_t* __restrict__ out,
+                                           int nwords, bool valid, int tig) {
+  constexpr int S = TPI * L;
+  write_limbs_lds<TPI>(slot, x, tig);
+  if (valid) {
+    for (int j = tig; j < nwords; j += TPI) out[j] = limbs_word(slot, S, j);
+  }
+  wave_lds_fence();
+}
+
+// ================================================================= encrypt
+// PaillierEncryptor.encrypt over an array (encryptor.py:71-114): encode -> c0 -> c0 * r^n mod n^2
+template <int TPI>
+__global__ __launch_bounds__(BLOCK) void k_encrypt(EncParams p) {
+  constexpr int S = TPI * L;
+  constexpr int GPB = BLOCK / TPI;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int tig = threadIdx.x % TPI;
+  const int gib = threadIdx.x / TPI;
+  uint32_t* slot = smem + gib * S;
+  uint32_t m[L];
+  load_limbs_g<TPI>(p.N, m, tig);
+  uint32_t* table = p.scratch + (size_t)(blockIdx.x * GPB + gib) * TABLE_ODD * S;
+
+  for (long long base = (long long)blockIdx.x * GPB; base < p.n; base += (long long)gridDim.x * GPB) {
+    const long long inst = base + gib;
+    const bool valid = inst < p.n;
+    const long long ii = valid ? inst : p.n - 1;
+    int64_t M = 0;
+    int e = 0, st;
+    const bool fixed = p.exp_mode != 0;
+    if (p.dtype == 0) st = encode_float((double)((const float*)p.x)[ii], fixed, p.fexp, M, e);
+    else if (p.dtype == 1) st = encode_float(((const double*)p.x)[ii], fixed, p.fexp, M, e);
+    else st = encode_int(((const int64_t*)p.x)[ii], fixed, p.fexp, M, e);
+
+    uint32_t c0[L], res[L];
+    make_c0<TPI>(M, p.nl, m, c0, lane, tig);
+    if (p.obf == 0) {
+#pragma unroll
+      for (int i = 0; i < L; ++i) res[i] = c0[i];
+    } else {
+      uint32_t rl[L];
+      if (p.obf == 1) {
+        words_to_limbs(p.r + ii * p.r_stride, p.r_words, rl, tig);
+      } else {
+        // ChaCha20 block `tig` of this element's stream -> LDS words -> limbs
+        const unsigned long long gidx = p.index_base + (unsigned long long)ii;
+        uint32_t blk[16];
+        chacha20_block(p.rng_key, (uint32_t)tig, (uint32_t)gidx, (uint32_t)(gidx >> 32), 0x66786169u, blk);
+        wave_lds_fence();
+#pragma unroll
+        for (int w = 0; w < 16; ++w) slot[tig * 16 + w] = blk[w];
+        wave_lds_fence();
+        words_to_limbs(slot, p.rng_words, rl, tig);
+        wave_lds_fence();
+      }
+      uint32_t xt[L], acc[L];
+      copy_g_to_lds<TPI>(slot, p.R2, tig);
+      montmul<TPI>(xt, rl, slot, TPI, m, p.mprime, lane, tig);          // r * R mod n^2
+      modexp_sliding<TPI>(acc, xt, slot, table, p.sched, p.nsched, p.first, m, p.mprime, lane, tig);
+      write_limbs_lds<TPI>(slot, c0, tig);
+      montmul<TPI>(res, acc, slot, TPI, m, p.mprime, lane, tig);       // r^n * c0 mod n^2 (< 2 n^2)
+      cond_sub<TPI>(res, m, lane, tig);
+    }
+    emit_words<TPI>(slot, res, p.ct + ii * p.ct_words, p.ct_words, valid, tig);
+    if (valid && tig == 0) {
+      p.exp[ii] = e;
+      if (p.status) p.status[ii] = st;
+    }
+  }
+}
+
+// ================================================================= k-way homomorphic add
+// prod_j c_j^(16^(E - e_j)) mod n^2 (encrypted_number.py:115-137, 166-185)
+template <int TPI>
+__global__ __launch_bounds__(BLOCK) void k_add(AddParams p) {
+  constexpr int S = TPI * L;
+  constexpr int GPB = BLOCK / TPI;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int tig = threadIdx.x % TPI;
+  const int gib = threadIdx.x / TPI;
+  uint32_t* slot = smem + gib * S;
+  uint32_t m[L];
+  load_limbs_g<TPI>(p.N, m, tig);
+
+  for (long long base = (long long)blockIdx.x * GPB; base < p.n; base += (long long)gridDim.x * GPB) {
+    const long long inst = base + gib;
+    const bool valid = inst < p.n;
+    const long long ii = valid ? inst : p.n - 1;
+    int E = p.exps[ii];
+    for (int j = 1; j < p.k; ++j) E = max(E, p.exps[(long long)j * p.n + ii]);
+    uint32_t acc[L];
+    for (int j = 0; j < p.k; ++j) {
+      uint32_t cl[L], ct[L];
+      words_to_limbs(p.cts + ((long long)j * p.n + ii) * p.ct_words, p.ct_words, cl, tig);
+      copy_g_to_lds<TPI>(slot, p.R2, tig);
+      montmul<TPI>(ct, cl, slot, TPI, m, p.mprime, lane, tig);         // Montgomery form
+      const int nsq = 4 * (E - p.exps[(long long)j * p.n + ii]);
+      for (int t = 0;; ++t) {                                            // wave-uniform trip count
+        const bool need = t < nsq;
+        if (ballot(need) == 0ull) break;
+        uint32_t sq[L];
+        write_limbs_lds<TPI>(slot, ct, tig);
+        montmul<TPI>(sq, ct, slot, TPI, m, p.mprime, lane, tig);
+#pragma unroll
+        for (int i = 0; i < L; ++i) ct[i] = need ? sq[i] : ct[i];
+      }
+      if (j == 0) {
+#pragma unroll
+        for (int i = 0; i < L; ++i) acc[i] = ct[i];
+      } else {
+        write_limbs_lds<TPI>(slot, ct, tig);
+        montmul<TPI>(acc, acc, slot, TPI, m, p.mprime, lane, tig);
+      }
+    }
+    write_one_lds<TPI>(slot, tig);
+    montmul<TPI>(acc, acc, slot, TPI, m, p.mprime, lane, tig);           // leave the Montgomery domain
+    cond_sub<TPI>(acc, m, lane, tig);
+    emit_words<TPI>(slot, acc, p.out + ii * p.ct_words, p.ct_words, valid, tig);
+    if (valid && tig == 0) p.out_exp[ii] = E;
+  }
+}
+
+// ================================================================= CRT decrypt + decode
+// decryptor.py:33-63 (mp = L(c^(p-1) mod p^2) * hp mod p, mq likewise, gmpy_math.crt :31-40) and
+// FixedPointNumber.decode (fixedpoint_number.py:92-107). Lanes [0,TPI) of an element pair run the
+// p-half, lanes [TPI,2TPI) the q-half, with identical control flow (fixed-window exponent).
+__device__ __forceinline__ void decode_element(const uint32_t* xl, const DecParams& p, long long ii) {
+  // xl: canonical limbs of the plaintext x in [0, n), in LDS; one lane.
+  const int e = p.exp[ii];
+  const int nl = p.n_limbs;
+  int cmp_max = 0;   // sign(x - maxint)
+  for (int k = nl - 1; k >= 0 && cmp_max == 0; --k) {
+    const uint32_t a = xl[k], b = p.maxint[k];
+    cmp_max = (a > b) - (a < b);
+  }
+  bool neg = false;
+  int st = ST_OK;
+  // |mantissa| is x (x <= maxint) or n - x (x >= n - maxint)
+  uint32_t magv[160];
+  if (cmp_max <= 0) {
+    for (int k = 0; k < nl; ++k) magv[k] = xl[k];
+  } else {
+    int32_t b = 0;
+    for (int k = 0; k < nl; ++k) {
+      const int32_t v = (int32_t)p.nlimb[k] - (int32_t)xl[k] + b;
+      magv[k] = (uint32_t)v & LMASK;
+      b = v >> LB;
+    }
+    int c2 = 0;
+    for (int k = nl - 1; k >= 0 && c2 == 0; --k) c2 = (magv[k] > p.maxint[k]) - (magv[k] < p.maxint[k]);
+    if (c2 > 0) st = ST_OVERFLOW;
+    neg = true;
+  }
+  double val = 0.0;
+  int64_t mant = 0;
+  if (st == ST_OK) {
+    int top = nl - 1;
+    while (top > 0 && magv[top] == 0) --top;
+    const int B = (magv[top] == 0) ? 0 : top * LB + (32 - __clz(magv[top]));   // bit length
+    const int lo_bit = B > 64 ? B - 64 : 0;
+    uint64_t hi64 = 0;
+    bool sticky = false;
+    for (int k = top; k >= 0; --k) {
+      const uint64_t v = magv[k];
+      if (!v) continue;
+      const int kb = k * LB;
+      if (kb + LB <= lo_bit) { sticky = true; continue; }
+      const int sh = kb - lo_bit;
+      if (sh >= 0) {
+        hi64 |= v << sh;
+      } else {
+        hi64 |= v >> (-sh);
+        if (v & ((1ull << (-sh)) - 1ull)) sticky = true;
+      }
+    }
+    double d;
+    if (B <= 53) {
+      d = (double)hi64;
+    } else {
+      const int drop = (B > 64 ? 64 : B) - 53;
+      uint64_t keep = hi64 >> drop;
+      const uint64_t rem = hi64 & ((1ull << drop) - 1ull);
+      const uint64_t half = 1ull << (drop - 1);
+      if (rem > half || (rem == half && (sticky || (keep & 1ull)))) keep += 1;
+      d = ldexp((double)keep, lo_bit + drop);
+    }
+    if (e > 0) {
+      if (isinf(d) || B > 1024) st = ST_FLOAT_OVF;
+      else val = (neg ? -d : d) * ldexp(1.0, -4 * e);
+    } else {
+      val = ldexp(neg ? -d : d, -4 * e);
+      const int sh = -4 * e;
+      if (B + sh <= 63) {
+        const int64_t mm = (int64_t)(hi64 << sh);
+        mant = neg ? -mm : mm;
+        st = ST_INT;
+      } else {
+        st = ST_INT_BIG;
+      }
+    }
+  }
+  p.val[ii] = val;
+  if (p.mant) p.mant[ii] = mant;
+  p.status[ii] = st;
+}
+
+template <int TPI>
+__global__ __launch_bounds__(BLOCK) void k_decrypt(DecParams p) {
+  constexpr int S = TPI * L;
+  constexpr int EPB = BLOCK / (2 * TPI);     // elements per block
+  constexpr int SLOT = 4 * S;                // [c: 2S limbs][B_p: S][B_q: S]; [0,2S) reused later
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int tig = threadIdx.x % TPI;
+  const int h = (threadIdx.x / TPI) & 1;
+  const int eib = threadIdx.x / (2 * TPI);
+  const int pair_lane = threadIdx.x % (2 * TPI);
+  uint32_t* eslot = smem + eib * SLOT;
+  uint32_t* bslot = eslot + 2 * S + h * S;   // this half's multiplicand
+  const DecHalf* H = p.halves + h;
+  const DecHalf* H0 = p.halves;
+  uint32_t m[L];
+  load_limbs_g<TPI>(H->m, m, tig);
+  const uint32_t mprime = H->mprime;
+  uint32_t* table = p.scratch + ((size_t)(blockIdx.x * EPB + eib) * 2 + h) * TABLE_FIX * S;
+
+  for (long long base = (long long)blockIdx.x * EPB; base < p.n; base += (long long)gridDim.x * EPB) {
+    const long long inst = base + eib;
+    const bool valid = inst < p.n;
+    const long long ii = valid ? inst : p.n - 1;
+
+    // 1. ciphertext (2*nb bits) -> 2S limbs in the element's shared region
+    {
+      const uint32_t* cw = p.ct + ii * p.ct_words;
+      wave_lds_fence();
+      for (int k = pair_lane; k < 2 * S; k += 2 * TPI) {
+        const int bit = k * LB, wi = bit >> 5, sh = bit & 31;
+        const uint64_t lo = wi < p.ct_words ? (uint64_t)cw[wi] : 0ull;
+        const uint64_t hi = wi + 1 < p.ct_words ? (uint64_t)cw[wi + 1] : 0ull;
+        eslot[k] = (uint32_t)(((hi << 32) | lo) >> sh) & LMASK;
+      }
+      wave_lds_fence();
+    }
+    // 2. x~ = c * R mod p^2: 2S-iteration Montgomery pass with A = R^3 mod p^2, B = c
+    uint32_t xt[L], acc[L], t[L];
+    load_limbs_g<TPI>(H->R3, t, tig);
+    montmul<TPI>(xt, t, eslot, 2 * TPI, m, mprime, lane, tig);
+    // 3. fixed-window table x~^0 .. x~^31 (global scratch)
+    load_limbs_g<TPI>(H->one, t, tig);
+    store_limbs_g<TPI>(table, t, tig);
+    store_limbs_g<TPI>(table + S, xt, tig);
+    write_limbs_lds<TPI>(bslot, xt, tig);
+#pragma unroll
+    for (int i = 0; i < L; ++i) t[i] = xt[i];
+    for (int k = 2; k < TABLE_FIX; ++k) {
+      montmul<TPI>(t, t, bslot, TPI, m, mprime, lane, tig);
+      store_limbs_g<TPI>(table + k * S, t, tig);
+    }
+    // 4. left-to-right fixed windows over p-1 (resp. q-1): identical trip counts in both halves
+    load_limbs_g<TPI>(table + H->digits[0] * S, acc, tig);
+    for (int w = 1; w < p.nwin; ++w) {
+#pragma unroll 1
+      for (int s = 0; s < 5; ++s) {
+        write_limbs_lds<TPI>(bslot, acc, tig);
+        montmul<TPI>(acc, acc, bslot, TPI, m, mprime, lane, tig);
+      }
+      write_limbs_lds<TPI>(bslot, acc, tig);
+      load_limbs_g<TPI>(table + H->digits[w] * S, t, tig);
+      montmul<TPI>(acc, t, bslot, TPI, m, mprime, lane, tig);
+    }
+    // 5. leave the Montgomery domain: x_h = c^(p_h - 1) mod p_h^2, canonical
+    write_one_lds<TPI>(bslot, tig);
+    montmul<TPI>(acc, acc, bslot, TPI, m, mprime, lane, tig);
+    cond_sub<TPI>(acc, m, lane, tig);
+    // 6. L_h = (x_h - 1) / p_h exactly: Hensel division digits (x - 1 == x + 2^(27S) - 1 mod 2^(27S))
+    uint32_t Ld[L], pl[L];
+    {
+      uint64_t P[L];
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+        P[i] = (uint64_t)acc[i] + LMASK;
+        Ld[i] = 0;
+      }
+      load_limbs_g<TPI>(H->pneg, pl, tig);
+      uint32_t dummy[L];
+      cios<TPI, false, true>(P, dummy, nullptr, TPI, pl, H->dprime, tig, Ld);
+    }
+    // 7. m_h = L_h * h_h mod p_h (hR = h_h * R mod p_h)
+    load_limbs_g<TPI>(H->ph, pl, tig);
+    copy_g_to_lds<TPI>(bslot, H->hR, tig);
+    uint32_t mh[L];
+    montmul<TPI>(mh, Ld, bslot, TPI, pl, H->pprime, lane, tig);
+    cond_sub<TPI>(mh, pl, lane, tig);
+    // 8. CRT (both halves compute, the p-half's result is kept):
+    //    u = (mp*qinv - mq*qinv) mod p ; x = mq + u*q      (gmpy_math.py:31-40)
+    write_limbs_lds<TPI>(eslot + h * S, mh, tig);     // region 0: mp, region 1: mq
+    uint32_t mp[L], mq[L];
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      mp[i] = eslot[tig * L + i];
+      mq[i] = eslot[S + tig * L + i];
+    }
+    wave_lds_fence();
+    uint32_t p0[L], a1[L], a2[L], u[L];
+    load_limbs_g<TPI>(H0->ph, p0, tig);
+    copy_g_to_lds<TPI>(bslot, p.qinvR, tig);
+    montmul<TPI>(a1, mp, bslot, TPI, p0, H0->pprime, lane, tig);
+    cond_sub<TPI>(a1, p0, lane, tig);
+    montmul<TPI>(a2, mq, bslot, TPI, p0, H0->pprime, lane, tig);
+    cond_sub<TPI>(a2, p0, lane, tig);
+    {
+      const bool neg = sub_limbs<TPI>(a1, a2, u, lane, tig);
+      uint64_t P[L];
+#pragma unroll
+      for (int i = 0; i < L; ++i) P[i] = (uint64_t)u[i] + (neg ? p0[i] : 0u);
+      normalize<TPI>(P, u, lane, tig);              // (mp - mq) qinv mod p, in [0, p)
+    }
+    uint32_t nlm[L], uq[L], x[L];
+    load_limbs_g<TPI>(p.nlimb, nlm, tig);
+    copy_g_to_lds<TPI>(bslot, p.qRn, tig);
+    montmul<TPI>(uq, u, bslot, TPI, nlm, p.nprime, lane, tig);   // u * q mod n
+    cond_sub<TPI>(uq, nlm, lane, tig);
+    {
+      uint64_t P[L];
+#pragma unroll
+      for (int i = 0; i < L; ++i) P[i] = (uint64_t)uq[i] + mq[i];
+      normalize<TPI>(P, x, lane, tig);
+    }
+    // 9. outputs from the p-half: raw plaintext words and the decoded value
+    write_limbs_lds_if<TPI>(eslot, x, tig, h == 0);
+    if (valid && h == 0 && p.raw) {
+      for (int j = tig; j < p.pt_words; j += TPI) p.raw[ii * p.pt_words + j] = limbs_word(eslot, S, j);
+    }
+    if (valid && h == 0 && tig == 0) decode_element(eslot, p, ii);
+    wave_lds_fence();
+  }
+}
+
+}  // namespace fpai
+
+namespace fpai {
+// Debug/unit-test kernel for the group engine (used by tests/test_gpu_engine.py only).
+// op 0: a*b*R^-1 mod N (< 2N) | 1: a -> limbs -> words | 2: c0(M = int64 from a[0..1])
+// op 3: MontMul(MontMul(a, R2), 1) | 4: a^n mod N via the sliding-window modexp
+// op 5: cond_sub(a, N) | 6: sub_limbs(a, b) (wrapped) | 7: normalize(a + b)
+struct DbgParams {
+  int op;
+  const uint32_t* a;
+  const uint32_t* b;
+  uint32_t* out;
+  int32_t* flag;
+  long long n;
+  int words;
+  const uint32_t* N;
+  const uint32_t* R2;
+  const uint32_t* nl;
+  uint32_t mprime;
+  const uint16_t* sched;
+  int nsched, first;
+  uint32_t* scratch;
+};
+
+template <int TPI>
+__global__ __launch_bounds__(BLOCK) void k_debug(DbgParams p) {
+  constexpr int S = TPI * L;
+  constexpr int GPB = BLOCK / TPI;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int tig = threadIdx.x % TPI;
+  const int gib = threadIdx.x / TPI;
+  uint32_t* slot = smem + gib * S;
+  uint32_t m[L];
+  load_limbs_g<TPI>(p.N, m, tig);
+  const long long inst = (long long)blockIdx.x * GPB + gib;
+  const bool valid = inst < p.n;
+  const long long ii = valid ? inst : p.n - 1;
+  uint32_t a[L], b[L], r[L];
+  words_to_limbs(p.a + ii * p.words, p.words, a, tig);
+  words_to_limbs(p.b + ii * p.words, p.words, b, tig);
+  int flag = 0;
+  if (p.op == 0) {
+    write_limbs_lds<TPI>(slot, b, tig);
+    montmul<TPI>(r, a, slot, TPI, m, p.mprime, lane, tig);
+  } else if (p.op == 1) {
+#pragma unroll
+    for (int i = 0; i < L; ++i) r[i] = a[i];
+  } else if (p.op == 2) {
+    const int64_t M = (int64_t)(((uint64_t)p.a[ii * p.words + 1] << 32) | p.a[ii * p.words]);
+    make_c0<TPI>(M, p.nl, m, r, lane, tig);
+  } else if (p.op == 3) {
+    uint32_t t[L];
+    copy_g_to_lds<TPI>(slot, p.R2, tig);
+    montmul<TPI>(t, a, slot, TPI, m, p.mprime, lane, tig);
+    write_one_lds<TPI>(slot, tig);
+    montmul<TPI>(r, t, slot, TPI, m, p.mprime, lane, tig);
+  } else if (p.op == 4) {
+    uint32_t t[L], acc[L];
+    uint32_t* table = p.scratch + (size_t)(blockIdx.x * GPB + gib) * TABLE_ODD * S;
+    copy_g_to_lds<TPI>(slot, p.R2, tig);
+    montmul<TPI>(t, a, slot, TPI, m, p.mprime, lane, tig);
+    modexp_sliding<TPI>(acc, t, slot, table, p.sched, p.nsched, p.first, m, p.mprime, lane, tig);
+    write_one_lds<TPI>(slot, tig);
+    montmul<TPI>(r, acc, slot, TPI, m, p.mprime, lane, tig);
+    cond_sub<TPI>(r, m, lane, tig);
+  } else if (p.op == 5) {
+#pragma unroll
+    for (int i = 0; i < L; ++i) r[i] = a[i];
+    cond_sub<TPI>(r, m, lane, tig);
+  } else if (p.op == 6) {
+    flag = sub_limbs<TPI>(a, b, r, lane, tig) ? 1 : 0;
+  } else {
+    uint64_t P[L];
+#pragma unroll
+    for (int i = 0; i < L; ++i) P[i] = (uint64_t)a[i] + b[i];
+    normalize<TPI>(P, r, lane, tig);
+  }
+  emit_words<TPI>(slot, r, p.out + ii * p.words, p.words, valid, tig);
+  if (valid && tig == 0) p.flag[ii] = flag;
+}
+}  // namespace fpai

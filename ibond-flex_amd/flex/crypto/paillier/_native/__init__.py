@@ -1,0 +1,186 @@
+"""ctypes binding of libflexpai.so, the MI355X Paillier engine (C ABI: include/flexpai.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (hipcc --offload-arch=gfx950)
+and is REQUIRED: there is no CPU fallback. Loading fails loudly if it is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libflexpai.so")
+
+PAI_F32, PAI_F64, PAI_I64 = 0, 1, 2
+PAI_OBF_NONE, PAI_OBF_GIVEN, PAI_OBF_RNG = 0, 1, 2
+PAI_EXP_AUTO, PAI_EXP_FIXED = 0, 1
+EL_OK, EL_INT, EL_INT_BIG, EL_OVERFLOW, EL_FLOAT_OVF, EL_ENC_RANGE = 0, 1, 2, 3, 4, 5
+
+EXPORTED = ("pai_ctx_create", "pai_ctx_set_private", "pai_ctx_destroy", "pai_ctx_info", "pai_last_error",
+            "pai_encrypt", "pai_add", "pai_decrypt", "pai_encrypt_dev", "pai_add_dev", "pai_decrypt_dev")
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libflexpai.so and declare the C signatures. Raises if the library is absent."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise NativeError(f"flexpai native library not found at {path}; run __graft_entry__.build() "
+                              f"(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        lib = ctypes.CDLL(path)
+        P, S, I, U64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+        lib.pai_ctx_create.argtypes = [P, S, I, ctypes.POINTER(ctypes.c_void_p)]
+        lib.pai_ctx_set_private.argtypes = [P, P, P, S]
+        lib.pai_ctx_destroy.argtypes = [P]
+        lib.pai_ctx_destroy.restype = None
+        lib.pai_ctx_info.argtypes = [P, P, P, P]
+        lib.pai_last_error.restype = ctypes.c_char_p
+        lib.pai_encrypt.argtypes = [P, I, P, S, I, ctypes.c_int32, I, P, S, S, P, U64, P, P, P]
+        lib.pai_add.argtypes = [P, P, P, I, S, P, P]
+        lib.pai_decrypt.argtypes = [P, P, P, S, P, P, P, P]
+        lib.pai_encrypt_dev.argtypes = [P, I, P, S, I, ctypes.c_int32, I, P, S, S, P, U64, P, P, P, P]
+        lib.pai_add_dev.argtypes = [P, P, P, I, S, P, P, P]
+        lib.pai_decrypt_dev.argtypes = [P, P, P, S, P, P, P, P, P]
+        for name in EXPORTED:
+            if name not in ("pai_ctx_destroy", "pai_last_error"):
+                getattr(lib, name).restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        msg = load_library().pai_last_error().decode(errors="replace")
+        if rc == -4 and "does not match" in msg or "have to be different" in msg:
+            raise ValueError(msg)
+        raise NativeError(f"flexpai error {rc}: {msg}")
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def int_to_le(v: int, nbytes: int) -> bytes:
+    return int(v).to_bytes(nbytes, "little")
+
+
+class Context:
+    """One key on one GPU. Created lazily by the Python layer (never pickled, never forked)."""
+
+    def __init__(self, n: int, device: int = 0, p: Optional[int] = None, q: Optional[int] = None):
+        self.lib = load_library()
+        self.n = n
+        nbytes = (n.bit_length() + 7) // 8
+        buf = int_to_le(n, nbytes)
+        h = ctypes.c_void_p()
+        _check(self.lib.pai_ctx_create(buf, nbytes, device, ctypes.byref(h)))
+        self._h = h
+        kb, cw, pw = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(self.lib.pai_ctx_info(h, ctypes.byref(kb), ctypes.byref(cw), ctypes.byref(pw)))
+        self.key_bits, self.ct_words, self.pt_words = kb.value, cw.value, pw.value
+        self.has_private = False
+        if p is not None:
+            self.set_private(p, q)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_private(self, p: int, q: int):
+        hb = max(p.bit_length(), q.bit_length()) // 8 + 1
+        _check(self.lib.pai_ctx_set_private(self._h, int_to_le(p, hb), int_to_le(q, hb), hb))
+        self.has_private = True
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.pai_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ----------------------------------------------------------------- host-buffer ops
+    def encrypt(self, x: np.ndarray, exp_mode: int = PAI_EXP_AUTO, fixed_exp: int = 0,
+                obf_mode: int = PAI_OBF_RNG, r: Optional[Sequence[int]] = None, r_scalar: Optional[int] = None,
+                rng_key: Optional[bytes] = None, index_base: int = 0) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        x = np.ascontiguousarray(x)
+        if x.dtype == np.float32:
+            dt = PAI_F32
+        elif x.dtype == np.float64:
+            dt = PAI_F64
+        elif x.dtype == np.int64:
+            dt = PAI_I64
+        else:
+            raise TypeError(f"unsupported dtype {x.dtype}")
+        N = x.size
+        ct = np.empty((N, self.ct_words), dtype=np.uint32)
+        ex = np.empty(N, dtype=np.int32)
+        st = np.empty(N, dtype=np.int32)
+        r_buf, r_stride, r_bytes = None, 0, 0
+        if obf_mode == PAI_OBF_GIVEN:
+            r_bytes = self.ct_words * 4
+            if r_scalar is not None:
+                r_buf = np.frombuffer(int_to_le(r_scalar, r_bytes), dtype=np.uint8).copy()
+                r_stride = 0
+            else:
+                r_buf = np.frombuffer(b"".join(int_to_le(v, r_bytes) for v in r), dtype=np.uint8).copy()
+                r_stride = r_bytes
+        key = rng_key if rng_key is not None else os.urandom(32)
+        _check(self.lib.pai_encrypt(self._h, dt, _ptr(x), N, exp_mode, fixed_exp, obf_mode,
+                                    _ptr(r_buf) if r_buf is not None else None, r_stride, r_bytes,
+                                    key, index_base, _ptr(ct), _ptr(ex), _ptr(st)))
+        return ct, ex, st
+
+    def add(self, cts: Sequence[np.ndarray], exps: Sequence[np.ndarray]) -> Tuple[np.ndarray, np.ndarray]:
+        k = len(cts)
+        cts = [np.ascontiguousarray(c, dtype=np.uint32) for c in cts]
+        exps = [np.ascontiguousarray(e, dtype=np.int32) for e in exps]
+        N = exps[0].size
+        ct_ptrs = (ctypes.c_void_p * k)(*[_ptr(c) for c in cts])
+        ex_ptrs = (ctypes.c_void_p * k)(*[_ptr(e) for e in exps])
+        out = np.empty((N, self.ct_words), dtype=np.uint32)
+        oe = np.empty(N, dtype=np.int32)
+        _check(self.lib.pai_add(self._h, ct_ptrs, ex_ptrs, k, N, _ptr(out), _ptr(oe)))
+        return out, oe
+
+    def decrypt(self, ct: np.ndarray, exp: np.ndarray, want_raw: bool = False):
+        ct = np.ascontiguousarray(ct, dtype=np.uint32)
+        exp = np.ascontiguousarray(exp, dtype=np.int32)
+        N = exp.size
+        val = np.empty(N, dtype=np.float64)
+        mant = np.empty(N, dtype=np.int64)
+        st = np.empty(N, dtype=np.int32)
+        raw = np.empty((N, self.pt_words), dtype=np.uint32) if want_raw else None
+        _check(self.lib.pai_decrypt(self._h, _ptr(ct), _ptr(exp), N, _ptr(val), _ptr(mant), _ptr(st),
+                                    _ptr(raw) if raw is not None else None))
+        return val, mant, st, raw
+
+
+def words_to_ints(words: np.ndarray):
+    """[N, W] little-endian uint32 words -> list of Python ints (zero-copy bytes view)."""
+    w = np.ascontiguousarray(words, dtype="<u4")
+    b = w.tobytes()
+    step = w.shape[1] * 4
+    return [int.from_bytes(b[i * step:(i + 1) * step], "little") for i in range(w.shape[0])]
+
+
+def ints_to_words(vals, nwords: int) -> np.ndarray:
+    nbytes = nwords * 4
+    buf = b"".join(int(v).to_bytes(nbytes, "little") for v in vals)
+    return np.frombuffer(buf, dtype="<u4").reshape(len(vals), nwords).copy()

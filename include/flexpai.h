@@ -1,0 +1,110 @@
+/*
+ * flexpai — MI355X-native Paillier array engine, C ABI.
+ *
+ * Drop-in boundary for tongdun/iBond-flex `flex.crypto.paillier` (Python). Each entry point
+ * replaces the per-element gmpy2 work that the reference does on the CPU:
+ *
+ *   pai_ctx_create        <- PaillierPublicKey(n)                  flex/crypto/paillier/keypair.py:20-39
+ *   pai_ctx_set_private   <- PaillierPrivateKey(pk, p, q)          flex/crypto/paillier/keypair.py:42-90
+ *   pai_encrypt[_dev]     <- PaillierEncryptor.encrypt(ndarray)    flex/crypto/paillier/encryptor.py:71-114
+ *                            (FixedPointNumber.encode fixedpoint_number.py:46-90, raw_encrypt
+ *                             raw_encrypt.py:22-49, apply_obfuscation obfuscator.py:23-37 ->
+ *                             gmpy_math.powmod/mulmod gmpy_math.py:43-63)
+ *   pai_add[_dev]         <- sum of PaillierEncryptedNumber arrays encrypted_number.py:65-69,
+ *                            115-137, 166-185 (k-way, order independent)
+ *   pai_decrypt[_dev]     <- PaillierDecryptor.decrypt(ndarray)    flex/crypto/paillier/decryptor.py:33-127
+ *                            (+ FixedPointNumber.decode fixedpoint_number.py:92-107)
+ *
+ * Conventions
+ *   - Integers cross the boundary as little-endian bytes (key material) or little-endian 32-bit
+ *     words, one ciphertext contiguous (AoS): ciphertext i occupies words [i*W, (i+1)*W) with
+ *     W = pai_ct_words(ctx) = 2*key_bits/32. This is zero-copy with Python int.to_bytes(...,'little').
+ *   - Host-buffer entry points are synchronous and never retain caller memory.
+ *   - *_dev entry points take device pointers and a hipStream_t (as void*) and are asynchronous.
+ *   - Return value 0 = success; negative = error, message in pai_last_error() (thread local).
+ *   - Per-element outcomes are reported in an int32 status array (PAI_EL_*), mapped by the Python
+ *     layer onto the reference's exceptions.
+ */
+#ifndef FLEXPAI_H
+#define FLEXPAI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pai_ctx pai_ctx;
+
+/* return codes */
+#define PAI_OK 0
+#define PAI_ERR_ARG (-1)
+#define PAI_ERR_HIP (-2)
+#define PAI_ERR_NOPRIV (-3)
+#define PAI_ERR_KEY (-4)
+
+/* input dtypes for pai_encrypt */
+#define PAI_F32 0
+#define PAI_F64 1
+#define PAI_I64 2
+
+/* obfuscation modes (SURVEY.md §8b randomness contract) */
+#define PAI_OBF_NONE 0   /* random_value == 0 : c = 1 + n*m                      (encryptor.py:61-67) */
+#define PAI_OBF_GIVEN 1  /* explicit r per element (r_stride 0 = one r for all)  (obfuscator.py:35)  */
+#define PAI_OBF_RNG 2    /* device ChaCha20 CSPRNG keyed by rng_key, nonce = global element index    */
+
+/* exponent modes for encode (fixedpoint_number.py:63-82) */
+#define PAI_EXP_AUTO 0   /* precision=None: exponent from frexp / 0 for ints */
+#define PAI_EXP_FIXED 1  /* precision given: exponent = fixed_exp for every element */
+
+/* per-element status */
+#define PAI_EL_OK 0           /* float result in val_out                                            */
+#define PAI_EL_INT 1          /* exponent <= 0: exact integer mant_out * 16^(-exp) (fits int64)      */
+#define PAI_EL_INT_BIG 2      /* exponent <= 0 and the mantissa does not fit int64 (use raw_out)     */
+#define PAI_EL_OVERFLOW 3     /* OverflowError('Overflow detected in decode number')  :104-105     */
+#define PAI_EL_FLOAT_OVF 4    /* OverflowError: int too large to convert to float (e > 0)           */
+#define PAI_EL_ENC_RANGE 5    /* encode ValueError (fixedpoint_number.py:86-88) / beyond int64      */
+
+int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** out);
+int pai_ctx_set_private(pai_ctx* ctx, const uint8_t* p_le, const uint8_t* q_le, size_t half_bytes);
+void pai_ctx_destroy(pai_ctx* ctx);
+/* key bits, 32-bit words per ciphertext (2*key_bits/32), words per plaintext (key_bits/32) */
+int pai_ctx_info(const pai_ctx* ctx, int* key_bits, int* ct_words, int* pt_words);
+const char* pai_last_error(void);
+
+/* Encrypt N plaintexts. dtype PAI_F32/F64/I64. obf_mode PAI_OBF_*.
+ *   r_le:      PAI_OBF_GIVEN only: r values as little-endian byte strings of r_bytes each, element i
+ *              at r_le + i*r_stride_bytes (stride 0 = the same r for every element). 1 <= r < n^2.
+ *   rng_key32: PAI_OBF_RNG only: 32-byte ChaCha20 key; element i uses nonce (index_base + i).
+ * Outputs: ct_out N*W words, exp_out N exponents, status_out N statuses (nullable).           */
+int pai_encrypt(pai_ctx* ctx, int dtype, const void* x, size_t N, int exp_mode, int32_t fixed_exp,
+                int obf_mode, const uint8_t* r_le, size_t r_stride_bytes, size_t r_bytes,
+                const uint8_t* rng_key32, uint64_t index_base,
+                uint32_t* ct_out, int32_t* exp_out, int32_t* status_out);
+
+/* k-way homomorphic add: out_i = prod_j ct_j,i^(16^(E_i - e_j,i)) mod n^2, E_i = max_j e_j,i. */
+int pai_add(pai_ctx* ctx, const uint32_t* const* cts, const int32_t* const* exps, int k, size_t N,
+            uint32_t* ct_out, int32_t* exp_out);
+
+/* Decrypt + decode. val_out: float64 value (status OK/INT), mant_out: signed mantissa when it
+ * fits int64 (nullable), status_out (required), raw_out: N * pt_words canonical plaintexts
+ * m = D(c) in [0, n) (nullable).                                                              */
+int pai_decrypt(pai_ctx* ctx, const uint32_t* ct, const int32_t* exp, size_t N, double* val_out,
+                int64_t* mant_out, int32_t* status_out, uint32_t* raw_out);
+
+/* Device-resident variants (device pointers, asynchronous on `stream`, a hipStream_t). */
+int pai_encrypt_dev(pai_ctx* ctx, int dtype, const void* d_x, size_t N, int exp_mode, int32_t fixed_exp,
+                    int obf_mode, const uint32_t* d_r_words, size_t r_stride_words, size_t r_words,
+                    const uint8_t* rng_key32, uint64_t index_base,
+                    uint32_t* d_ct, int32_t* d_exp, int32_t* d_status, void* stream);
+/* d_cts: k consecutive [N][W] ciphertext arrays; d_exps: k consecutive [N] exponent arrays. */
+int pai_add_dev(pai_ctx* ctx, const uint32_t* d_cts, const int32_t* d_exps, int k, size_t N,
+                uint32_t* d_out, int32_t* d_exp_out, void* stream);
+int pai_decrypt_dev(pai_ctx* ctx, const uint32_t* d_ct, const int32_t* d_exp, size_t N, double* d_val,
+                    int64_t* d_mant, int32_t* d_status, uint32_t* d_raw, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLEXPAI_H */

@@ -1,0 +1,89 @@
+"""Host-side big-integer helpers for one-time key setup (keygen) and for the scalar object
+operators. Restates flex/crypto/gmpy_math.py:27-93 on Python ints (no gmpy2 dependency).
+Array paths never use these: they go to the GPU through _runtime.py."""
+from __future__ import annotations
+
+import random
+
+POWMOD_GMP_SIZE = 1 << 64
+
+_SMALL_PRIMES = [p for p in range(3, 2000) if all(p % d for d in range(2, int(p ** 0.5) + 1))]
+
+
+def mul(a: int, b: int) -> int:                      # gmpy_math.py:27-28
+    return a * b
+
+
+def crt(mp: int, mq: int, p: int, q: int, q_inverse: int, n: int) -> int:   # gmpy_math.py:31-40
+    u = (mp - mq) * q_inverse % p
+    return (mq + u * q) % n
+
+
+def mulmod(a: int, b: int, c: int) -> int:           # gmpy_math.py:43-48
+    return a * b % c
+
+
+def powmod(a: int, b: int, c: int) -> int:           # gmpy_math.py:51-63
+    if a == 1:
+        return 1
+    return pow(a, b, c)
+
+
+def invert(a: int, b: int) -> int:                   # gmpy_math.py:66-74
+    try:
+        x = pow(a, -1, b)
+    except ValueError:
+        x = 0
+    if x == 0:
+        raise ZeroDivisionError('invert(a, b) no inverse exists')
+    return x
+
+
+def is_probable_prime(x: int) -> bool:
+    if x < 2:
+        return False
+    for p in _SMALL_PRIMES:
+        if x % p == 0:
+            return x == p
+    d, s = x - 1, 0
+    while d % 2 == 0:
+        d //= 2
+        s += 1
+    for a in _SMALL_PRIMES[:40]:
+        y = pow(a, d, x)
+        if y == 1 or y == x - 1:
+            continue
+        for _ in range(s - 1):
+            y = y * y % x
+            if y == x - 1:
+                break
+        else:
+            return False
+    return True
+
+
+def next_prime(x: int) -> int:
+    """gmpy2.next_prime: the smallest (probable) prime strictly greater than x."""
+    c = x + 1
+    if c <= 2:
+        return 2
+    if c % 2 == 0:
+        c += 1
+    while not is_probable_prime(c):
+        c += 2
+    return c
+
+
+def getprimeover(n: int, seed=None) -> int:          # gmpy_math.py:77-87
+    if not seed:
+        r = random.SystemRandom().getrandbits(n)
+    else:
+        random.seed(seed)
+        r = random.getrandbits(n)
+    r |= 1 << (n - 1)
+    return next_prime(r)
+
+
+def isqrt(n: int) -> int:                            # gmpy_math.py:90-93
+    import math
+    return math.isqrt(n)

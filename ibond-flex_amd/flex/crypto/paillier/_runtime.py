@@ -1,0 +1,50 @@
+"""Process-local GPU runtime for the Paillier package: one native context per (key, device,
+process). Contexts are created lazily, never pickled and never shared across a fork (a forked
+child builds its own), so PaillierEncryptor/PaillierDecryptor stay picklable exactly like the
+reference's (encryptor.py / decryptor.py are sent to peers, e.g. he_otp_lr_ft1/train.py:70).
+
+Device selection: $FLEXPAI_DEVICE, else $LOCAL_RANK, else 0.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from typing import Dict, Tuple
+
+import numpy as np
+
+from . import _native
+
+_lock = threading.Lock()
+_ctxs: Dict[Tuple[int, int, int], "_native.Context"] = {}
+
+
+def device_index() -> int:
+    for var in ("FLEXPAI_DEVICE", "LOCAL_RANK"):
+        v = os.environ.get(var)
+        if v is not None and v.strip() != "":
+            return int(v)
+    return 0
+
+
+def context(public_key, private_key=None) -> "_native.Context":
+    """The native context of `public_key` on this process's device (private part attached when
+    `private_key` is given)."""
+    dev = device_index()
+    k = (public_key.n, dev, os.getpid())
+    with _lock:
+        ctx = _ctxs.get(k)
+        if ctx is None:
+            ctx = _native.Context(public_key.n, dev)
+            _ctxs[k] = ctx
+        if private_key is not None and not ctx.has_private:
+            ctx.set_private(private_key.p, private_key.q)
+    return ctx
+
+
+def ints_to_words(vals, nwords: int) -> np.ndarray:
+    return _native.ints_to_words(vals, nwords)
+
+
+def words_to_ints(words: np.ndarray):
+    return _native.words_to_ints(words)

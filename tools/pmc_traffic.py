@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE counter CSVs (separate passes) into per-launch HBM
+bytes for one kernel, with the gfx950 correction of MI355X_MICROARCH.md §HBM: FETCH_SIZE reads
+half of the bytes of a wide coalesced stream (so it is doubled); WRITE_SIZE is taken as is. Both are
+in KiB. Writes profiles/pmc_encrypt_latest.json, which bench.py reports as roofline.traffic.
+
+    python tools/pmc_traffic.py FETCH.csv WRITE.csv --kernel k_encrypt --n 1048576 --nb 2048 [-o out.json]
+"""
+import argparse
+import csv
+import json
+import os
+import statistics
+
+
+def per_launch(path, counter, kernel):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]]
+    if not vals:
+        raise SystemExit(f"no {counter} rows for {kernel} in {path}")
+    return statistics.mean(vals), len(vals)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_csv")
+    ap.add_argument("write_csv")
+    ap.add_argument("--kernel", default="k_encrypt")
+    ap.add_argument("--n", type=int, required=True)
+    ap.add_argument("--nb", type=int, required=True)
+    ap.add_argument("-o", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                               "profiles", "pmc_encrypt_latest.json"))
+    a = ap.parse_args()
+    f, nf = per_launch(a.fetch_csv, "FETCH_SIZE", a.kernel)
+    w, nw = per_launch(a.write_csv, "WRITE_SIZE", a.kernel)
+    out = {"kernel": a.kernel, "n": a.n, "nb": a.nb,
+           "fetch_size_kib_raw": f, "write_size_kib_raw": w, "launches": [nf, nw],
+           "hbm_read_bytes_per_launch": 2 * f * 1024, "hbm_write_bytes_per_launch": w * 1024,
+           "hbm_bytes_per_launch": (2 * f + w) * 1024,
+           "correction": "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads), WRITE_SIZE x1; KiB -> bytes"}
+    with open(a.o, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

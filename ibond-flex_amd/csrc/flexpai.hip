@@ -32,8 +32,9 @@ struct pai_ctx {
   HBig n, N;
   uint32_t mprime_N = 0;
   uint32_t *d_N = nullptr, *d_R2 = nullptr, *d_nl = nullptr;
-  uint16_t* d_sched = nullptr;
-  int nsched = 0, first = 0;
+  uint32_t* d_prog = nullptr;   // Montgomery program for x^n (run_program, kernels.hpp)
+  int nprog = 0;
+  uint32_t* d_oneR = nullptr;   // R mod n^2
   // private key material
   bool has_priv = false;
   DecHalf* d_halves = nullptr;
@@ -62,9 +63,9 @@ static int upload(pai_ctx* c, const std::vector<T>& v, T** out) {
   return 0;
 }
 
-static int tpi_for_bits(size_t need_bits) {
-  for (int t : {2, 4, 8, 16})
-    if ((size_t)27 * 19 * t >= need_bits) return t;
+static int tpi_for_bits(size_t need_bits, int min_tpi) {
+  for (int t : {1, 2, 4, 8})
+    if (t >= min_tpi && (size_t)LB * L * t >= need_bits) return t;
   return 0;
 }
 
@@ -101,6 +102,36 @@ static void sliding_schedule(const HBig& e, std::vector<uint16_t>& ops, int& fir
     ops.push_back((uint16_t)nsq);
     ops.push_back(0xFFFF);
   }
+}
+
+// Op list for run_program: x~ = x R (the caller puts R^2 in the slot), odd powers x~^(2k+1) into
+// tiles k = 0..15, then the left-to-right sliding-window chain over e. The kernel appends the final
+// product with tile T_FINAL.
+static bool build_modexp_program(const HBig& e, std::vector<uint32_t>& prog) {
+  std::vector<uint16_t> sched;
+  int first = 0;
+  sliding_schedule(e, sched, first);
+  auto op = [](uint32_t flags, int bidx, int aidx, int sidx) {
+    return flags | ((uint32_t)bidx << 8) | ((uint32_t)aidx << 16) | ((uint32_t)sidx << 24);
+  };
+  prog.clear();
+  prog.push_back(op(OP_STORE, 0, 0, 0));                                  // x~ = x R        -> T0
+  prog.push_back(op(OP_B_FROM_A, 0, 0, 0));                               // x~^2
+  prog.push_back(op(OP_B_FROM_A | OP_A_FROM_T | OP_STORE, 0, 0, 1));      // x~^3           -> T1
+  for (int k = 2; k < TABLE_ODD; ++k) prog.push_back(op(OP_STORE, 0, 0, k));   // x~^(2k+1) -> Tk
+  bool loaded = false;   // accumulator still to be taken from tile `first`
+  for (size_t i = 0; i + 1 < sched.size(); i += 2) {
+    const int nsq = sched[i], idx = sched[i + 1];
+    for (int t = 0; t < nsq; ++t) {
+      prog.push_back(loaded ? op(OP_B_FROM_A, 0, 0, 0) : op(OP_B_FROM_T | OP_A_FROM_T, first, first, 0));
+      loaded = true;
+    }
+    if (idx != 0xFFFF) {
+      prog.push_back(loaded ? op(OP_B_FROM_A | OP_A_FROM_T, 0, idx, 0) : op(OP_B_FROM_T | OP_A_FROM_T, first, idx, 0));
+      loaded = true;
+    }
+  }
+  return loaded;   // false only for single-window exponents, which n (odd, >= 64 bits) never is
 }
 
 template <typename K>
@@ -144,25 +175,30 @@ int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** ou
   c->n = n;
   c->nb = (int)n.bits();
   c->N = mul(n, n);
-  c->tpi_e = tpi_for_bits(2 * (size_t)c->nb + 2);
-  c->tpi_d = tpi_for_bits((size_t)c->nb + 3);
+  c->tpi_e = tpi_for_bits(2 * (size_t)c->nb + 2, 2);
+  c->tpi_d = tpi_for_bits((size_t)c->nb + 3, 1);
   if (!c->tpi_e || !c->tpi_d) {
     delete c;
     return fail(PAI_ERR_KEY, "pai_ctx_create: key size not supported (max 4096 bits)");
   }
-  c->S_e = 19 * c->tpi_e;
-  c->S_d = 19 * c->tpi_d;
+  c->S_e = L * c->tpi_e;
+  c->S_d = L * c->tpi_d;
   c->ct_words = (2 * c->nb + 31) / 32;
   c->pt_words = (c->nb + 31) / 32;
-  c->mprime_N = mont_prime27(c->N);
-  const size_t Rbits = (size_t)27 * c->S_e;
+  c->mprime_N = mont_prime(c->N, LB);
+  const size_t Rbits = (size_t)LB * c->S_e;
   HBig R2 = mul_pow2_mod(HBig(1), 2 * Rbits, c->N);
-  std::vector<uint16_t> sched;
-  sliding_schedule(n, sched, c->first);
-  c->nsched = (int)sched.size() / 2;
+  std::vector<uint32_t> prog;
+  if (!build_modexp_program(n, prog)) {
+    delete c;
+    return fail(PAI_ERR_KEY, "pai_ctx_create: degenerate exponent schedule");
+  }
+  c->nprog = (int)prog.size();
+  HBig oneR = mul_pow2_mod(HBig(1), Rbits, c->N);
   int rc;
-  if ((rc = upload(c, c->N.limbs27(c->S_e), &c->d_N)) || (rc = upload(c, R2.limbs27(c->S_e), &c->d_R2)) ||
-      (rc = upload(c, n.limbs27(c->S_e), &c->d_nl)) || (rc = upload(c, sched, &c->d_sched))) {
+  if ((rc = upload(c, c->N.limbs(c->S_e, LB), &c->d_N)) || (rc = upload(c, R2.limbs(c->S_e, LB), &c->d_R2)) ||
+      (rc = upload(c, n.limbs(c->S_e, LB), &c->d_nl)) || (rc = upload(c, prog, &c->d_prog)) ||
+      (rc = upload(c, oneR.limbs(c->S_e, LB), &c->d_oneR))) {
     delete c;
     return rc;
   }
@@ -178,7 +214,7 @@ int pai_ctx_set_private(pai_ctx* c, const uint8_t* p_le, const uint8_t* q_le, si
   if (cmp(p, q) == 0) return fail(PAI_ERR_KEY, "p and q have to be different");
   if (cmp(q, p) < 0) std::swap(p, q);   // keypair.py:57-62
   const int S = c->S_d;
-  const size_t Rbits = (size_t)27 * S;
+  const size_t Rbits = (size_t)LB * S;
   HBig hp, hq;
   {
     HBig qi = inv_mod(q, p), pi = inv_mod(p, q);
@@ -204,25 +240,25 @@ int pai_ctx_set_private(pai_ctx* c, const uint8_t* p_le, const uint8_t* q_le, si
     uint32_t *dm, *dR3, *done, *dpneg, *dph, *dhR;
     uint8_t* ddig;
     HBig pneg = sub(pow2(Rbits), ph);
-    if ((rc = upload(c, m.limbs27(S), &dm)) ||
-        (rc = upload(c, mul_pow2_mod(HBig(1), 3 * Rbits, m).limbs27(S), &dR3)) ||
-        (rc = upload(c, mul_pow2_mod(HBig(1), Rbits, m).limbs27(S), &done)) ||
-        (rc = upload(c, pneg.limbs27(S), &dpneg)) || (rc = upload(c, ph.limbs27(S), &dph)) ||
-        (rc = upload(c, mul_pow2_mod(hs[h], Rbits, ph).limbs27(S), &dhR)) || (rc = upload(c, dig, &ddig)))
+    if ((rc = upload(c, m.limbs(S, LB), &dm)) ||
+        (rc = upload(c, mul_pow2_mod(HBig(1), 3 * Rbits, m).limbs(S, LB), &dR3)) ||
+        (rc = upload(c, mul_pow2_mod(HBig(1), Rbits, m).limbs(S, LB), &done)) ||
+        (rc = upload(c, pneg.limbs(S, LB), &dpneg)) || (rc = upload(c, ph.limbs(S, LB), &dph)) ||
+        (rc = upload(c, mul_pow2_mod(hs[h], Rbits, ph).limbs(S, LB), &dhR)) || (rc = upload(c, dig, &ddig)))
       return rc;
-    hh[h] = DecHalf{dm, dR3, done, dpneg, dph, dhR, ddig, mont_prime27(m), mont_prime27(pneg), mont_prime27(ph), 0u};
+    hh[h] = DecHalf{dm, dR3, done, dpneg, dph, dhR, ddig, mont_prime(m, LB), mont_prime(pneg, LB), mont_prime(ph, LB), 0u};
   }
   std::vector<DecHalf> hv(hh, hh + 2);
   if ((rc = upload(c, hv, &c->d_halves))) return rc;
   HBig qinv = inv_mod(q, p);
   HBig maxint = sub(div_small(c->n, 3), HBig(1));   // keypair.py:29
-  if ((rc = upload(c, mul_pow2_mod(qinv, Rbits, p).limbs27(S), &c->d_qinvR)) ||
-      (rc = upload(c, c->n.limbs27(S), &c->d_nlimb)) ||
-      (rc = upload(c, mul_pow2_mod(mod(q, c->n), Rbits, c->n).limbs27(S), &c->d_qRn)) ||
-      (rc = upload(c, maxint.limbs27(S), &c->d_maxint)))
+  if ((rc = upload(c, mul_pow2_mod(qinv, Rbits, p).limbs(S, LB), &c->d_qinvR)) ||
+      (rc = upload(c, c->n.limbs(S, LB), &c->d_nlimb)) ||
+      (rc = upload(c, mul_pow2_mod(mod(q, c->n), Rbits, c->n).limbs(S, LB), &c->d_qRn)) ||
+      (rc = upload(c, maxint.limbs(S, LB), &c->d_maxint)))
     return rc;
-  c->nprime_d = mont_prime27(c->n);
-  c->n_limbs = (int)((c->n.bits() + 26) / 27);
+  c->nprime_d = mont_prime(c->n, LB);
+  c->n_limbs = (int)((c->n.bits() + LB - 1) / LB);
   c->has_priv = true;
   return 0;
 }
@@ -244,7 +280,7 @@ static int launch_encrypt(pai_ctx* c, EncParams& p, hipStream_t st) {
   constexpr int GPB = BLOCK / TPI;
   const size_t lds = (size_t)GPB * S * 4;
   const int grid = grid_for(c, k_encrypt<TPI>, lds, p.n, GPB);
-  int rc = ensure_scratch(c, (size_t)grid * GPB * TABLE_ODD * S * 4);
+  int rc = ensure_scratch(c, (size_t)grid * BLOCK * TILE_WORDS_PER_LANE * 4);
   if (rc) return rc;
   p.scratch = (uint32_t*)c->d_scratch;
   hipLaunchKernelGGL(k_encrypt<TPI>, dim3(grid), dim3(BLOCK), lds, st, p);
@@ -284,16 +320,14 @@ int pai_encrypt_dev(pai_ctx* c, int dtype, const void* d_x, size_t N, int exp_mo
   p.R2 = c->d_R2;
   p.nl = c->d_nl;
   p.mprime = c->mprime_N;
-  p.sched = c->d_sched;
-  p.nsched = c->nsched;
-  p.first = c->first;
+  p.prog = c->d_prog;
+  p.nprog = c->nprog;
   p.ct_words = c->ct_words;
   hipStream_t st = (hipStream_t)stream;
   switch (c->tpi_e) {
     case 2: return launch_encrypt<2>(c, p, st);
     case 4: return launch_encrypt<4>(c, p, st);
     case 8: return launch_encrypt<8>(c, p, st);
-    case 16: return launch_encrypt<16>(c, p, st);
   }
   return fail(PAI_ERR_KEY, "unsupported group size");
 }
@@ -304,6 +338,9 @@ static int launch_add(pai_ctx* c, AddParams& p, hipStream_t st) {
   constexpr int GPB = BLOCK / TPI;
   const size_t lds = (size_t)GPB * S * 4;
   const int grid = grid_for(c, k_add<TPI>, lds, p.n, GPB);
+  int rc = ensure_scratch(c, (size_t)grid * BLOCK * TILE_WORDS_PER_LANE * 4);
+  if (rc) return rc;
+  p.scratch = (uint32_t*)c->d_scratch;
   hipLaunchKernelGGL(k_add<TPI>, dim3(grid), dim3(BLOCK), lds, st, p);
   HIPCHK(hipGetLastError());
   return 0;
@@ -315,13 +352,13 @@ int pai_add_dev(pai_ctx* c, const uint32_t* d_cts, const int32_t* d_exps, int k,
   if (N == 0) return 0;
   if (k < 1 || !d_cts || !d_exps || !d_out || !d_exp_out) return fail(PAI_ERR_ARG, "pai_add_dev: bad arguments");
   HIPCHK(hipSetDevice(c->device));
-  AddParams p{d_cts, d_exps, k, d_out, d_exp_out, (long long)N, c->d_N, c->d_R2, c->mprime_N, c->ct_words};
+  AddParams p{d_cts, d_exps, k, d_out, d_exp_out, (long long)N, c->d_N, c->d_R2, c->d_oneR, c->mprime_N,
+              c->ct_words, nullptr};
   hipStream_t st = (hipStream_t)stream;
   switch (c->tpi_e) {
     case 2: return launch_add<2>(c, p, st);
     case 4: return launch_add<4>(c, p, st);
     case 8: return launch_add<8>(c, p, st);
-    case 16: return launch_add<16>(c, p, st);
   }
   return fail(PAI_ERR_KEY, "unsupported group size");
 }
@@ -367,10 +404,9 @@ int pai_decrypt_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size
   p.n_limbs = c->n_limbs;
   hipStream_t st = (hipStream_t)stream;
   switch (c->tpi_d) {
+    case 1: return launch_decrypt<1>(c, p, st);
     case 2: return launch_decrypt<2>(c, p, st);
     case 4: return launch_decrypt<4>(c, p, st);
-    case 8: return launch_decrypt<8>(c, p, st);
-    case 16: return launch_decrypt<16>(c, p, st);
   }
   return fail(PAI_ERR_KEY, "unsupported group size");
 }
@@ -493,7 +529,7 @@ static int launch_debug(pai_ctx* c, DbgParams& p) {
   constexpr int GPB = BLOCK / TPI;
   const size_t lds = (size_t)GPB * S * 4;
   const int grid = (int)((p.n + GPB - 1) / GPB);
-  int rc = ensure_scratch(c, (size_t)grid * GPB * TABLE_ODD * S * 4);
+  int rc = ensure_scratch(c, (size_t)grid * BLOCK * TILE_WORDS_PER_LANE * 4);
   if (rc) return rc;
   p.scratch = (uint32_t*)c->d_scratch;
   hipLaunchKernelGGL(k_debug<TPI>, dim3(grid), dim3(BLOCK), lds, (hipStream_t)0, p);
@@ -514,13 +550,12 @@ extern "C" int pai_debug_engine(pai_ctx* c, int op, const uint32_t* a, const uin
   HIPCHK(hipMemcpy(da, a, N * W * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(db, b, N * W * 4, hipMemcpyHostToDevice));
   DbgParams p{op, da, db, dout, dflag, (long long)N, (int)W, c->d_N, c->d_R2, c->d_nl, c->mprime_N,
-              c->d_sched, c->nsched, c->first, nullptr};
+              c->d_prog, c->nprog, nullptr};
   int rc = 0;
   switch (c->tpi_e) {
     case 2: rc = launch_debug<2>(c, p); break;
     case 4: rc = launch_debug<4>(c, p); break;
     case 8: rc = launch_debug<8>(c, p); break;
-    case 16: rc = launch_debug<16>(c, p); break;
   }
   if (rc) return rc;
   HIPCHK(hipDeviceSynchronize());

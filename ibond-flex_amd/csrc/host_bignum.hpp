@@ -36,12 +36,12 @@ struct HBig {
     size_t k = i / 32;
     return k < w.size() ? (int)((w[k] >> (i % 32)) & 1u) : 0;
   }
-  // 27-bit limbs, zero padded to n limbs
-  std::vector<uint32_t> limbs27(size_t n) const {
+  // `lb`-bit limbs (device limb width), zero padded to n limbs
+  std::vector<uint32_t> limbs(size_t n, int lb) const {
     std::vector<uint32_t> out(n, 0);
     for (size_t k = 0; k < n; ++k) {
       uint32_t v = 0;
-      for (int b = 0; b < 27; ++b) v |= (uint32_t)bit(27 * k + b) << b;
+      for (int b = 0; b < lb; ++b) v |= (uint32_t)bit((size_t)lb * k + b) << b;
       out[k] = v;
     }
     return out;
@@ -164,12 +164,12 @@ inline HBig inv_mod(const HBig& a0, const HBig& m) {
   }
   return cmp(u, one) == 0 ? mod(x1, m) : mod(x2, m);
 }
-// -m^{-1} mod 2^27 for odd m
-inline uint32_t mont_prime27(const HBig& m) {
+// -m^{-1} mod 2^lb for odd m
+inline uint32_t mont_prime(const HBig& m, int lb) {
   uint32_t m0 = m.w.empty() ? 1 : m.w[0];
   uint32_t x = 1;
   for (int i = 0; i < 6; ++i) x *= 2u - m0 * x;   // Newton: x = m0^{-1} mod 2^32
-  return (0u - x) & ((1u << 27) - 1u);
+  return (0u - x) & ((1u << lb) - 1u);
 }
 
 }  // namespace fpai

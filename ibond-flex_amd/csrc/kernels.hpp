@@ -23,12 +23,12 @@ struct EncParams {
   int32_t* exp;
   int32_t* status;
   long long n;
-  const uint32_t* N;    // n^2, 27-bit limbs (S)
+  const uint32_t* N;    // n^2, LB-bit limbs (S)
   const uint32_t* R2;   // R^2 mod n^2
   const uint32_t* nl;   // n limbs (S, zero padded)
   uint32_t mprime;
-  const uint16_t* sched;
-  int nsched, first;
+  const uint32_t* prog;  // Montgomery program (run_program)
+  int nprog;
   uint32_t* scratch;
   int ct_words;
 };
@@ -42,17 +42,19 @@ struct AddParams {
   long long n;
   const uint32_t* N;
   const uint32_t* R2;
+  const uint32_t* oneR;   // R mod n^2
   uint32_t mprime;
   int ct_words;
+  uint32_t* scratch;
 };
 
-// Per-half (p: h=0, q: h=1) constants for CRT decryption; all 27-bit limb arrays of S limbs.
+// Per-half (p: h=0, q: h=1) constants for CRT decryption; all LB-bit limb arrays of S limbs.
 // Lives in device memory (indexed per lane by the half a lane works on).
 struct DecHalf {
   const uint32_t* m;      // p^2
   const uint32_t* R3;     // R^3 mod p^2
   const uint32_t* one;    // R mod p^2
-  const uint32_t* pneg;   // 2^(27S) - p
+  const uint32_t* pneg;   // 2^(LB*S) - p
   const uint32_t* ph;     // p
   const uint32_t* hR;     // hp * R mod p
   const uint8_t* digits;  // exponent p-1 in 5-bit windows, most significant first
@@ -138,39 +140,69 @@ __device__ __forceinline__ void make_c0(int64_t M, const uint32_t* __restrict__ 
   normalize<TPI>(P, c0, lane, tig);
 }
 
-// acc = x^E mod m in the Montgomery domain, sliding window k=5 over the fixed public exponent
-// E = n (host-built schedule), odd-power table in global scratch.
-template <int TPI>
-__device__ __forceinline__ void modexp_sliding(uint32_t (&acc)[L], const uint32_t (&xt)[L], uint32_t* slot,
-                                               uint32_t* __restrict__ table, const uint16_t* __restrict__ sched,
-                                               int nsched, int first, const uint32_t (&m)[L], uint32_t mprime,
-                                               int lane, int tig) {
-  constexpr int S = TPI * L;
-  uint32_t cur[L];
-  store_limbs_g<TPI>(table, xt, tig);
-  write_limbs_lds<TPI>(slot, xt, tig);
-  uint32_t x2[L];
-  montmul<TPI>(x2, xt, slot, TPI, m, mprime, lane, tig);
-  write_limbs_lds<TPI>(slot, x2, tig);
+// ---------------------------------------------------------------- Montgomery program machine
+// Every modular product of an encrypt runs through ONE inlined montmul call site, driven by a
+// host-built op list (wave-uniform, read with scalar loads). This keeps the kernel's register
+// set at the montmul working set (P: 2L, a: L, m: L VGPRs) instead of one copy per call site,
+// and the hot loop's code (L unrolled CIOS iterations) resident in the instruction cache.
+//   op bit 0  B_FROM_A : LDS slot <- a             (squaring / multiply by the accumulator)
+//   op bit 1  B_FROM_T : LDS slot <- tile[bidx]
+//   op bit 2  A_FROM_T : a <- tile[aidx]
+//   op bit 3  STORE    : tile[sidx] <- a (after the product)
+//   fields    bidx = op[15:8], aidx = op[23:16], sidx = op[31:24]
+// then a <- a * slot * R^-1 mod m. Tiles are per-lane scratch in global memory laid out
+// [lane][tile][limb] (see lane_tiles).
+enum : uint32_t { OP_B_FROM_A = 1u, OP_B_FROM_T = 2u, OP_A_FROM_T = 4u, OP_STORE = 8u };
+constexpr int T_FINAL = TABLE_ODD;          // tile holding the final multiplier (c0, or 1)
+constexpr int NTILE = TABLE_ODD + 1;
+constexpr int TROW = (L + 3) & ~3;          // limbs per tile row, padded for 16-byte accesses
+constexpr size_t TILE_WORDS_PER_LANE = (size_t)NTILE * TROW;
+
+// Per-lane tiles, [lane][tile][TROW]: one 64-bit base per lane and immediate offsets (< 4 KiB)
+// for every limb, 16-byte loads/stores. (A [tile][limb][lane] layout coalesces better but needs
+// one 64-bit address per limb row, which the compiler hoists and keeps live: L*2 VGPRs.)
+__device__ __forceinline__ uint32_t* lane_tiles(uint32_t* scratch) {
+  return scratch + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * TILE_WORDS_PER_LANE;
+}
+__device__ __forceinline__ void tile_load(const uint32_t* __restrict__ tl, int k, uint32_t (&x)[L], int /*lane*/) {
+  const uint4* q = reinterpret_cast<const uint4*>(tl + k * TROW);
 #pragma unroll
-  for (int i = 0; i < L; ++i) cur[i] = xt[i];
-  for (int k = 1; k < TABLE_ODD; ++k) {
-    montmul<TPI>(cur, cur, slot, TPI, m, mprime, lane, tig);
-    store_limbs_g<TPI>(table + k * S, cur, tig);
+  for (int j = 0; j < TROW / 4; ++j) {
+    const uint4 v = q[j];
+    if (4 * j + 0 < L) x[4 * j + 0] = v.x;
+    if (4 * j + 1 < L) x[4 * j + 1] = v.y;
+    if (4 * j + 2 < L) x[4 * j + 2] = v.z;
+    if (4 * j + 3 < L) x[4 * j + 3] = v.w;
   }
-  load_limbs_g<TPI>(table + first * S, acc, tig);
-  for (int op = 0; op < nsched; ++op) {
-    const int nsq = sched[2 * op];
-    const int idx = sched[2 * op + 1];
-    for (int t = 0; t < nsq; ++t) {
-      write_limbs_lds<TPI>(slot, acc, tig);
-      montmul<TPI>(acc, acc, slot, TPI, m, mprime, lane, tig);
+}
+__device__ __forceinline__ void tile_store(uint32_t* __restrict__ tl, int k, const uint32_t (&x)[L], int /*lane*/) {
+  uint4* q = reinterpret_cast<uint4*>(tl + k * TROW);
+#pragma unroll
+  for (int j = 0; j < TROW / 4; ++j) {
+    uint4 v;
+    v.x = 4 * j + 0 < L ? x[4 * j + 0] : 0u;
+    v.y = 4 * j + 1 < L ? x[4 * j + 1] : 0u;
+    v.z = 4 * j + 2 < L ? x[4 * j + 2] : 0u;
+    v.w = 4 * j + 3 < L ? x[4 * j + 3] : 0u;
+    q[j] = v;
+  }
+}
+
+template <int TPI>
+__device__ __forceinline__ void run_program(uint32_t (&a)[L], uint32_t* slot, uint32_t* __restrict__ tw,
+                                            const uint32_t* __restrict__ prog, int nprog, const uint32_t (&m)[L],
+                                            uint32_t mprime, int lane, int tig) {
+  for (int i = 0; i <= nprog; ++i) {
+    const uint32_t op = (i < nprog) ? __builtin_amdgcn_readfirstlane(prog[i]) : (OP_B_FROM_T | (T_FINAL << 8));
+    if (op & OP_B_FROM_A) write_limbs_lds<TPI>(slot, a, tig);
+    if (op & OP_B_FROM_T) {
+      uint32_t t[L];
+      tile_load(tw, (op >> 8) & 0xFF, t, lane);
+      write_limbs_lds<TPI>(slot, t, tig);
     }
-    if (idx != 0xFFFF) {
-      write_limbs_lds<TPI>(slot, acc, tig);
-      load_limbs_g<TPI>(table + idx * S, cur, tig);
-      montmul<TPI>(acc, cur, slot, TPI, m, mprime, lane, tig);
-    }
+    if (op & OP_A_FROM_T) tile_load(tw, (op >> 16) & 0xFF, a, lane);
+    montmul<TPI>(a, a, slot, TPI, m, mprime, lane, tig);
+    if (op & OP_STORE) tile_store(tw, op >> 24, a, lane);
   }
 }
 
@@ -188,9 +220,12 @@ __device__ __forceinline__ void emit_words(uint32_t* slot, const uint32_t (&x)[L
 }
 
 // ================================================================= encrypt
-// PaillierEncryptor.encrypt over an array (encryptor.py:71-114): encode -> c0 -> c0 * r^n mod n^2
+// PaillierEncryptor.encrypt over an array (encryptor.py:71-114): encode -> c0 -> c0 * r^n mod n^2.
+// The op list (host: build_encrypt_program) computes r~ = r R, the odd powers r~^1..r~^31 into
+// tiles 0..15, the sliding-window chain over n, and finally multiplies by tile T_FINAL = c0,
+// which also leaves the Montgomery domain: (r^n R) * c0 * R^-1 = c0 r^n.
 template <int TPI>
-__global__ __launch_bounds__(BLOCK) void k_encrypt(EncParams p) {
+__global__ __launch_bounds__(BLOCK, 2) void k_encrypt(EncParams p) {
   constexpr int S = TPI * L;
   constexpr int GPB = BLOCK / TPI;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -200,7 +235,7 @@ __global__ __launch_bounds__(BLOCK) void k_encrypt(EncParams p) {
   uint32_t* slot = smem + gib * S;
   uint32_t m[L];
   load_limbs_g<TPI>(p.N, m, tig);
-  uint32_t* table = p.scratch + (size_t)(blockIdx.x * GPB + gib) * TABLE_ODD * S;
+  uint32_t* tw = lane_tiles(p.scratch);
 
   for (long long base = (long long)blockIdx.x * GPB; base < p.n; base += (long long)gridDim.x * GPB) {
     const long long inst = base + gib;
@@ -213,36 +248,31 @@ __global__ __launch_bounds__(BLOCK) void k_encrypt(EncParams p) {
     else if (p.dtype == 1) st = encode_float(((const double*)p.x)[ii], fixed, p.fexp, M, e);
     else st = encode_int(((const int64_t*)p.x)[ii], fixed, p.fexp, M, e);
 
-    uint32_t c0[L], res[L];
-    make_c0<TPI>(M, p.nl, m, c0, lane, tig);
-    if (p.obf == 0) {
-#pragma unroll
-      for (int i = 0; i < L; ++i) res[i] = c0[i];
-    } else {
-      uint32_t rl[L];
+    uint32_t a[L];
+    make_c0<TPI>(M, p.nl, m, a, lane, tig);
+    if (p.obf != 0) {
+      tile_store(tw, T_FINAL, a, lane);
       if (p.obf == 1) {
-        words_to_limbs(p.r + ii * p.r_stride, p.r_words, rl, tig);
+        words_to_limbs(p.r + ii * p.r_stride, p.r_words, a, tig);
       } else {
-        // ChaCha20 block `tig` of this element's stream -> LDS words -> limbs
+        // ChaCha20 blocks tig, tig+TPI, ... of this element's stream -> LDS words -> limbs
         const unsigned long long gidx = p.index_base + (unsigned long long)ii;
-        uint32_t blk[16];
-        chacha20_block(p.rng_key, (uint32_t)tig, (uint32_t)gidx, (uint32_t)(gidx >> 32), 0x66786169u, blk);
         wave_lds_fence();
+        for (int b = tig; b * 16 < p.rng_words; b += TPI) {
+          uint32_t blk[16];
+          chacha20_block(p.rng_key, (uint32_t)b, (uint32_t)gidx, (uint32_t)(gidx >> 32), 0x66786169u, blk);
 #pragma unroll
-        for (int w = 0; w < 16; ++w) slot[tig * 16 + w] = blk[w];
+          for (int w = 0; w < 16; ++w) slot[b * 16 + w] = blk[w];
+        }
         wave_lds_fence();
-        words_to_limbs(slot, p.rng_words, rl, tig);
+        words_to_limbs(slot, p.rng_words, a, tig);
         wave_lds_fence();
       }
-      uint32_t xt[L], acc[L];
       copy_g_to_lds<TPI>(slot, p.R2, tig);
-      montmul<TPI>(xt, rl, slot, TPI, m, p.mprime, lane, tig);          // r * R mod n^2
-      modexp_sliding<TPI>(acc, xt, slot, table, p.sched, p.nsched, p.first, m, p.mprime, lane, tig);
-      write_limbs_lds<TPI>(slot, c0, tig);
-      montmul<TPI>(res, acc, slot, TPI, m, p.mprime, lane, tig);       // r^n * c0 mod n^2 (< 2 n^2)
-      cond_sub<TPI>(res, m, lane, tig);
+      run_program<TPI>(a, slot, tw, p.prog, p.nprog, m, p.mprime, lane, tig);
+      cond_sub<TPI>(a, m, lane, tig);
     }
-    emit_words<TPI>(slot, res, p.ct + ii * p.ct_words, p.ct_words, valid, tig);
+    emit_words<TPI>(slot, a, p.ct + ii * p.ct_words, p.ct_words, valid, tig);
     if (valid && tig == 0) {
       p.exp[ii] = e;
       if (p.status) p.status[ii] = st;
@@ -251,9 +281,11 @@ __global__ __launch_bounds__(BLOCK) void k_encrypt(EncParams p) {
 }
 
 // ================================================================= k-way homomorphic add
-// prod_j c_j^(16^(E - e_j)) mod n^2 (encrypted_number.py:115-137, 166-185)
+// prod_j c_j^(16^(E - e_j)) mod n^2 (encrypted_number.py:115-137, 166-185).
+// The running product lives in tile 0; groups that need fewer alignment squarings than their
+// wave-mates multiply by R mod n^2 (the Montgomery one) instead, which leaves them unchanged.
 template <int TPI>
-__global__ __launch_bounds__(BLOCK) void k_add(AddParams p) {
+__global__ __launch_bounds__(BLOCK, 2) void k_add(AddParams p) {
   constexpr int S = TPI * L;
   constexpr int GPB = BLOCK / TPI;
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -263,6 +295,7 @@ __global__ __launch_bounds__(BLOCK) void k_add(AddParams p) {
   uint32_t* slot = smem + gib * S;
   uint32_t m[L];
   load_limbs_g<TPI>(p.N, m, tig);
+  uint32_t* tw = lane_tiles(p.scratch);
 
   for (long long base = (long long)blockIdx.x * GPB; base < p.n; base += (long long)gridDim.x * GPB) {
     const long long inst = base + gib;
@@ -270,34 +303,33 @@ __global__ __launch_bounds__(BLOCK) void k_add(AddParams p) {
     const long long ii = valid ? inst : p.n - 1;
     int E = p.exps[ii];
     for (int j = 1; j < p.k; ++j) E = max(E, p.exps[(long long)j * p.n + ii]);
-    uint32_t acc[L];
+    uint32_t a[L];
     for (int j = 0; j < p.k; ++j) {
-      uint32_t cl[L], ct[L];
-      words_to_limbs(p.cts + ((long long)j * p.n + ii) * p.ct_words, p.ct_words, cl, tig);
+      words_to_limbs(p.cts + ((long long)j * p.n + ii) * p.ct_words, p.ct_words, a, tig);
       copy_g_to_lds<TPI>(slot, p.R2, tig);
-      montmul<TPI>(ct, cl, slot, TPI, m, p.mprime, lane, tig);         // Montgomery form
+      montmul<TPI>(a, a, slot, TPI, m, p.mprime, lane, tig);           // Montgomery form
       const int nsq = 4 * (E - p.exps[(long long)j * p.n + ii]);
       for (int t = 0;; ++t) {                                            // wave-uniform trip count
         const bool need = t < nsq;
         if (ballot(need) == 0ull) break;
-        uint32_t sq[L];
-        write_limbs_lds<TPI>(slot, ct, tig);
-        montmul<TPI>(sq, ct, slot, TPI, m, p.mprime, lane, tig);
-#pragma unroll
-        for (int i = 0; i < L; ++i) ct[i] = need ? sq[i] : ct[i];
+        if (need) {
+          write_limbs_lds<TPI>(slot, a, tig);
+        } else {
+          copy_g_to_lds<TPI>(slot, p.oneR, tig);
+        }
+        montmul<TPI>(a, a, slot, TPI, m, p.mprime, lane, tig);
       }
-      if (j == 0) {
-#pragma unroll
-        for (int i = 0; i < L; ++i) acc[i] = ct[i];
-      } else {
-        write_limbs_lds<TPI>(slot, ct, tig);
-        montmul<TPI>(acc, acc, slot, TPI, m, p.mprime, lane, tig);
+      if (j > 0) {
+        write_limbs_lds<TPI>(slot, a, tig);
+        tile_load(tw, 0, a, lane);
+        montmul<TPI>(a, a, slot, TPI, m, p.mprime, lane, tig);
       }
+      tile_store(tw, 0, a, lane);
     }
     write_one_lds<TPI>(slot, tig);
-    montmul<TPI>(acc, acc, slot, TPI, m, p.mprime, lane, tig);           // leave the Montgomery domain
-    cond_sub<TPI>(acc, m, lane, tig);
-    emit_words<TPI>(slot, acc, p.out + ii * p.ct_words, p.ct_words, valid, tig);
+    montmul<TPI>(a, a, slot, TPI, m, p.mprime, lane, tig);               // leave the Montgomery domain
+    cond_sub<TPI>(a, m, lane, tig);
+    emit_words<TPI>(slot, a, p.out + ii * p.ct_words, p.ct_words, valid, tig);
     if (valid && tig == 0) p.out_exp[ii] = E;
   }
 }
@@ -537,8 +569,8 @@ struct DbgParams {
   const uint32_t* R2;
   const uint32_t* nl;
   uint32_t mprime;
-  const uint16_t* sched;
-  int nsched, first;
+  const uint32_t* prog;
+  int nprog;
   uint32_t* scratch;
 };
 
@@ -576,13 +608,15 @@ __global__ __launch_bounds__(BLOCK) void k_debug(DbgParams p) {
     write_one_lds<TPI>(slot, tig);
     montmul<TPI>(r, t, slot, TPI, m, p.mprime, lane, tig);
   } else if (p.op == 4) {
-    uint32_t t[L], acc[L];
-    uint32_t* table = p.scratch + (size_t)(blockIdx.x * GPB + gib) * TABLE_ODD * S;
+    uint32_t* tw = lane_tiles(p.scratch);
+    uint32_t one[L];
+#pragma unroll
+    for (int i = 0; i < L; ++i) one[i] = (tig == 0 && i == 0) ? 1u : 0u;
+    tile_store(tw, T_FINAL, one, lane);
+#pragma unroll
+    for (int i = 0; i < L; ++i) r[i] = a[i];
     copy_g_to_lds<TPI>(slot, p.R2, tig);
-    montmul<TPI>(t, a, slot, TPI, m, p.mprime, lane, tig);
-    modexp_sliding<TPI>(acc, t, slot, table, p.sched, p.nsched, p.first, m, p.mprime, lane, tig);
-    write_one_lds<TPI>(slot, tig);
-    montmul<TPI>(r, acc, slot, TPI, m, p.mprime, lane, tig);
+    run_program<TPI>(r, slot, tw, p.prog, p.nprog, m, p.mprime, lane, tig);
     cond_sub<TPI>(r, m, lane, tig);
   } else if (p.op == 5) {
 #pragma unroll

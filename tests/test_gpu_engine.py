@@ -29,8 +29,8 @@ def setup(request, golden):
     k = golden["keys"][str(request.param)]
     n = int(k["n"], 16)
     ctx = N.Context(n, 0)
-    S = 19 * {1024: 4, 2048: 8, 4096: 16}[request.param]
-    return ctx, n, n * n, 27 * S
+    S = 37 * {1024: 2, 2048: 4, 4096: 8}[request.param]   # L = 37 limbs per lane (bn_group.hpp)
+    return ctx, n, n * n, 28 * S
 
 
 def test_roundtrip_words(setup):

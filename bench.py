@@ -1,21 +1,30 @@
 #!/usr/bin/env python3
 """bench.py — Paillier-2048 array encryption on MI355X (BASELINE.json metric).
 
-A step = one device-resident encryption of the rank's 1M-element float32 vector (encode ->
-c0 -> c0 * r^n mod n^2 with a device ChaCha20 obfuscator r per element), then, for N > 1, one
-RCCL all-gather of the ciphertext shards so every rank holds the whole encrypted vector.
+A step = one device-resident encryption of the rank's 1M-element float32 vector: fixed-point
+encode -> c0 = 1 + n*m -> c0 * r^n mod n^2 with a device ChaCha20 obfuscator r per element
+(flex/crypto/paillier/encryptor.py:71-114 semantics), then, for N > 1 GPUs, one RCCL all-gather of
+the ciphertext shards so every rank holds the whole encrypted vector (weak scaling).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, weak scaling)
+The workload (BASELINE.json configs[1]: "encrypt+decrypt on 1 MI355X") holds the private key, so
+the default path is the CRT encryption (kernels_crt.hpp: r^n via half-size exponentiations mod p,
+p^2, q, q^2; bit-identical ciphertexts). The public-key-only kernel is timed on the same input in
+the same run and reported as `public_key_path`; `--path public` makes it the timed path.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--path crt|public]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU)
 
 Rank 0 prints ONE JSON line. `value` = encrypts/s over all ranks (max-over-ranks wall clock of the
-K timed steps). `roofline` is for the dominant kernel (k_encrypt), timed with HIP events on the
-stream it is launched on; `cpu_baseline` is the GMP restatement of the reference's CPU path
-(oracle/gmp_oracle.c) timed on this host on a bounded sample of the same workload.
+K timed steps). `roofline` is for the dominant kernel of the timed path, timed live with HIP events
+recorded on the launch stream between the kernels of every timed encrypt call; its work figure is
+the SURVEY.md §8d canonical 32x32->64 MAC count. `cpu_baseline` is the
+GMP restatement of the reference CPU path (oracle/gmp_oracle.c) on this host's cores, on a bounded
+sample of the same workload, which doubles as a bit-exact check of the GPU output.
 """
 import argparse
 import hashlib
 import json
+import math
 import os
 import sys
 import time
@@ -28,24 +37,49 @@ for p in (ROOT, os.path.join(ROOT, "ibond-flex_amd")):
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-INT_MAC_PEAK = 31.94e12      # measured v_mad_u64_u32 issue rate, profiles/r01_step0_int_throughput.txt
+# Peak 32x32->64 multiply-accumulate issue rate of one MI355X: v_mad_u64_u32 lanes/s measured by
+# tools/microbench/int_throughput.hip (profiles/r01_step0_int_throughput.txt).
+INT_MAC_PEAK = float(os.environ.get("FLEXPAI_INT_MAC_PEAK", "31.94e12"))
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 
 
-def canonical_w_enc(nb: int) -> float:
-    """SURVEY.md §8d canonical algorithmic work of one encryption in 32x32->64 MACs."""
-    s = nb // 16
-    M = 2 * s * s + s
-    P = (nb - 1) + (nb + 3) // 4 + 16
-    return float((P + 1) * M)
+# ------------------------------------------------------------- canonical work
+def _M(s: int) -> int:
+    """Montgomery product of s 32-bit limbs: 2 s^2 + s MACs."""
+    return 2 * s * s + s
 
 
-def canonical_w_dec(nb: int) -> float:
-    s = nb // 32
-    M = 2 * s * s + s
-    b = nb // 2
-    P = (b - 1) + (b + 3) // 4 + 16
-    return float(2 * (P + 2) * M)
+def _P(b: int) -> int:
+    """Products of a fixed-window-4 exponentiation with a b-bit exponent."""
+    return (b - 1) + (b + 3) // 4 + 14 + 2
+
+
+def work_enc_public(nb: int) -> float:
+    return float((_P(nb) + 1) * _M(nb // 16))
+
+
+def work_crt(nb: int) -> dict:
+    """Per-element canonical MACs of the CRT encryption stages."""
+    h = nb // 2
+    return {"k_crt_a": float(2 * (_P(h) + 1) * _M(nb // 64)),      # (r mod p_h)^(e_h) mod p_h, both halves
+            "k_crt_b": float(2 * (_P(h) + 2) * _M(nb // 32)),      # y^(p_h) * coef mod p_h^2, both halves
+            "k_crt_fin": float(3 * _M(nb // 16))}                  # (u_p q^2 + u_q p^2) * c0 mod n^2
+
+
+def work_dec(nb: int) -> float:
+    return float(2 * (_P(nb // 2) + 2) * _M(nb // 32))
+
+
+def load_traffic(kernel: str, n: int, nb: int):
+    path = os.path.join(ROOT, "profiles", f"pmc_{kernel}_latest.json")
+    try:
+        with open(path) as f:
+            pm = json.load(f)
+        if pm.get("n") == n and pm.get("nb") == nb:
+            return pm.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
 
 
 def main():
@@ -55,10 +89,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--n", type=int, default=1 << 20, help="elements per GPU")
     ap.add_argument("--nb", type=int, default=2048, help="Paillier key bits")
+    ap.add_argument("--path", choices=("crt", "public"), default="crt")
     ap.add_argument("--cpu-sample", type=int, default=16384)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-decrypt", action="store_true")
+    ap.add_argument("--no-public", action="store_true", help="skip timing the public-key path beside CRT")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -76,6 +112,9 @@ def main():
 
     pk, sk = generate_paillier_keypair(args.nb, seed=1)
     ctx = _native.Context(pk.n, local_rank, sk.p, sk.q)
+    use_crt = args.path == "crt" and ctx.crt_available
+    ctx.set_crt(use_crt)
+    ctx.set_stage_timing(True)
     lib = _native.load_library()
     N, W = args.n, ctx.ct_words
     x_host = np.random.default_rng(rank).standard_normal(N, dtype=np.float32)
@@ -84,36 +123,30 @@ def main():
     ex = torch.empty(N, dtype=torch.int32, device=dev)
     st = torch.empty(N, dtype=torch.int32, device=dev)
     rng_key = hashlib.sha256(b"flexpai-bench-key").digest()
-    index_base = rank * N
+    index_base = rank * N            # obfuscators keyed by the GLOBAL element index
     stream = torch.cuda.current_stream(dev)
-    gathered = None
-    if world > 1:
-        gathered = torch.empty((world * N, W), dtype=torch.int32, device=dev)
+    gathered = torch.empty((world * N, W), dtype=torch.int32, device=dev) if world > 1 else None
 
-    def encrypt():
+    def encrypt(out):
         rc = lib.pai_encrypt_dev(ctx.handle, _native.PAI_F32, x.data_ptr(), N, 0, 0, _native.PAI_OBF_RNG,
-                                 None, 0, 0, rng_key, index_base, ct.data_ptr(), ex.data_ptr(), st.data_ptr(),
+                                 None, 0, 0, rng_key, index_base, out.data_ptr(), ex.data_ptr(), st.data_ptr(),
                                  stream.cuda_stream)
         if rc != 0:
             raise RuntimeError(lib.pai_last_error().decode())
 
-    def step():
-        encrypt()
+    for _ in range(args.warmup):
+        encrypt(ct)
         if world > 1:
             dist.all_gather_into_tensor(gathered, ct)
-
-    for _ in range(args.warmup):
-        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    stage_ms = []
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record(stream)
-        encrypt()
-        ev[k][1].record(stream)
+    for _ in range(args.steps):
+        encrypt(ct)
+        stage_ms.append(ctx.stage_times())     # HIP events recorded between this call's kernels
         if world > 1:
             dist.all_gather_into_tensor(gathered, ct)
     torch.cuda.synchronize()
@@ -125,10 +158,29 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    stage_avg = [float(np.mean([s[i] for s in stage_ms])) for i in range(len(stage_ms[0]))]
+    ct_host_check = ct[: min(N, args.cpu_sample)].cpu().numpy().view(np.uint32).copy()
+    ex_host_check = ex[: min(N, args.cpu_sample)].cpu().numpy().copy()
 
-    # correctness on the timed output: decrypt on the device and compare with the input exactly
     extra = {}
+    # the other path on the same input (untimed region), for the record and as a parity check
+    if use_crt and not args.no_public:
+        ct2 = torch.empty_like(ct)
+        ctx.set_crt(False)
+        encrypt(ct2)
+        pub_ms = ctx.stage_times()[0]
+        ctx.set_crt(True)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(ct2, ct))
+        extra["public_key_path"] = {"value": N / (pub_ms * 1e-3), "unit": "encrypts/s per GPU",
+                                    "kernel": "k_encrypt", "kernel_ms": pub_ms,
+                                    "int_mac_frac": N * work_enc_public(args.nb) / (pub_ms * 1e-3) / INT_MAC_PEAK,
+                                    "bit_identical_to_crt": same}
+        del ct2
+        if not same:
+            raise SystemExit("CRT and public-key ciphertexts differ")
+
+    # correctness of the timed output: decrypt on the device and compare with the input exactly
     if not args.no_decrypt:
         val = torch.empty(N, dtype=torch.float64, device=dev)
         stt = torch.empty(N, dtype=torch.int32, device=dev)
@@ -144,8 +196,8 @@ def main():
         ok = bool(torch.equal(val, x.double())) and int((stt > 1).sum().item()) == 0
         extra["decrypt_per_s_per_gpu"] = N / (dec_ms * 1e-3)
         extra["decrypt_kernel_ms"] = dec_ms
+        extra["decrypt_int_mac_frac"] = N * work_dec(args.nb) / (dec_ms * 1e-3) / INT_MAC_PEAK
         extra["roundtrip_exact"] = ok
-        extra["decrypt_int_mac_frac"] = (N * canonical_w_dec(args.nb) / (dec_ms * 1e-3)) / INT_MAC_PEAK
         if not ok:
             raise SystemExit("decrypt(encrypt(x)) != x on the device")
 
@@ -155,20 +207,25 @@ def main():
         return
 
     value = world * N * args.steps / elapsed
-    w_enc = canonical_w_enc(args.nb)
-    achieved_mac = N * w_enc / (kern_ms * 1e-3)
-    alg_bytes = 4 + W * 4 + 4     # x in, ciphertext out, exponent out (r generated on device)
-    achieved_gbs = N * alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_encrypt_latest.json")
-    if os.path.exists(pmc_path):
-        try:
-            with open(pmc_path) as f:
-                pm = json.load(f)
-            if pm.get("n") == N and pm.get("nb") == args.nb:
-                traffic = pm.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    if use_crt:
+        names = ["k_crt_a", "k_crt_b", "k_crt_fin"]
+        works = work_crt(args.nb)
+        stages = {nm: {"kernel_ms": ms, "work_mac_per_elem": works[nm],
+                       "achieved_tmac_s": N * works[nm] / (ms * 1e-3) / 1e12}
+                  for nm, ms in zip(names, stage_avg)}
+        dom = max(names, key=lambda nm: stages[nm]["kernel_ms"])
+        dom_ms, dom_work = stages[dom]["kernel_ms"], works[dom]
+        extra["stages"] = stages
+        total_work = sum(works.values())
+    else:
+        dom, dom_ms, dom_work = "k_encrypt", stage_avg[0], work_enc_public(args.nb)
+        total_work = dom_work
+    achieved = N * dom_work / (dom_ms * 1e-3)
+    alg_bytes = 4 + W * 4 + 4     # x in, ciphertext out, exponent out (r generated on the device)
+    extra["path"] = "crt" if use_crt else "public"
+    extra["encrypt_call_ms"] = float(sum(stage_avg))
+    extra["path_int_mac_frac"] = N * total_work / (sum(stage_avg) * 1e-3) / INT_MAC_PEAK
+    extra["hbm_algorithmic_gbs"] = N * alg_bytes / (sum(stage_avg) * 1e-3) / 1e9
 
     cpu = None
     if not args.no_cpu_baseline:
@@ -179,13 +236,11 @@ def main():
             t1 = time.perf_counter()
             cct, cex = gmp_oracle.encrypt_f32_chacha(pk.n, x_host[:S], rng_key, index_base, th)
             cdt = time.perf_counter() - t1
-            # the sample doubles as a bit-exact parity check of the timed GPU output
-            gct = ct[:S].cpu().numpy().view(np.uint32)
-            same = bool(np.array_equal(gct, cct) and np.array_equal(ex[:S].cpu().numpy(), cex))
+            same = bool(np.array_equal(ct_host_check[:S], cct) and np.array_equal(ex_host_check[:S], cex))
             cpu = {"value": S / cdt, "unit": "encrypts/s", "cores": th, "kind": "port",
-                   "sample": f"first {S} elements of the rank-0 vector, same ChaCha20 r stream; "
-                             f"GMP 6.2.1 mpz_powm per element (the library gmpy2 2.0.8 wraps), "
-                             f"{th} worker threads like the reference's Pool(cpu_count())",
+                   "sample": f"first {S} elements of the rank-0 vector with the same ChaCha20 obfuscators; "
+                             f"GMP 6.2.1 mpz_powm(r, n, n^2) per element (the library gmpy2 2.0.8 wraps, "
+                             f"obfuscator.py:36), {th} worker threads like the reference's Pool(cpu_count())",
                    "gpu_bit_exact_on_sample": same}
             if not same:
                 raise SystemExit("GPU ciphertexts differ from the GMP oracle on the CPU sample")
@@ -203,17 +258,20 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32",
-        "data": "synthetic: numpy default_rng(rank).standard_normal float32; seeded key generate_paillier_keypair(nb, seed=1)",
+        "data": "synthetic: numpy default_rng(rank).standard_normal float32; seeded key "
+                "generate_paillier_keypair(nb, seed=1); device ChaCha20 obfuscators keyed by global index",
         "config": {"workload": f"Paillier n={args.nb} encrypt of a {N}-element float32 vector per GPU, "
-                               f"device-resident, device ChaCha20 obfuscators"
+                               f"device-resident, key holder ({'CRT' if use_crt else 'public-key'} path)"
                                + (", RCCL all-gather of ciphertext shards" if world > 1 else ""),
                    "key_bits": args.nb, "elements_per_gpu": N, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "valu-int-mac", "achieved": achieved_mac / 1e12, "peak": INT_MAC_PEAK / 1e12,
-                     "unit": "TMAC/s", "frac": achieved_mac / INT_MAC_PEAK, "traffic": traffic,
-                     "kernel": "k_encrypt", "kernel_ms": kern_ms,
-                     "work_per_unit": f"{w_enc:.4g} 32x32->64 MAC per encrypt (SURVEY.md §8d canonical)"},
-        "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_unit": alg_bytes},
+        "roofline": {"bound": "valu-int-mac", "achieved": achieved / 1e12, "peak": INT_MAC_PEAK / 1e12,
+                     "unit": "TMAC/s", "frac": achieved / INT_MAC_PEAK,
+                     "traffic": load_traffic(dom, N, args.nb),
+                     "kernel": dom, "kernel_ms": dom_ms,
+                     "work_per_unit": f"{dom_work:.4g} canonical 32x32->64 MAC per element (SURVEY.md §8d)"},
+        "roofline_hbm": {"bound": "hbm", "achieved": extra["hbm_algorithmic_gbs"], "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": extra["hbm_algorithmic_gbs"] / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_unit": alg_bytes},
         "cpu_baseline": cpu,
         "extra": extra,
     }

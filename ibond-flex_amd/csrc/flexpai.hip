@@ -8,6 +8,7 @@
 #include "flexpai.h"
 #include "host_bignum.hpp"
 #include "kernels.hpp"
+#include "kernels_crt.hpp"
 
 using namespace fpai;
 
@@ -41,15 +42,31 @@ struct pai_ctx {
   uint32_t *d_qinvR = nullptr, *d_nlimb = nullptr, *d_qRn = nullptr, *d_maxint = nullptr;
   uint32_t nprime_d = 0;
   int nwin = 0, n_limbs = 0;
+  // CRT encryption (kernels_crt.hpp): available when the private key is set and the halves fit
+  bool crt_ok = false;
+  bool crt_enabled = true;
+  int crt_sa = 0, crt_sb = 0;
+  CrtHalf* d_crt_a = nullptr;   // [2] stage A halves
+  CrtHalf* d_crt_b = nullptr;   // [2] stage B halves
+  uint32_t *d_kq = nullptr, *d_kp = nullptr;
   std::vector<void*> allocs;
   // scratch (exponent tables), grown on demand
   void* d_scratch = nullptr;
   size_t scratch_bytes = 0;
+  void* d_work = nullptr;       // CRT intermediates (y, u)
+  size_t work_bytes = 0;
   int cus = 0;
+  // optional per-stage timing of the last encrypt call (PAI_OPT_STAGE_TIMING)
+  bool timing = false;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  int nev = 0;
   ~pai_ctx() {
-    hipSetDevice(device);
-    for (void* p : allocs) hipFree(p);
-    if (d_scratch) hipFree(d_scratch);
+    (void)hipSetDevice(device);
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    for (void* p : allocs) (void)hipFree(p);
+    if (d_scratch) (void)hipFree(d_scratch);
+    if (d_work) (void)hipFree(d_work);
   }
 };
 
@@ -134,6 +151,35 @@ static bool build_modexp_program(const HBig& e, std::vector<uint32_t>& prog) {
   return loaded;   // false only for single-window exponents, which n (odd, >= 64 bits) never is
 }
 
+// Op list for run_lane_program (kernels_crt.hpp): the kernel stores x~ in tile 0; odd powers into
+// tiles 0..15 (x~^2 kept in tile 16), then the sliding-window chain over e.
+static bool build_lane_program(const HBig& e, std::vector<uint32_t>& prog) {
+  if (e.bits() < 8) return false;
+  std::vector<uint16_t> sched;
+  int first = 0;
+  sliding_schedule(e, sched, first);
+  auto op = [](uint32_t flags, int bidx, int aidx, int sidx) {
+    return flags | ((uint32_t)bidx << 8) | ((uint32_t)aidx << 16) | ((uint32_t)sidx << 24);
+  };
+  prog.clear();
+  prog.push_back(op(LOP_SQR | LOP_STORE, 0, 0, 16));                   // x~^2       -> T16
+  prog.push_back(op(LOP_A_FROM_T | LOP_STORE, 16, 0, 1));             // x~ * x~^2  -> T1
+  for (int k = 2; k < 16; ++k) prog.push_back(op(LOP_STORE, 16, 0, k));
+  bool loaded = false;
+  for (size_t i = 0; i + 1 < sched.size(); i += 2) {
+    const int nsq = sched[i], idx = sched[i + 1];
+    for (int t = 0; t < nsq; ++t) {
+      prog.push_back(loaded ? op(LOP_SQR, 0, 0, 0) : op(LOP_SQR | LOP_A_FROM_T, 0, first, 0));
+      loaded = true;
+    }
+    if (idx != 0xFFFF) {
+      prog.push_back(loaded ? op(0, idx, 0, 0) : op(LOP_A_FROM_T, idx, first, 0));
+      loaded = true;
+    }
+  }
+  return loaded;
+}
+
 template <typename K>
 static int grid_for(pai_ctx* c, K kernel, size_t lds, long long units, int per_block) {
   int occ = 0;
@@ -151,6 +197,30 @@ static int ensure_scratch(pai_ctx* c, size_t bytes) {
   HIPCHK(hipMalloc(&c->d_scratch, bytes));
   c->scratch_bytes = bytes;
   return 0;
+}
+
+static int ensure_work(pai_ctx* c, size_t bytes) {
+  if (bytes <= c->work_bytes) return 0;
+  if (c->d_work) HIPCHK(hipFree(c->d_work));
+  c->d_work = nullptr;
+  c->work_bytes = 0;
+  HIPCHK(hipMalloc(&c->d_work, bytes));
+  c->work_bytes = bytes;
+  return 0;
+}
+
+static void stage_mark(pai_ctx* c, int i, hipStream_t st) {
+  if (!c->timing || i >= 4) return;
+  if (!c->ev[i]) (void)hipEventCreate(&c->ev[i]);
+  (void)hipEventRecord(c->ev[i], st);
+  c->nev = i + 1;
+}
+
+template <typename K>
+static int blocks_per_cu(K kernel, int threads, size_t lds) {
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, threads, lds) != hipSuccess || occ < 1) occ = 1;
+  return occ;
 }
 
 // C-linkage comes from the declarations in flexpai.h.
@@ -203,6 +273,66 @@ int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** ou
     return rc;
   }
   *out = c;
+  return 0;
+}
+
+// CRT encryption constants (kernels_crt.hpp). p < q here (sorted like keypair.py:57-62).
+static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
+  c->crt_ok = false;
+  const size_t pb = std::max(p.bits(), q.bits());
+  int sa = 0, sb = 0;
+  for (auto cand : {std::pair<int, int>{19, 37}, std::pair<int, int>{37, 74}}) {
+    if ((size_t)LB * cand.first >= pb + 2 && (size_t)LB * cand.second >= 2 * pb + 2) {
+      sa = cand.first;
+      sb = cand.second;
+      break;
+    }
+  }
+  if (!sa) return 0;   // key too large for the lane engine: public-key path only
+  const size_t RA = (size_t)LB * sa, RB = (size_t)LB * sb, RE = (size_t)LB * c->S_e;
+  const HBig primes[2] = {p, q};
+  const HBig sq[2] = {mul(p, p), mul(q, q)};
+  CrtHalf ha[2], hb[2];
+  int rc;
+  for (int h = 0; h < 2; ++h) {
+    const HBig& ph = primes[h];
+    const HBig& other = primes[1 - h];
+    // stage A: (r mod p_h)^(other mod (p_h - 1)) mod p_h
+    HBig ea = mod(other, sub(ph, HBig(1)));
+    std::vector<uint32_t> pa, pbp;
+    if (!build_lane_program(ea, pa) || !build_lane_program(ph, pbp)) return 0;
+    std::vector<uint32_t> ck;
+    for (int K = 1; K <= KMAX_CHUNKS; ++K) {
+      std::vector<uint32_t> v = mul_pow2_mod(HBig(1), RA * (K + 1), ph).limbs(sa, LB);
+      ck.insert(ck.end(), v.begin(), v.end());
+    }
+    std::vector<uint32_t> one(sa, 0);
+    one[0] = 1;
+    uint32_t *dm, *dck, *done, *dpa;
+    if ((rc = upload(c, ph.limbs(sa, LB), &dm)) || (rc = upload(c, ck, &dck)) || (rc = upload(c, one, &done)) ||
+        (rc = upload(c, pa, &dpa)))
+      return rc;
+    ha[h] = CrtHalf{dm, dck, done, dpa, (int)pa.size(), mont_prime(ph, LB)};
+    // stage B: y^(p_h) mod p_h^2, times (other^2)^-1 mod p_h^2
+    const HBig& m2 = sq[h];
+    HBig coef = inv_mod(sq[1 - h], m2);
+    if (coef.is_zero()) return 0;
+    uint32_t *dm2, *dr2, *dcoef, *dpb;
+    if ((rc = upload(c, m2.limbs(sb, LB), &dm2)) ||
+        (rc = upload(c, mul_pow2_mod(HBig(1), 2 * RB, m2).limbs(sb, LB), &dr2)) ||
+        (rc = upload(c, coef.limbs(sb, LB), &dcoef)) || (rc = upload(c, pbp, &dpb)))
+      return rc;
+    hb[h] = CrtHalf{dm2, dr2, dcoef, dpb, (int)pbp.size(), mont_prime(m2, LB)};
+  }
+  std::vector<CrtHalf> va(ha, ha + 2), vb(hb, hb + 2);
+  if ((rc = upload(c, va, &c->d_crt_a)) || (rc = upload(c, vb, &c->d_crt_b))) return rc;
+  // finish: q^2 R^2 mod n^2 and p^2 R^2 mod n^2 (group layout)
+  if ((rc = upload(c, mul_pow2_mod(sq[1], 2 * RE, c->N).limbs(c->S_e, LB), &c->d_kq)) ||
+      (rc = upload(c, mul_pow2_mod(sq[0], 2 * RE, c->N).limbs(c->S_e, LB), &c->d_kp)))
+    return rc;
+  c->crt_sa = sa;
+  c->crt_sb = sb;
+  c->crt_ok = true;
   return 0;
 }
 
@@ -260,10 +390,42 @@ int pai_ctx_set_private(pai_ctx* c, const uint8_t* p_le, const uint8_t* q_le, si
   c->nprime_d = mont_prime(c->n, LB);
   c->n_limbs = (int)((c->n.bits() + LB - 1) / LB);
   c->has_priv = true;
+  if ((rc = setup_crt(c, p, q))) return rc;
   return 0;
 }
 
 void pai_ctx_destroy(pai_ctx* c) { delete c; }
+
+int pai_ctx_set_option(pai_ctx* c, int option, int value) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  switch (option) {
+    case PAI_OPT_CRT_ENCRYPT: c->crt_enabled = value != 0; return 0;
+    case PAI_OPT_STAGE_TIMING: c->timing = value != 0; c->nev = 0; return 0;
+  }
+  return fail(PAI_ERR_ARG, "pai_ctx_set_option: unknown option");
+}
+
+int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
+  if (!c || !value) return fail(PAI_ERR_ARG, "null argument");
+  switch (option) {
+    case PAI_OPT_CRT_ENCRYPT: *value = c->crt_enabled ? 1 : 0; return 0;
+    case PAI_OPT_CRT_AVAILABLE: *value = c->crt_ok ? 1 : 0; return 0;
+    case PAI_OPT_STAGE_TIMING: *value = c->timing ? 1 : 0; return 0;
+  }
+  return fail(PAI_ERR_ARG, "pai_ctx_get_option: unknown option");
+}
+
+int pai_ctx_stage_times(pai_ctx* c, float* ms_out, int max_out, int* count) {
+  if (!c || !count) return fail(PAI_ERR_ARG, "null argument");
+  *count = 0;
+  if (c->nev < 2) return 0;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipEventSynchronize(c->ev[c->nev - 1]));
+  const int k = std::min(c->nev - 1, max_out);
+  for (int i = 0; i < k; ++i) HIPCHK(hipEventElapsedTime(&ms_out[i], c->ev[i], c->ev[i + 1]));
+  *count = k;
+  return 0;
+}
 
 int pai_ctx_info(const pai_ctx* c, int* key_bits, int* ct_words, int* pt_words) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
@@ -283,8 +445,102 @@ static int launch_encrypt(pai_ctx* c, EncParams& p, hipStream_t st) {
   int rc = ensure_scratch(c, (size_t)grid * BLOCK * TILE_WORDS_PER_LANE * 4);
   if (rc) return rc;
   p.scratch = (uint32_t*)c->d_scratch;
+  stage_mark(c, 0, st);
   hipLaunchKernelGGL(k_encrypt<TPI>, dim3(grid), dim3(BLOCK), lds, st, p);
   HIPCHK(hipGetLastError());
+  stage_mark(c, 1, st);
+  return 0;
+}
+
+// CRT encryption (kernels_crt.hpp) in chunks of CRT_CHUNK elements: stage A (mod p, q), stage B
+// (mod p^2, q^2), finish (mod n^2), all asynchronous on `st`.
+constexpr long long CRT_CHUNK = 1ll << 22;
+
+template <int TPI>
+static int launch_crt_fin(pai_ctx* c, CrtFinParams& f, hipStream_t st) {
+  constexpr int S = TPI * L;
+  constexpr int GPB = BLOCK / TPI;
+  const size_t lds = (size_t)GPB * S * 4;
+  const int grid = grid_for(c, k_crt_fin<TPI>, lds, f.n, GPB);
+  hipLaunchKernelGGL(k_crt_fin<TPI>, dim3(grid), dim3(BLOCK), lds, st, f);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+template <int SA, int SB>
+static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
+  const long long N = e.n;
+  const int r_words = e.obf == PAI_OBF_GIVEN ? e.r_words : e.rng_words;
+  const int kchunks = (32 * r_words + LB * SA - 1) / (LB * SA);
+  if (kchunks > KMAX_CHUNKS || (e.obf == PAI_OBF_RNG && r_words > RBUF_WORDS))
+    return fail(PAI_ERR_ARG, "CRT encrypt: obfuscator too wide");
+  const long long chunk = std::min(N, CRT_CHUNK);
+  const int occA = blocks_per_cu(k_crt_a<SA>, LANE_BLOCK, 0), occB = blocks_per_cu(k_crt_b<SA, SB>, LANE_BLOCK, 0);
+  const long long lanes_blocks = (chunk + LANE_BLOCK - 1) / LANE_BLOCK;
+  const int gxA = (int)std::max<long long>(1, std::min<long long>(lanes_blocks, (long long)occA * c->cus / 2));
+  const int gxB = (int)std::max<long long>(1, std::min<long long>(lanes_blocks, (long long)occB * c->cus / 2));
+  const size_t scrA = (size_t)2 * gxA * LANE_BLOCK * lane_scratch_words<SA>() * 4;
+  const size_t scrB = (size_t)2 * gxB * LANE_BLOCK * lane_scratch_words<SB>() * 4;
+  int rc = ensure_scratch(c, std::max(scrA, scrB));
+  if (rc) return rc;
+  if ((rc = ensure_work(c, (size_t)2 * (SA + SB) * chunk * 4))) return rc;
+  uint32_t* y = (uint32_t*)c->d_work;
+  uint32_t* u = y + (size_t)2 * SA * chunk;
+  const size_t esz = e.dtype == PAI_F32 ? 4 : 8;
+  for (long long off = 0; off < N; off += chunk) {
+    const long long n = std::min(chunk, N - off);
+    CrtParams pa{};
+    pa.halves = c->d_crt_a;
+    pa.n = n;
+    pa.obf = e.obf;
+    pa.r = e.r ? e.r + (size_t)off * e.r_stride : nullptr;
+    pa.r_stride = e.r_stride;
+    pa.r_words = r_words;
+    std::memcpy(pa.rng_key, e.rng_key, sizeof(pa.rng_key));
+    pa.index_base = e.index_base + (unsigned long long)off;
+    pa.kchunks = kchunks;
+    pa.out = y;
+    pa.scratch = (uint32_t*)c->d_scratch;
+    const int gA = (int)std::min<long long>(gxA, (n + LANE_BLOCK - 1) / LANE_BLOCK);
+    stage_mark(c, 0, st);
+    hipLaunchKernelGGL(k_crt_a<SA>, dim3(gA, 2), dim3(LANE_BLOCK), 0, st, pa);
+    stage_mark(c, 1, st);
+    HIPCHK(hipGetLastError());
+    CrtParams pb{};
+    pb.halves = c->d_crt_b;
+    pb.n = n;
+    pb.yin = y;
+    pb.out = u;
+    pb.scratch = (uint32_t*)c->d_scratch;
+    const int gB = (int)std::min<long long>(gxB, (n + LANE_BLOCK - 1) / LANE_BLOCK);
+    hipLaunchKernelGGL((k_crt_b<SA, SB>), dim3(gB, 2), dim3(LANE_BLOCK), 0, st, pb);
+    HIPCHK(hipGetLastError());
+    stage_mark(c, 2, st);
+    CrtFinParams f{};
+    f.x = (const char*)e.x + (size_t)off * esz;
+    f.dtype = e.dtype;
+    f.exp_mode = e.exp_mode;
+    f.fexp = e.fexp;
+    f.u = u;
+    f.sb = SB;
+    f.n = n;
+    f.N = c->d_N;
+    f.nl = c->d_nl;
+    f.kq = c->d_kq;
+    f.kp = c->d_kp;
+    f.mprime = c->mprime_N;
+    f.ct = e.ct + (size_t)off * c->ct_words;
+    f.exp = e.exp + off;
+    f.status = e.status ? e.status + off : nullptr;
+    f.ct_words = c->ct_words;
+    switch (c->tpi_e) {
+      case 2: rc = launch_crt_fin<2>(c, f, st); break;
+      case 4: rc = launch_crt_fin<4>(c, f, st); break;
+      default: rc = fail(PAI_ERR_KEY, "CRT finish: unsupported group size");
+    }
+    if (rc) return rc;
+    stage_mark(c, 3, st);
+  }
   return 0;
 }
 
@@ -324,6 +580,10 @@ int pai_encrypt_dev(pai_ctx* c, int dtype, const void* d_x, size_t N, int exp_mo
   p.nprog = c->nprog;
   p.ct_words = c->ct_words;
   hipStream_t st = (hipStream_t)stream;
+  if (obf_mode != PAI_OBF_NONE && c->crt_ok && c->crt_enabled) {
+    if (c->crt_sa == 19) return launch_crt<19, 37>(c, p, st);
+    if (c->crt_sa == 37) return launch_crt<37, 74>(c, p, st);
+  }
   switch (c->tpi_e) {
     case 2: return launch_encrypt<2>(c, p, st);
     case 4: return launch_encrypt<4>(c, p, st);

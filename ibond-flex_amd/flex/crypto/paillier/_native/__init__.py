@@ -20,7 +20,10 @@ PAI_OBF_NONE, PAI_OBF_GIVEN, PAI_OBF_RNG = 0, 1, 2
 PAI_EXP_AUTO, PAI_EXP_FIXED = 0, 1
 EL_OK, EL_INT, EL_INT_BIG, EL_OVERFLOW, EL_FLOAT_OVF, EL_ENC_RANGE = 0, 1, 2, 3, 4, 5
 
+PAI_OPT_CRT_ENCRYPT, PAI_OPT_CRT_AVAILABLE, PAI_OPT_STAGE_TIMING = 1, 2, 3
+
 EXPORTED = ("pai_ctx_create", "pai_ctx_set_private", "pai_ctx_destroy", "pai_ctx_info", "pai_last_error",
+            "pai_ctx_set_option", "pai_ctx_get_option", "pai_ctx_stage_times",
             "pai_encrypt", "pai_add", "pai_decrypt", "pai_encrypt_dev", "pai_add_dev", "pai_decrypt_dev")
 
 _lib = None
@@ -48,6 +51,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.pai_ctx_destroy.restype = None
         lib.pai_ctx_info.argtypes = [P, P, P, P]
         lib.pai_last_error.restype = ctypes.c_char_p
+        lib.pai_ctx_set_option.argtypes = [P, I, I]
+        lib.pai_ctx_get_option.argtypes = [P, I, P]
+        lib.pai_ctx_stage_times.argtypes = [P, P, I, P]
         lib.pai_encrypt.argtypes = [P, I, P, S, I, ctypes.c_int32, I, P, S, S, P, U64, P, P, P]
         lib.pai_add.argtypes = [P, P, P, I, S, P, P]
         lib.pai_decrypt.argtypes = [P, P, P, S, P, P, P, P]
@@ -64,7 +70,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
 def _check(rc: int):
     if rc != 0:
         msg = load_library().pai_last_error().decode(errors="replace")
-        if rc == -4 and "does not match" in msg or "have to be different" in msg:
+        if rc == -4 and ("does not match" in msg or "have to be different" in msg):
             raise ValueError(msg)
         raise NativeError(f"flexpai error {rc}: {msg}")
 
@@ -103,6 +109,37 @@ class Context:
         hb = max(p.bit_length(), q.bit_length()) // 8 + 1
         _check(self.lib.pai_ctx_set_private(self._h, int_to_le(p, hb), int_to_le(q, hb), hb))
         self.has_private = True
+        if os.environ.get("FLEXPAI_CRT", "1").strip() == "0":
+            self.set_crt(False)
+
+    def _get_option(self, opt: int) -> int:
+        v = ctypes.c_int()
+        _check(self.lib.pai_ctx_get_option(self._h, opt, ctypes.byref(v)))
+        return v.value
+
+    @property
+    def crt_available(self) -> bool:
+        """True when the private key is set and the CRT encryption kernels fit this key size."""
+        return bool(self._get_option(PAI_OPT_CRT_AVAILABLE))
+
+    @property
+    def crt_enabled(self) -> bool:
+        return bool(self._get_option(PAI_OPT_CRT_ENCRYPT))
+
+    def set_stage_timing(self, enabled: bool):
+        _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_STAGE_TIMING, 1 if enabled else 0))
+
+    def stage_times(self):
+        """Kernel durations (ms) of the last encrypt call (needs set_stage_timing(True))."""
+        buf = (ctypes.c_float * 8)()
+        cnt = ctypes.c_int()
+        _check(self.lib.pai_ctx_stage_times(self._h, buf, 8, ctypes.byref(cnt)))
+        return [float(buf[i]) for i in range(cnt.value)]
+
+    def set_crt(self, enabled: bool):
+        """Encrypt through the private-key CRT kernels (default when available) or the public-key one.
+        The ciphertext bits are identical either way."""
+        _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_CRT_ENCRYPT, 1 if enabled else 0))
 
     def close(self):
         if getattr(self, "_h", None):

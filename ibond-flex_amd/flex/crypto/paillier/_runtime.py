@@ -4,6 +4,11 @@ child builds its own), so PaillierEncryptor/PaillierDecryptor stay picklable exa
 reference's (encryptor.py / decryptor.py are sent to peers, e.g. he_otp_lr_ft1/train.py:70).
 
 Device selection: $FLEXPAI_DEVICE, else $LOCAL_RANK, else 0.
+
+Private keys known to this process (a PaillierDecryptor was built, or the factory
+generate_paillier_encryptor_decryptor made the pair) are registered here so that the context
+of that key can encrypt through the CRT kernels (same ciphertext bits, ~4x fewer multiplies);
+the registry is process-local and never pickled. $FLEXPAI_CRT=0 disables CRT encryption.
 """
 from __future__ import annotations
 
@@ -17,6 +22,13 @@ from . import _native
 
 _lock = threading.Lock()
 _ctxs: Dict[Tuple[int, int, int], "_native.Context"] = {}
+_private: Dict[int, object] = {}
+
+
+def register_private(public_key, private_key) -> None:
+    """Remember this process's private key for `public_key` (enables CRT encryption)."""
+    with _lock:
+        _private[public_key.n] = private_key
 
 
 def device_index() -> int:
@@ -33,6 +45,8 @@ def context(public_key, private_key=None) -> "_native.Context":
     dev = device_index()
     k = (public_key.n, dev, os.getpid())
     with _lock:
+        if private_key is None:
+            private_key = _private.get(public_key.n)
         ctx = _ctxs.get(k)
         if ctx is None:
             ctx = _native.Context(public_key.n, dev)

@@ -18,6 +18,14 @@ class PaillierDecryptor(object):
     def __init__(self, pub_key: PaillierPublicKey, priv_key: PaillierPrivateKey):
         self.pub_key = pub_key
         self.priv_key = priv_key
+        from . import _runtime
+        _runtime.register_private(pub_key, priv_key)
+
+    def __setstate__(self, state):
+        # unpickled in another process (the reference pickles decryptors into pool workers)
+        self.__dict__.update(state)
+        from . import _runtime
+        _runtime.register_private(self.pub_key, self.priv_key)
 
     def _check(self, encrypted_number):
         if not isinstance(encrypted_number, PaillierEncryptedNumber):          # decryptor.py:73-75

@@ -6,6 +6,7 @@
  *
  *   pai_ctx_create        <- PaillierPublicKey(n)                  flex/crypto/paillier/keypair.py:20-39
  *   pai_ctx_set_private   <- PaillierPrivateKey(pk, p, q)          flex/crypto/paillier/keypair.py:42-90
+ *   pai_ctx_set_option    <- (no reference counterpart: selects the CRT encryption kernels)
  *   pai_encrypt[_dev]     <- PaillierEncryptor.encrypt(ndarray)    flex/crypto/paillier/encryptor.py:71-114
  *                            (FixedPointNumber.encode fixedpoint_number.py:46-90, raw_encrypt
  *                             raw_encrypt.py:22-49, apply_obfuscation obfuscator.py:23-37 ->
@@ -66,9 +67,21 @@ typedef struct pai_ctx pai_ctx;
 #define PAI_EL_FLOAT_OVF 4    /* OverflowError: int too large to convert to float (e > 0)           */
 #define PAI_EL_ENC_RANGE 5    /* encode ValueError (fixedpoint_number.py:86-88) / beyond int64      */
 
+/* context options */
+#define PAI_OPT_CRT_ENCRYPT 1    /* 1 (default): encrypt via the private-key CRT path when available */
+#define PAI_OPT_CRT_AVAILABLE 2  /* read-only: 1 when the private key is set and the CRT kernels fit */
+#define PAI_OPT_STAGE_TIMING 3   /* 1: record HIP events between the kernels of each encrypt call */
+
 int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** out);
 int pai_ctx_set_private(pai_ctx* ctx, const uint8_t* p_le, const uint8_t* q_le, size_t half_bytes);
 void pai_ctx_destroy(pai_ctx* ctx);
+/* Encryption with the private key set uses CRT over p^2, q^2 (same ciphertext bits, ~4x fewer
+ * multiply-accumulates); PAI_OPT_CRT_ENCRYPT = 0 forces the public-key kernel. */
+int pai_ctx_set_option(pai_ctx* ctx, int option, int value);
+int pai_ctx_get_option(const pai_ctx* ctx, int option, int* value);
+/* With PAI_OPT_STAGE_TIMING on: kernel durations (ms) of the last encrypt call's final chunk, in launch
+ * order (CRT: stage A, stage B, finish; public key: the one encrypt kernel). Waits for them. */
+int pai_ctx_stage_times(pai_ctx* ctx, float* ms_out, int max_out, int* count);
 /* key bits, 32-bit words per ciphertext (2*key_bits/32), words per plaintext (key_bits/32) */
 int pai_ctx_info(const pai_ctx* ctx, int* key_bits, int* ct_words, int* pt_words);
 const char* pai_last_error(void);

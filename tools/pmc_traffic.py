@@ -2,7 +2,7 @@
 """Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE counter CSVs (separate passes) into per-launch HBM
 bytes for one kernel, with the gfx950 correction of MI355X_MICROARCH.md §HBM: FETCH_SIZE reads
 half of the bytes of a wide coalesced stream (so it is doubled); WRITE_SIZE is taken as is. Both are
-in KiB. Writes profiles/pmc_encrypt_latest.json, which bench.py reports as roofline.traffic.
+in KiB. Writes profiles/pmc_<kernel>_latest.json, which bench.py reports as roofline.traffic.
 
     python tools/pmc_traffic.py FETCH.csv WRITE.csv --kernel k_encrypt --n 1048576 --nb 2048 [-o out.json]
 """
@@ -28,9 +28,11 @@ def main():
     ap.add_argument("--kernel", default="k_encrypt")
     ap.add_argument("--n", type=int, required=True)
     ap.add_argument("--nb", type=int, required=True)
-    ap.add_argument("-o", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                               "profiles", "pmc_encrypt_latest.json"))
+    ap.add_argument("-o", default=None, help="default: profiles/pmc_<kernel>_latest.json (read by bench.py)")
     a = ap.parse_args()
+    if a.o is None:
+        a.o = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                           f"pmc_{a.kernel}_latest.json")
     f, nf = per_launch(a.fetch_csv, "FETCH_SIZE", a.kernel)
     w, nw = per_launch(a.write_csv, "WRITE_SIZE", a.kernel)
     out = {"kernel": a.kernel, "n": a.n, "nb": a.nb,

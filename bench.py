@@ -38,8 +38,9 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 # Peak 32x32->64 multiply-accumulate issue rate of one MI355X: v_mad_u64_u32 lanes/s measured by
-# tools/microbench/int_throughput.hip (profiles/r01_step0_int_throughput.txt).
-INT_MAC_PEAK = float(os.environ.get("FLEXPAI_INT_MAC_PEAK", "31.94e12"))
+# tools/microbench/int_throughput.hip, 16 independent chains, 32 waves/CU, 3.9 ms runs
+# (profiles/r01_step0_int_throughput_long.txt).
+INT_MAC_PEAK = float(os.environ.get("FLEXPAI_INT_MAC_PEAK", "35.13e12"))
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 
 
@@ -95,6 +96,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-decrypt", action="store_true")
     ap.add_argument("--no-public", action="store_true", help="skip timing the public-key path beside CRT")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-boundary (PCIe, Python objects) rates")
+    ap.add_argument("--host-sample", type=int, default=1 << 16,
+                    help="elements for the Python-object (PaillierEncryptor.encrypt) rate")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -109,6 +113,7 @@ def main():
 
     from flex.crypto.paillier import _native
     from flex.crypto.paillier.keypair import generate_paillier_keypair
+    from flex.crypto.paillier.sharding import gather_shards, shard_bounds
 
     pk, sk = generate_paillier_keypair(args.nb, seed=1)
     ctx = _native.Context(pk.n, local_rank, sk.p, sk.q)
@@ -123,9 +128,9 @@ def main():
     ex = torch.empty(N, dtype=torch.int32, device=dev)
     st = torch.empty(N, dtype=torch.int32, device=dev)
     rng_key = hashlib.sha256(b"flexpai-bench-key").digest()
-    index_base = rank * N            # obfuscators keyed by the GLOBAL element index
+    total = world * N                 # weak scaling: N elements per GPU
+    index_base, _ = shard_bounds(total, world, rank)   # obfuscators keyed by the GLOBAL element index
     stream = torch.cuda.current_stream(dev)
-    gathered = torch.empty((world * N, W), dtype=torch.int32, device=dev) if world > 1 else None
 
     def encrypt(out):
         rc = lib.pai_encrypt_dev(ctx.handle, _native.PAI_F32, x.data_ptr(), N, 0, 0, _native.PAI_OBF_RNG,
@@ -137,7 +142,7 @@ def main():
     for _ in range(args.warmup):
         encrypt(ct)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, ct)
+            gather_shards(ct, total, world)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -148,7 +153,7 @@ def main():
         encrypt(ct)
         stage_ms.append(ctx.stage_times())     # HIP events recorded between this call's kernels
         if world > 1:
-            dist.all_gather_into_tensor(gathered, ct)
+            gathered = gather_shards(ct, total, world)   # RCCL all-gather over xGMI
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -200,6 +205,31 @@ def main():
         extra["roundtrip_exact"] = ok
         if not ok:
             raise SystemExit("decrypt(encrypt(x)) != x on the device")
+
+    # host boundary (DESIGN.md §Host boundary): plaintexts start in host numpy and ciphertexts leave as
+    # host buffers / PaillierEncryptedNumber objects; never part of `value`
+    if not args.no_host and rank == 0:
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        hct, hex_, _ = ctx.encrypt(x_host, obf_mode=_native.PAI_OBF_RNG, rng_key=rng_key, index_base=index_base)
+        t_host = time.perf_counter() - t1
+        hb = {"host_buffers_encrypts_per_s": N / t_host,
+              "host_buffers_note": "pai_encrypt: H2D float32 x, kernels, D2H ciphertext words "
+                                   f"({N * W * 4 / 2**20:.0f} MiB), pageable host memory",
+              "host_buffers_bit_identical": bool(np.array_equal(hct[: len(ct_host_check)], ct_host_check))}
+        from flex.crypto.paillier import _runtime
+        from flex.crypto.paillier.encryptor import PaillierEncryptor
+        _runtime.register_private(pk, sk)        # this process holds the key (CRT path, as above)
+        enc = PaillierEncryptor(pk)
+        hs = min(args.host_sample, N)
+        t1 = time.perf_counter()
+        objs = enc.encrypt(x_host[:hs])
+        t_obj = time.perf_counter() - t1
+        hb["python_objects_encrypts_per_s"] = hs / t_obj
+        hb["python_objects_note"] = (f"PaillierEncryptor.encrypt(ndarray[{hs}]) -> object ndarray of "
+                                     "PaillierEncryptedNumber (encryptor.py:99-114 API), incl. materialisation")
+        del objs
+        extra["host_boundary"] = hb
 
     if rank != 0:
         if world > 1:

@@ -164,17 +164,25 @@ static bool build_lane_program(const HBig& e, std::vector<uint32_t>& prog) {
   prog.clear();
   prog.push_back(op(LOP_SQR | LOP_STORE, 0, 0, 16));                   // x~^2       -> T16
   prog.push_back(op(LOP_A_FROM_T | LOP_STORE, 16, 0, 1));             // x~ * x~^2  -> T1
-  for (int k = 2; k < 16; ++k) prog.push_back(op(LOP_STORE, 16, 0, k));
+  for (int k = 2; k < 16; ++k) prog.push_back(op(LOP_STORE | LOP_B_READY, 16, 0, k));   // b = x~^2 kept
   bool loaded = false;
+  size_t first_sq = SIZE_MAX;   // first squaring since the last multiply (prefetch slot)
   for (size_t i = 0; i + 1 < sched.size(); i += 2) {
     const int nsq = sched[i], idx = sched[i + 1];
     for (int t = 0; t < nsq; ++t) {
+      if (first_sq == SIZE_MAX) first_sq = prog.size();
       prog.push_back(loaded ? op(LOP_SQR, 0, 0, 0) : op(LOP_SQR | LOP_A_FROM_T, 0, first, 0));
       loaded = true;
     }
     if (idx != 0xFFFF) {
-      prog.push_back(loaded ? op(0, idx, 0, 0) : op(LOP_A_FROM_T, idx, first, 0));
+      if (first_sq != SIZE_MAX) {
+        prog[first_sq] |= LOP_PREFETCH | ((uint32_t)idx << 8);
+        prog.push_back(op(LOP_B_READY, idx, 0, 0));
+      } else {
+        prog.push_back(loaded ? op(0, idx, 0, 0) : op(LOP_A_FROM_T, idx, first, 0));
+      }
       loaded = true;
+      first_sq = SIZE_MAX;
     }
   }
   return loaded;

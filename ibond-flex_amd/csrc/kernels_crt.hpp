@@ -22,7 +22,11 @@ namespace fpai {
 constexpr int LANE_BLOCK = 256;
 
 // op list of the lane machine (run_lane_program)
-enum : uint32_t { LOP_SQR = 1u, LOP_A_FROM_T = 2u, LOP_STORE = 4u, LOP_B_CONST = 8u };
+enum : uint32_t {
+  LOP_SQR = 1u, LOP_A_FROM_T = 2u, LOP_STORE = 4u, LOP_B_CONST = 8u,
+  LOP_PREFETCH = 16u,   // SQR op: load tile[bidx] into b before squaring (the next MUL's operand)
+  LOP_B_READY = 32u,    // MUL op: b already holds the operand (prefetched, or unchanged)
+};
 constexpr int LANE_NTILE = 17;   // 16 odd powers + x^2
 constexpr int KMAX_CHUNKS = 5;   // stage A reduces r of up to KMAX_CHUNKS * LB * SA bits
 constexpr int RBUF_WORDS = 160;  // per-lane staging of the ChaCha stream (stage A)
@@ -92,7 +96,9 @@ __device__ __forceinline__ void ltile_store(uint32_t* __restrict__ tl, int k, co
 
 // The lane machine: per op (wave-uniform, scalar-loaded)
 //   A_FROM_T : a <- tile[aidx]
-//   SQR      : a <- a^2 R^-1        else  a <- a * B R^-1 with B = const c1 (B_CONST) or tile[bidx]
+//   SQR      : a <- a^2 R^-1   (PREFETCH: first issue b <- tile[bidx], consumed by a later MUL, so
+//              the HBM/L2 latency of the table row hides behind the squarings)
+//   MUL      : a <- a * b R^-1 with b = const c1 (B_CONST), b as is (B_READY) or b <- tile[bidx]
 //   STORE    : tile[sidx] <- a
 // fields: bidx = op[15:8], aidx = op[23:16], sidx = op[31:24]. The kernel appends the final
 // product with c1.
@@ -101,17 +107,20 @@ __device__ __forceinline__ void run_lane_program(uint32_t (&a)[S], uint32_t* __r
                                                  const uint32_t* __restrict__ prog, int nprog,
                                                  const uint32_t* __restrict__ c1, const uint32_t (&m)[S],
                                                  uint32_t mprime) {
+  uint32_t b[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) b[j] = 0;
   for (int i = 0; i <= nprog; ++i) {
     const uint32_t op = (i < nprog) ? __builtin_amdgcn_readfirstlane(prog[i]) : LOP_B_CONST;
     if (op & LOP_A_FROM_T) ltile_load<S>(tl, (op >> 16) & 0xFF, a);
     if (op & LOP_SQR) {
+      if (op & LOP_PREFETCH) ltile_load<S>(tl, (op >> 8) & 0xFF, b);
       lane::mont_sqr<S>(a, m, mprime);
     } else {
-      uint32_t b[S];
       if (op & LOP_B_CONST) {
 #pragma unroll
         for (int j = 0; j < S; ++j) b[j] = c1[j];
-      } else {
+      } else if (!(op & LOP_B_READY)) {
         ltile_load<S>(tl, (op >> 8) & 0xFF, b);
       }
       lane::mont_mul<S>(a, b, m, mprime);

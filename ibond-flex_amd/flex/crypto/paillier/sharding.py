@@ -1,0 +1,38 @@
+"""Multi-GPU sharding of a Paillier array: one process per GPU, contiguous shards,
+obfuscators keyed by the GLOBAL element index (so the ciphertexts do not depend on the number of
+GPUs), one all-gather to reassemble. Elements are independent (flex/crypto/paillier/encryptor.py:71-97
+maps element-wise), so there is no other communication. The collective is torch.distributed:
+RCCL over xGMI on GPUs ("nccl" backend), gloo in the CPU tests.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+
+def shard_bounds(total: int, world: int, rank: int) -> Tuple[int, int]:
+    """[start, stop) of rank's contiguous block of ceil(total / world) elements (the last may be short)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad world/rank")
+    per = -(-total // world)
+    start = min(rank * per, total)
+    return start, min(start + per, total)
+
+
+def gather_shards(local, total: int, world: int, group=None):
+    """All-gather equal-size (padded) shards of a [rows, ...] tensor into the [total, ...] array."""
+    import torch
+    import torch.distributed as dist
+    per = -(-total // world)
+    if local.shape[0] > per:
+        raise ValueError("shard larger than ceil(total / world)")
+    if local.shape[0] < per:
+        pad = torch.zeros((per - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        local = torch.cat([local, pad])
+    out = torch.empty((world * per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    if local.is_cuda:
+        dist.all_gather_into_tensor(out, local.contiguous(), group=group)
+    else:
+        parts = list(out.chunk(world))
+        dist.all_gather(parts, local.contiguous(), group=group)
+        out = torch.cat(parts)
+    return out[:total]

@@ -198,6 +198,15 @@ def main():
             raise RuntimeError(lib.pai_last_error().decode())
         torch.cuda.synchronize()
         dec_ms = d0.elapsed_time(d1)
+        dst = ctx.stage_times()
+        if ctx.lane_decrypt and len(dst) == 3:
+            wd = work_dec(args.nb)
+            extra["decrypt_stages"] = {
+                "k_dec_pre": {"kernel_ms": dst[0]},
+                "k_dec_pow": {"kernel_ms": dst[1], "work_mac_per_elem": wd,
+                              "achieved_tmac_s": N * wd / (dst[1] * 1e-3) / 1e12},
+                "k_dec_fin": {"kernel_ms": dst[2]}}
+        extra["decrypt_path"] = "lane" if ctx.lane_decrypt else "group"
         ok = bool(torch.equal(val, x.double())) and int((stt > 1).sum().item()) == 0
         extra["decrypt_per_s_per_gpu"] = N / (dec_ms * 1e-3)
         extra["decrypt_kernel_ms"] = dec_ms

@@ -122,6 +122,38 @@ __device__ __forceinline__ void mont_mul(uint32_t (&a)[S], const uint32_t (&b)[S
   normalize<S>(P, a);
 }
 
+// a <- a b R^-1 mod m with the multiplier b in LDS, one column of 16-byte quads per lane:
+// limbs 4g..4g+3 at bq[g * BSTRIDE] (layout [quad][lane]: conflict-free ds_read_b128). Quad g+1 is
+// read while quad g's steps run, so the LDS latency hides behind the MACs and b never occupies
+// S VGPRs.
+template <int S, int BSTRIDE, int J>
+__device__ __forceinline__ void mul_step_lds(uint64_t (&P)[S], const uint32_t (&a)[S], uint4& cur, uint4& nxt,
+                                             const uint4* __restrict__ bq, const uint32_t (&m)[S], uint32_t mprime) {
+  if constexpr (J % 4 == 0) {
+    cur = nxt;
+    if constexpr (J / 4 + 1 < (S + 3) / 4) nxt = bq[(J / 4 + 1) * BSTRIDE];
+  }
+  const uint32_t bj = (J % 4 == 0) ? cur.x : (J % 4 == 1) ? cur.y : (J % 4 == 2) ? cur.z : cur.w;
+#pragma unroll
+  for (int i = 0; i < S; ++i) P[(i + J) % S] += (uint64_t)a[i] * bj;
+  reduce_step<S, J>(P, m, mprime);
+}
+template <int S, int BSTRIDE, int... Js>
+__device__ __forceinline__ void mul_all_lds(uint64_t (&P)[S], const uint32_t (&a)[S], const uint4* __restrict__ bq,
+                                            const uint32_t (&m)[S], uint32_t mprime, std::integer_sequence<int, Js...>) {
+  uint4 cur, nxt = bq[0];
+  (mul_step_lds<S, BSTRIDE, Js>(P, a, cur, nxt, bq, m, mprime), ...);
+}
+template <int S, int BSTRIDE>
+__device__ __forceinline__ void mont_mul_lds(uint32_t (&a)[S], const uint4* __restrict__ bq, const uint32_t (&m)[S],
+                                             uint32_t mprime) {
+  uint64_t P[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) P[i] = 0;
+  mul_all_lds<S, BSTRIDE>(P, a, bq, m, mprime, std::make_integer_sequence<int, S>{});
+  normalize<S>(P, a);
+}
+
 // d = a - b over S canonical limbs; returns the borrow out (true when a < b, d then wraps)
 template <int S>
 __device__ __forceinline__ bool sub(const uint32_t (&a)[S], const uint32_t (&b)[S], uint32_t (&d)[S]) {

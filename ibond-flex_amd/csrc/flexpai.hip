@@ -9,6 +9,8 @@
 #include "host_bignum.hpp"
 #include "kernels.hpp"
 #include "kernels_crt.hpp"
+#include "engine_dec.hpp"
+#include "engine_lane.hpp"
 
 using namespace fpai;
 
@@ -49,6 +51,14 @@ struct pai_ctx {
   CrtHalf* d_crt_a = nullptr;   // [2] stage A halves
   CrtHalf* d_crt_b = nullptr;   // [2] stage B halves
   uint32_t *d_kq = nullptr, *d_kp = nullptr;
+  // lane-engine CRT decryption (kernels_dec.hpp): same sizes as the CRT encryption halves
+  bool dec_lane_ok = false;
+  bool dec_lane_enabled = true;
+  int dec_kchunks = 0;
+  DecLaneHalf* d_dec_halves = nullptr;
+  CrtHalf* d_dec_pow = nullptr;   // [2] exponentiation halves: p_h^2, op list for p_h - 1
+  uint32_t *d_dec_p = nullptr, *d_dec_q = nullptr, *d_dec_qinvR = nullptr, *d_dec_nl = nullptr, *d_dec_maxint = nullptr;
+  uint32_t dec_pprime = 0;
   std::vector<void*> allocs;
   // scratch (exponent tables), grown on demand
   void* d_scratch = nullptr;
@@ -152,7 +162,7 @@ static bool build_modexp_program(const HBig& e, std::vector<uint32_t>& prog) {
 }
 
 // Op list for run_lane_program (kernels_crt.hpp): the kernel stores x~ in tile 0; odd powers into
-// tiles 0..15 (x~^2 kept in tile 16), then the sliding-window chain over e.
+// tiles 0..15 (x~^2 kept as the LDS multiplier), then the sliding-window chain over e.
 static bool build_lane_program(const HBig& e, std::vector<uint32_t>& prog) {
   if (e.bits() < 8) return false;
   std::vector<uint16_t> sched;
@@ -162,9 +172,9 @@ static bool build_lane_program(const HBig& e, std::vector<uint32_t>& prog) {
     return flags | ((uint32_t)bidx << 8) | ((uint32_t)aidx << 16) | ((uint32_t)sidx << 24);
   };
   prog.clear();
-  prog.push_back(op(LOP_SQR | LOP_STORE, 0, 0, 16));                   // x~^2       -> T16
-  prog.push_back(op(LOP_A_FROM_T | LOP_STORE, 16, 0, 1));             // x~ * x~^2  -> T1
-  for (int k = 2; k < 16; ++k) prog.push_back(op(LOP_STORE | LOP_B_READY, 16, 0, k));   // b = x~^2 kept
+  prog.push_back(op(LOP_SQR | LOP_B_SET, 0, 0, 0));                       // x~^2 -> LDS multiplier
+  prog.push_back(op(LOP_A_FROM_T | LOP_B_READY | LOP_STORE, 0, 0, 1));    // x~ * x~^2  -> T1
+  for (int k = 2; k < 16; ++k) prog.push_back(op(LOP_STORE | LOP_B_READY, 0, 0, k));   // multiplier x~^2 kept
   bool loaded = false;
   size_t first_sq = SIZE_MAX;   // first squaring since the last multiply (prefetch slot)
   for (size_t i = 0; i + 1 < sched.size(); i += 2) {
@@ -341,6 +351,49 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
   c->crt_sa = sa;
   c->crt_sb = sb;
   c->crt_ok = true;
+  // lane-engine decryption: x_h = c^(p_h - 1) mod p_h^2, L_h, m_h = L_h h_h mod p_h; CRT + decode
+  {
+    const int kd = (int)((32 * (size_t)c->ct_words + RB - 1) / RB);
+    if (kd > KMAX_CHUNKS) return 0;
+    DecLaneHalf dh[2];
+    CrtHalf ph_pow[2];
+    for (int h = 0; h < 2; ++h) {
+      const HBig& ph = primes[h];
+      const HBig& other = primes[1 - h];
+      const HBig& m2 = sq[h];
+      std::vector<uint32_t> pd;
+      if (!build_lane_program(sub(ph, HBig(1)), pd)) return 0;
+      // h_h = L(g^(p_h - 1) mod p_h^2, p_h)^-1 mod p_h = (-other)^-1 mod p_h (g = n + 1)
+      HBig oi = inv_mod(mod(other, ph), ph);
+      if (oi.is_zero()) return 0;
+      HBig hh = sub(ph, oi);
+      std::vector<uint32_t> one(sb, 0);
+      one[0] = 1;
+      uint32_t *dm2, *dck, *done, *dprog, *dph, *dhR, *dpm1;
+      if ((rc = upload(c, m2.limbs(sb, LB), &dm2)) ||
+          (rc = upload(c, mul_pow2_mod(HBig(1), RB * (kd + 1), m2).limbs(sb, LB), &dck)) ||
+          (rc = upload(c, one, &done)) || (rc = upload(c, pd, &dprog)) || (rc = upload(c, ph.limbs(sa, LB), &dph)) ||
+          (rc = upload(c, mul_pow2_mod(hh, RA, ph).limbs(sa, LB), &dhR)) ||
+          (rc = upload(c, sub(ph, HBig(1)).limbs(sa, LB), &dpm1)))
+        return rc;
+      const uint32_t mp1 = mont_prime(ph, LB), mp2 = mont_prime(m2, LB);
+      dh[h] = DecLaneHalf{dm2, dck, mp2, (0u - mp1) & LMASK, mp1, 0u, dph, dhR, dpm1};
+      ph_pow[h] = CrtHalf{dm2, nullptr, done, dprog, (int)pd.size(), mp2};
+    }
+    std::vector<DecLaneHalf> dv(dh, dh + 2);
+    std::vector<CrtHalf> pv(ph_pow, ph_pow + 2);
+    if ((rc = upload(c, pv, &c->d_dec_pow))) return rc;
+    HBig qinv = inv_mod(mod(q, p), p);
+    HBig maxint = sub(div_small(c->n, 3), HBig(1));   // keypair.py:29
+    if ((rc = upload(c, dv, &c->d_dec_halves)) || (rc = upload(c, p.limbs(sa, LB), &c->d_dec_p)) ||
+        (rc = upload(c, q.limbs(sa, LB), &c->d_dec_q)) ||
+        (rc = upload(c, mul_pow2_mod(qinv, RA, p).limbs(sa, LB), &c->d_dec_qinvR)) ||
+        (rc = upload(c, c->n.limbs(sb, LB), &c->d_dec_nl)) || (rc = upload(c, maxint.limbs(sb, LB), &c->d_dec_maxint)))
+      return rc;
+    c->dec_pprime = mont_prime(p, LB);
+    c->dec_kchunks = kd;
+    c->dec_lane_ok = true;
+  }
   return 0;
 }
 
@@ -409,6 +462,7 @@ int pai_ctx_set_option(pai_ctx* c, int option, int value) {
   switch (option) {
     case PAI_OPT_CRT_ENCRYPT: c->crt_enabled = value != 0; return 0;
     case PAI_OPT_STAGE_TIMING: c->timing = value != 0; c->nev = 0; return 0;
+    case PAI_OPT_LANE_DECRYPT: c->dec_lane_enabled = value != 0; return 0;
   }
   return fail(PAI_ERR_ARG, "pai_ctx_set_option: unknown option");
 }
@@ -419,6 +473,7 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
     case PAI_OPT_CRT_ENCRYPT: *value = c->crt_enabled ? 1 : 0; return 0;
     case PAI_OPT_CRT_AVAILABLE: *value = c->crt_ok ? 1 : 0; return 0;
     case PAI_OPT_STAGE_TIMING: *value = c->timing ? 1 : 0; return 0;
+    case PAI_OPT_LANE_DECRYPT: *value = (c->dec_lane_ok && c->dec_lane_enabled) ? 1 : 0; return 0;
   }
   return fail(PAI_ERR_ARG, "pai_ctx_get_option: unknown option");
 }
@@ -477,13 +532,15 @@ static int launch_crt_fin(pai_ctx* c, CrtFinParams& f, hipStream_t st) {
 
 template <int SA, int SB>
 static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
+  static_assert(SB == 2 * SA || SB == 2 * SA - 1, "stage sizes");
   const long long N = e.n;
   const int r_words = e.obf == PAI_OBF_GIVEN ? e.r_words : e.rng_words;
   const int kchunks = (32 * r_words + LB * SA - 1) / (LB * SA);
   if (kchunks > KMAX_CHUNKS || (e.obf == PAI_OBF_RNG && r_words > RBUF_WORDS))
     return fail(PAI_ERR_ARG, "CRT encrypt: obfuscator too wide");
   const long long chunk = std::min(N, CRT_CHUNK);
-  const int occA = blocks_per_cu(k_crt_a<SA>, LANE_BLOCK, 0), occB = blocks_per_cu(k_crt_b<SA, SB>, LANE_BLOCK, 0);
+  int occA = 1, occB = 1;
+  if (crt_lane_occupancy(SA, &occA, &occB)) return fail(PAI_ERR_KEY, "CRT encrypt: unsupported size");
   const long long lanes_blocks = (chunk + LANE_BLOCK - 1) / LANE_BLOCK;
   const int gxA = (int)std::max<long long>(1, std::min<long long>(lanes_blocks, (long long)occA * c->cus / 2));
   const int gxB = (int)std::max<long long>(1, std::min<long long>(lanes_blocks, (long long)occB * c->cus / 2));
@@ -511,7 +568,7 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
     pa.scratch = (uint32_t*)c->d_scratch;
     const int gA = (int)std::min<long long>(gxA, (n + LANE_BLOCK - 1) / LANE_BLOCK);
     stage_mark(c, 0, st);
-    hipLaunchKernelGGL(k_crt_a<SA>, dim3(gA, 2), dim3(LANE_BLOCK), 0, st, pa);
+    HIPCHK(crt_launch_a(SA, pa, gA, st));
     stage_mark(c, 1, st);
     HIPCHK(hipGetLastError());
     CrtParams pb{};
@@ -521,7 +578,7 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
     pb.out = u;
     pb.scratch = (uint32_t*)c->d_scratch;
     const int gB = (int)std::min<long long>(gxB, (n + LANE_BLOCK - 1) / LANE_BLOCK);
-    hipLaunchKernelGGL((k_crt_b<SA, SB>), dim3(gB, 2), dim3(LANE_BLOCK), 0, st, pb);
+    HIPCHK(crt_launch_b(SA, pb, gB, st));
     HIPCHK(hipGetLastError());
     stage_mark(c, 2, st);
     CrtFinParams f{};
@@ -645,6 +702,55 @@ static int launch_decrypt(pai_ctx* c, DecParams& p, hipStream_t st) {
   return 0;
 }
 
+// lane-engine decryption (kernels_dec.hpp, engine_dec.hip), in chunks of CRT_CHUNK elements
+static int launch_dec_lane(pai_ctx* c, const DecParams& d, hipStream_t st) {
+  const long long N = d.n;
+  const long long chunk = std::min(N, CRT_CHUNK);
+  DecLaneGeom g;
+  if (dec_lane_geometry(c->crt_sa, c->cus, chunk, &g)) return fail(PAI_ERR_KEY, "lane decrypt: unsupported size");
+  int rc = ensure_scratch(c, g.scratch_bytes);
+  if (rc) return rc;
+  const int SB = c->crt_sb;
+  if ((rc = ensure_work(c, (size_t)2 * SB * chunk * 4))) return rc;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  if (c->timing) {
+    for (int i = 0; i < 4; ++i) {
+      if (!c->ev[i]) HIPCHK(hipEventCreate(&c->ev[i]));
+      ev[i] = c->ev[i];
+    }
+    c->nev = 4;
+  }
+  for (long long off = 0; off < N; off += chunk) {
+    const long long n = std::min(chunk, N - off);
+    uint32_t* xw = (uint32_t*)c->d_work;   // [2][SB][n]: c~, then x_h in place
+    DecPreParams pre{c->d_dec_halves, n, d.ct + (size_t)off * c->ct_words, c->ct_words, c->dec_kchunks, xw};
+    CrtParams pw{};
+    pw.halves = c->d_dec_pow;
+    pw.n = n;
+    pw.yin = xw;
+    pw.out = xw;
+    pw.scratch = (uint32_t*)c->d_scratch;
+    DecFinParams f{};
+    f.halves = c->d_dec_halves;
+    f.n = n;
+    f.xh = xw;
+    f.exp = d.exp + off;
+    f.p = c->d_dec_p;
+    f.q = c->d_dec_q;
+    f.qinvR = c->d_dec_qinvR;
+    f.pprime = c->dec_pprime;
+    f.nlimb = c->d_dec_nl;
+    f.maxint = c->d_dec_maxint;
+    f.val = d.val + off;
+    f.mant = d.mant ? d.mant + off : nullptr;
+    f.status = d.status + off;
+    f.raw = d.raw ? d.raw + (size_t)off * c->pt_words : nullptr;
+    f.pt_words = c->pt_words;
+    HIPCHK(dec_lane_launch(c->crt_sa, pre, pw, f, g, st, ev));
+  }
+  return 0;
+}
+
 int pai_decrypt_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t N, double* d_val, int64_t* d_mant,
                     int32_t* d_status, uint32_t* d_raw, void* stream) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
@@ -671,6 +777,7 @@ int pai_decrypt_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size
   p.pt_words = c->pt_words;
   p.n_limbs = c->n_limbs;
   hipStream_t st = (hipStream_t)stream;
+  if (c->dec_lane_ok && c->dec_lane_enabled) return launch_dec_lane(c, p, st);
   switch (c->tpi_d) {
     case 1: return launch_decrypt<1>(c, p, st);
     case 2: return launch_decrypt<2>(c, p, st);
@@ -683,7 +790,7 @@ int pai_decrypt_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size
 struct DevScope {
   std::vector<void*> ptrs;
   ~DevScope() {
-    for (void* p : ptrs) hipFree(p);
+    for (void* p : ptrs) (void)hipFree(p);
   }
   template <typename T>
   T* alloc(size_t n) {

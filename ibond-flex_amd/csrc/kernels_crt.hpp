@@ -20,14 +20,20 @@
 namespace fpai {
 
 constexpr int LANE_BLOCK = 256;
+#ifndef FPAI_LANE_OCC
+#define FPAI_LANE_OCC 1
+#endif
+constexpr int LANE_OCC = FPAI_LANE_OCC;   // waves per SIMD the exponentiation kernels are built for
 
 // op list of the lane machine (run_lane_program)
 enum : uint32_t {
   LOP_SQR = 1u, LOP_A_FROM_T = 2u, LOP_STORE = 4u, LOP_B_CONST = 8u,
-  LOP_PREFETCH = 16u,   // SQR op: load tile[bidx] into b before squaring (the next MUL's operand)
-  LOP_B_READY = 32u,    // MUL op: b already holds the operand (prefetched, or unchanged)
+  LOP_PREFETCH = 16u,   // SQR op: start the DMA tile[bidx] -> LDS multiplier before squaring (the next
+                        // MUL's operand), so the HBM latency of the table row hides behind the squarings
+  LOP_B_READY = 32u,    // MUL op: the LDS multiplier already holds the operand (prefetched or kept)
+  LOP_B_SET = 64u,      // after the op: LDS multiplier <- a
 };
-constexpr int LANE_NTILE = 17;   // 16 odd powers + x^2
+constexpr int LANE_NTILE = 16;   // odd powers x^1 .. x^31
 constexpr int KMAX_CHUNKS = 5;   // stage A reduces r of up to KMAX_CHUNKS * LB * SA bits
 constexpr int RBUF_WORDS = 160;  // per-lane staging of the ChaCha stream (stage A)
 
@@ -57,81 +63,132 @@ struct CrtParams {
   uint32_t* scratch;        // per-lane tiles
 };
 
+// Per-lane scratch, interleaved across the lanes of the grid in 16-byte quads: quad g of lane l
+// lives at quad index g * NL + l (NL = lanes in the grid), so every wave access is 1 KiB
+// contiguous and the address is a wave-uniform row base plus the lane. Tile k = quads
+// [k TQ, (k+1) TQ) (TQ = ceil(S / 4)); stage A's ChaCha staging follows the tiles.
+template <int S>
+constexpr int tile_quads() { return (S + 3) / 4; }
 template <int S>
 constexpr size_t lane_scratch_words() {
-  return (size_t)LANE_NTILE * ((S + 3) & ~3) + RBUF_WORDS;
+  return ((size_t)LANE_NTILE * tile_quads<S>() + RBUF_WORDS / 4) * 4;
+}
+struct LaneScratch {
+  uint4* scratch;      // grid scratch base (wave-uniform)
+  uint32_t nl;         // lanes in the grid (wave-uniform)
+  uint32_t lid;        // this lane
+  __device__ __forceinline__ uint4& quad(int g) const { return scratch[(size_t)g * nl + lid]; }
+};
+__device__ __forceinline__ LaneScratch lane_scratch(uint32_t* scratch) {
+  const uint32_t nl = gridDim.x * gridDim.y * blockDim.x;
+  const uint32_t lid = (blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+  return LaneScratch{reinterpret_cast<uint4*>(scratch), nl, lid};
 }
 template <int S>
-__device__ __forceinline__ uint32_t* lane_tiles_s(uint32_t* scratch) {
-  const size_t lane_id = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
-  return scratch + lane_id * lane_scratch_words<S>();
+__device__ __forceinline__ void unpack_quad(const uint4 v, int g, uint32_t (&x)[S]) {
+  if (4 * g + 0 < S) x[4 * g + 0] = v.x;
+  if (4 * g + 1 < S) x[4 * g + 1] = v.y;
+  if (4 * g + 2 < S) x[4 * g + 2] = v.z;
+  if (4 * g + 3 < S) x[4 * g + 3] = v.w;
 }
 template <int S>
-__device__ __forceinline__ void ltile_load(const uint32_t* __restrict__ tl, int k, uint32_t (&x)[S]) {
-  constexpr int TR = (S + 3) & ~3;
-  const uint4* q = reinterpret_cast<const uint4*>(tl + k * TR);
+__device__ __forceinline__ uint4 pack_quad(const uint32_t (&x)[S], int g) {
+  uint4 v;
+  v.x = 4 * g + 0 < S ? x[4 * g + 0] : 0u;
+  v.y = 4 * g + 1 < S ? x[4 * g + 1] : 0u;
+  v.z = 4 * g + 2 < S ? x[4 * g + 2] : 0u;
+  v.w = 4 * g + 3 < S ? x[4 * g + 3] : 0u;
+  return v;
+}
+template <int S>
+__device__ __forceinline__ void ltile_load(const LaneScratch& t, int k, uint32_t (&x)[S]) {
+  constexpr int TQ = tile_quads<S>();
 #pragma unroll
-  for (int j = 0; j < TR / 4; ++j) {
-    const uint4 v = q[j];
-    if (4 * j + 0 < S) x[4 * j + 0] = v.x;
-    if (4 * j + 1 < S) x[4 * j + 1] = v.y;
-    if (4 * j + 2 < S) x[4 * j + 2] = v.z;
-    if (4 * j + 3 < S) x[4 * j + 3] = v.w;
-  }
+  for (int g = 0; g < TQ; ++g) unpack_quad<S>(t.quad(k * TQ + g), g, x);
 }
 template <int S>
-__device__ __forceinline__ void ltile_store(uint32_t* __restrict__ tl, int k, const uint32_t (&x)[S]) {
-  constexpr int TR = (S + 3) & ~3;
-  uint4* q = reinterpret_cast<uint4*>(tl + k * TR);
+__device__ __forceinline__ void ltile_store(const LaneScratch& t, int k, const uint32_t (&x)[S]) {
+  constexpr int TQ = tile_quads<S>();
 #pragma unroll
-  for (int j = 0; j < TR / 4; ++j) {
-    uint4 v;
-    v.x = 4 * j + 0 < S ? x[4 * j + 0] : 0u;
-    v.y = 4 * j + 1 < S ? x[4 * j + 1] : 0u;
-    v.z = 4 * j + 2 < S ? x[4 * j + 2] : 0u;
-    v.w = 4 * j + 3 < S ? x[4 * j + 3] : 0u;
-    q[j] = v;
-  }
+  for (int g = 0; g < TQ; ++g) t.quad(k * TQ + g) = pack_quad<S>(x, g);
+}
+// DMA tile k -> the LDS multiplier ([quad][lane] image, 16 bytes per lane per instruction; the
+// destination is the wave's 64-lane slice of quad row g). Completion: lds_dma_wait().
+template <int S>
+__device__ __forceinline__ void ltile_to_lds(const LaneScratch& t, int k, uint4* wave_row0) {
+  constexpr int TQ = tile_quads<S>();
+#pragma unroll
+  for (int g = 0; g < TQ; ++g)
+    __builtin_amdgcn_global_load_lds((const void*)&t.quad(k * TQ + g),
+                                     (__attribute__((address_space(3))) void*)(wave_row0 + g * LANE_BLOCK), 16, 0, 0);
+}
+__device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// One op of the list through the scalar cache. The compiler will not use s_load here (the kernel
+// stores to global memory, so it cannot prove the list invariant) and a vector load - or an LDS
+// read, which it orders behind any LDS-DMA in flight - would make every op wait vmcnt(0) and so
+// drain the multiplier prefetch. The list is written by the host before the launch and never
+// changes, so the scalar cache is coherent for it.
+__device__ __forceinline__ uint32_t lane_op(const uint32_t* __restrict__ prog, int i) {
+  uint32_t v;
+  asm volatile("s_load_dword %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(prog), "s"(i * 4));
+  return v;
 }
 
 // The lane machine: per op (wave-uniform, scalar-loaded)
 //   A_FROM_T : a <- tile[aidx]
-//   SQR      : a <- a^2 R^-1   (PREFETCH: first issue b <- tile[bidx], consumed by a later MUL, so
-//              the HBM/L2 latency of the table row hides behind the squarings)
-//   MUL      : a <- a * b R^-1 with b = const c1 (B_CONST), b as is (B_READY) or b <- tile[bidx]
+//   SQR      : a <- a^2 R^-1   (PREFETCH: first start the DMA tile[bidx] -> LDS multiplier)
+//   MUL      : a <- a * b R^-1 with b the LDS multiplier: const c1 (B_CONST), as is (B_READY) or
+//              tile[bidx] (DMA now)
 //   STORE    : tile[sidx] <- a
+//   B_SET    : LDS multiplier <- a
 // fields: bidx = op[15:8], aidx = op[23:16], sidx = op[31:24]. The kernel appends the final
-// product with c1.
+// product with c1. The multiplier never occupies VGPRs: MUL reads one limb per CIOS step from LDS.
 template <int S>
-__device__ __forceinline__ void run_lane_program(uint32_t (&a)[S], uint32_t* __restrict__ tl,
+__device__ __forceinline__ void run_lane_program(uint32_t (&a)[S], const LaneScratch& t,
                                                  const uint32_t* __restrict__ prog, int nprog,
                                                  const uint32_t* __restrict__ c1, const uint32_t (&m)[S],
                                                  uint32_t mprime) {
-  uint32_t b[S];
-#pragma unroll
-  for (int j = 0; j < S; ++j) b[j] = 0;
+  constexpr int TQ = tile_quads<S>();
+  __shared__ uint4 ldsb[TQ * LANE_BLOCK];
+  uint4* bcol = ldsb + threadIdx.x;
+  uint4* brow = ldsb + (threadIdx.x & ~63u);
   for (int i = 0; i <= nprog; ++i) {
-    const uint32_t op = (i < nprog) ? __builtin_amdgcn_readfirstlane(prog[i]) : LOP_B_CONST;
-    if (op & LOP_A_FROM_T) ltile_load<S>(tl, (op >> 16) & 0xFF, a);
+    const uint32_t op = (i < nprog) ? lane_op(prog, i) : LOP_B_CONST;
+    if (op & LOP_A_FROM_T) {
+      ltile_load<S>(t, (op >> 16) & 0xFF, a);
+      // consume the loads here, inside the branch: otherwise the shared SQR/MUL code below starts
+      // with the wait for them, which (vmcnt counts in order) also drains a prefetch DMA
+#pragma unroll
+      for (int j = 0; j < S; ++j) asm volatile("" : "+v"(a[j]));
+    }
     if (op & LOP_SQR) {
-      if (op & LOP_PREFETCH) ltile_load<S>(tl, (op >> 8) & 0xFF, b);
+      if (op & LOP_PREFETCH) ltile_to_lds<S>(t, (op >> 8) & 0xFF, brow);
       lane::mont_sqr<S>(a, m, mprime);
     } else {
       if (op & LOP_B_CONST) {
+        uint32_t cv[S];
 #pragma unroll
-        for (int j = 0; j < S; ++j) b[j] = c1[j];
+        for (int j = 0; j < S; ++j) cv[j] = c1[j];
+#pragma unroll
+        for (int g = 0; g < TQ; ++g) bcol[g * LANE_BLOCK] = pack_quad<S>(cv, g);
       } else if (!(op & LOP_B_READY)) {
-        ltile_load<S>(tl, (op >> 8) & 0xFF, b);
+        ltile_to_lds<S>(t, (op >> 8) & 0xFF, brow);
       }
-      lane::mont_mul<S>(a, b, m, mprime);
+      lds_dma_wait();
+      lane::mont_mul_lds<S, LANE_BLOCK>(a, bcol, m, mprime);
     }
-    if (op & LOP_STORE) ltile_store<S>(tl, op >> 24, a);
+    if (op & LOP_STORE) ltile_store<S>(t, op >> 24, a);
+    if (op & LOP_B_SET) {
+#pragma unroll
+      for (int g = 0; g < TQ; ++g) bcol[g * LANE_BLOCK] = pack_quad<S>(a, g);
+    }
   }
 }
 
 // ---------------------------------------------------------------- stage A: y_h = r^(e_h) mod p_h
 template <int SA>
-__global__ __launch_bounds__(LANE_BLOCK, 1) void k_crt_a(CrtParams p) {
+__global__ __launch_bounds__(LANE_BLOCK, LANE_OCC) void k_crt_a(CrtParams p) {
   const int half = blockIdx.y;
   const CrtHalf* H = p.halves + half;
   uint32_t m[SA];
@@ -142,24 +199,30 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_crt_a(CrtParams p) {
   const uint32_t* prog = H->prog;
   const uint32_t* c1 = H->c1;
   const uint32_t* cK = H->c0 + (size_t)(p.kchunks - 1) * SA;    // R^(K+1) mod p_h
-  uint32_t* tl = lane_tiles_s<SA>(p.scratch);
-  uint32_t* rbuf = tl + (size_t)LANE_NTILE * ((SA + 3) & ~3);
+  const LaneScratch tl = lane_scratch(p.scratch);
   for (long long base = (long long)blockIdx.x * LANE_BLOCK; base < p.n; base += (long long)gridDim.x * LANE_BLOCK) {
     const long long i = base + threadIdx.x;
     const long long ii = i < p.n ? i : p.n - 1;
-    const uint32_t* rw;
-    if (p.obf == 1) {
-      rw = p.r + ii * p.r_stride;
-    } else {
+    // r words: the caller's (GIVEN) or this element's ChaCha stream staged in the lane scratch
+    const bool given = p.obf == 1;
+    const uint32_t* rg = p.r + (given ? ii * p.r_stride : 0);
+    if (!given) {
       const unsigned long long g = p.index_base + (unsigned long long)ii;
       for (int b = 0; b * 16 < p.r_words; ++b) {
         uint32_t blk[16];
         chacha20_block(p.rng_key, (uint32_t)b, (uint32_t)g, (uint32_t)(g >> 32), 0x66786169u, blk);
 #pragma unroll
-        for (int w = 0; w < 16; ++w) rbuf[b * 16 + w] = blk[w];
+        for (int w = 0; w < 4; ++w)
+          tl.quad(LANE_NTILE * tile_quads<SA>() + b * 4 + w) =
+              make_uint4(blk[4 * w], blk[4 * w + 1], blk[4 * w + 2], blk[4 * w + 3]);
       }
-      rw = rbuf;
     }
+    auto rw = [&](int wi) -> uint32_t {
+      if (given) return rg[wi];
+      const uint4 v = tl.quad(LANE_NTILE * tile_quads<SA>() + (wi >> 2));
+      const int c = wi & 3;
+      return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
+    };
     // x~ = r R mod p_h: K CIOS passes over the SA-limb chunks of r with a = R^(K+1) mod p_h
     // (invariant T < a + p_h < 2 p_h for any digits < 2^LB)
     uint32_t a[SA];
@@ -174,8 +237,8 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_crt_a(CrtParams p) {
 #pragma unroll
         for (int j = 0; j < SA; ++j) {
           const int bit = (k * SA + j) * lane::LB, wi = bit >> 5, sh = bit & 31;
-          const uint64_t lo = wi < nw ? (uint64_t)rw[wi] : 0ull;
-          const uint64_t hi = wi + 1 < nw ? (uint64_t)rw[wi + 1] : 0ull;
+          const uint64_t lo = wi < nw ? (uint64_t)rw(wi) : 0ull;
+          const uint64_t hi = wi + 1 < nw ? (uint64_t)rw(wi + 1) : 0ull;
           b[j] = (uint32_t)(((hi << 32) | lo) >> sh) & lane::LMASK;
           cst[j] = cK[j];
         }
@@ -195,7 +258,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_crt_a(CrtParams p) {
 
 // ---------------------------------------------------------------- stage B: u_h = y^(p_h) * coef mod p_h^2
 template <int SA, int SB>
-__global__ __launch_bounds__(LANE_BLOCK, 1) void k_crt_b(CrtParams p) {
+__global__ __launch_bounds__(LANE_BLOCK, LANE_OCC) void k_crt_b(CrtParams p) {
   const int half = blockIdx.y;
   const CrtHalf* H = p.halves + half;
   uint32_t m[SB];
@@ -205,7 +268,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_crt_b(CrtParams p) {
   const int nprog = H->nprog;
   const uint32_t* prog = H->prog;
   const uint32_t* c1 = H->c1;
-  uint32_t* tl = lane_tiles_s<SB>(p.scratch);
+  const LaneScratch tl = lane_scratch(p.scratch);
   for (long long base = (long long)blockIdx.x * LANE_BLOCK; base < p.n; base += (long long)gridDim.x * LANE_BLOCK) {
     const long long i = base + threadIdx.x;
     const long long ii = i < p.n ? i : p.n - 1;

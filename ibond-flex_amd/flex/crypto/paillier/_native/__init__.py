@@ -20,7 +20,7 @@ PAI_OBF_NONE, PAI_OBF_GIVEN, PAI_OBF_RNG = 0, 1, 2
 PAI_EXP_AUTO, PAI_EXP_FIXED = 0, 1
 EL_OK, EL_INT, EL_INT_BIG, EL_OVERFLOW, EL_FLOAT_OVF, EL_ENC_RANGE = 0, 1, 2, 3, 4, 5
 
-PAI_OPT_CRT_ENCRYPT, PAI_OPT_CRT_AVAILABLE, PAI_OPT_STAGE_TIMING = 1, 2, 3
+PAI_OPT_CRT_ENCRYPT, PAI_OPT_CRT_AVAILABLE, PAI_OPT_STAGE_TIMING, PAI_OPT_LANE_DECRYPT = 1, 2, 3, 4
 
 EXPORTED = ("pai_ctx_create", "pai_ctx_set_private", "pai_ctx_destroy", "pai_ctx_info", "pai_last_error",
             "pai_ctx_set_option", "pai_ctx_get_option", "pai_ctx_stage_times",
@@ -140,6 +140,14 @@ class Context:
         """Encrypt through the private-key CRT kernels (default when available) or the public-key one.
         The ciphertext bits are identical either way."""
         _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_CRT_ENCRYPT, 1 if enabled else 0))
+
+    @property
+    def lane_decrypt(self) -> bool:
+        """True when decrypt runs on the lane engine (kernels_dec.hpp), False for the lane-group kernel."""
+        return bool(self._get_option(PAI_OPT_LANE_DECRYPT))
+
+    def set_lane_decrypt(self, enabled: bool):
+        _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_LANE_DECRYPT, 1 if enabled else 0))
 
     def close(self):
         if getattr(self, "_h", None):

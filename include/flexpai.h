@@ -70,7 +70,9 @@ typedef struct pai_ctx pai_ctx;
 /* context options */
 #define PAI_OPT_CRT_ENCRYPT 1    /* 1 (default): encrypt via the private-key CRT path when available */
 #define PAI_OPT_CRT_AVAILABLE 2  /* read-only: 1 when the private key is set and the CRT kernels fit */
-#define PAI_OPT_STAGE_TIMING 3   /* 1: record HIP events between the kernels of each encrypt call */
+#define PAI_OPT_STAGE_TIMING 3   /* 1: record HIP events between the kernels of each encrypt/decrypt call */
+#define PAI_OPT_LANE_DECRYPT 4   /* 1 (default): decrypt on the lane engine when the key halves fit it;
+                                    0: lane-group kernel. Read back: 1 when the lane path is in use  */
 
 int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** out);
 int pai_ctx_set_private(pai_ctx* ctx, const uint8_t* p_le, const uint8_t* q_le, size_t half_bytes);

@@ -67,6 +67,19 @@ def work_crt(nb: int) -> dict:
             "k_crt_fin": float(3 * _M(nb // 16))}                  # (u_p q^2 + u_q p^2) * c0 mod n^2
 
 
+def fb_digit_count(nb: int, window: int) -> int:
+    """Exponent digits K of the fixed-base sampler: window-bit digits of an (nb/2 + 64)-bit exponent."""
+    return -(-(nb // 2 + 64) // window)
+
+
+def work_fb(nb: int, digits: int) -> dict:
+    """Per-element canonical MACs of the fixed-base path (kernels_fb.hpp): per half K - 1 table
+    products + 1 coefficient product mod p_h^2, no squarings; the ChaCha digit kernel does no MACs."""
+    return {"k_fb_digits": 0.0,
+            "k_fb": float(2 * digits * _M(nb // 32)),
+            "k_crt_fin": float(3 * _M(nb // 16))}
+
+
 def work_dec(nb: int) -> float:
     return float(2 * (_P(nb // 2) + 2) * _M(nb // 32))
 
@@ -91,6 +104,8 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 20, help="elements per GPU")
     ap.add_argument("--nb", type=int, default=2048, help="Paillier key bits")
     ap.add_argument("--path", choices=("crt", "public"), default="crt")
+    ap.add_argument("--obf", choices=("fixedbase", "generic"), default="fixedbase",
+                    help="device-RNG sampler of r^n on the CRT path (kernels_fb.hpp vs r from ChaCha20)")
     ap.add_argument("--cpu-sample", type=int, default=16384)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -119,6 +134,10 @@ def main():
     ctx = _native.Context(pk.n, local_rank, sk.p, sk.q)
     use_crt = args.path == "crt" and ctx.crt_available
     ctx.set_crt(use_crt)
+    use_fb = use_crt and args.obf == "fixedbase"
+    ctx.set_fixed_base(use_fb)
+    use_fb = use_fb and ctx.fixed_base
+    fb_info = ctx.fixed_base_info() if use_fb else None
     ctx.set_stage_timing(True)
     lib = _native.load_library()
     N, W = args.n, ctx.ct_words
@@ -164,11 +183,34 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     stage_avg = [float(np.mean([s[i] for s in stage_ms])) for i in range(len(stage_ms[0]))]
-    ct_host_check = ct[: min(N, args.cpu_sample)].cpu().numpy().view(np.uint32).copy()
-    ex_host_check = ex[: min(N, args.cpu_sample)].cpu().numpy().copy()
+    S_chk = min(N, args.cpu_sample)
+    ct_timed_check = ct[:S_chk].cpu().numpy().view(np.uint32).copy()
+    ex_timed_check = ex[:S_chk].cpu().numpy().copy()
 
     extra = {}
-    # the other path on the same input (untimed region), for the record and as a parity check
+    # Fixed-base sampling (kernels_fb.hpp) draws r^n directly, so its ciphertexts are not the ones of
+    # the ChaCha r stream; the generic CRT path on the same input (untimed) is the bit-reproducible
+    # reference the public-key kernel and the GMP CPU baseline are compared with.
+    ct_ref = ct
+    if use_fb:
+        ct_ref = torch.empty_like(ct)
+        ctx.set_fixed_base(False)
+        encrypt(ct_ref)
+        encrypt(ct_ref)
+        gen_ms = ctx.stage_times()
+        ctx.set_fixed_base(True)
+        torch.cuda.synchronize()
+        wc = work_crt(args.nb)
+        extra["generic_crt_path"] = {
+            "value": N / (sum(gen_ms) * 1e-3), "unit": "encrypts/s per GPU",
+            "note": "r from the ChaCha20 stream and r^n by CRT exponentiation (kernels_crt.hpp); "
+                    "bit-identical to the public-key kernel and the GMP baseline",
+            "stages_ms": dict(zip(["k_crt_a", "k_crt_b", "k_crt_fin"], gen_ms)),
+            "k_crt_b_int_mac_frac": N * wc["k_crt_b"] / (gen_ms[1] * 1e-3) / INT_MAC_PEAK if len(gen_ms) > 1 else None}
+    ct_host_check = ct_ref[:S_chk].cpu().numpy().view(np.uint32).copy()
+    ex_host_check = ex[:S_chk].cpu().numpy().copy()
+
+    # the public-key path on the same input (untimed region), for the record and as a parity check
     if use_crt and not args.no_public:
         ct2 = torch.empty_like(ct)
         ctx.set_crt(False)
@@ -176,7 +218,7 @@ def main():
         pub_ms = ctx.stage_times()[0]
         ctx.set_crt(True)
         torch.cuda.synchronize()
-        same = bool(torch.equal(ct2, ct))
+        same = bool(torch.equal(ct2, ct_ref))
         extra["public_key_path"] = {"value": N / (pub_ms * 1e-3), "unit": "encrypts/s per GPU",
                                     "kernel": "k_encrypt", "kernel_ms": pub_ms,
                                     "int_mac_frac": N * work_enc_public(args.nb) / (pub_ms * 1e-3) / INT_MAC_PEAK,
@@ -225,7 +267,7 @@ def main():
         hb = {"host_buffers_encrypts_per_s": N / t_host,
               "host_buffers_note": "pai_encrypt: H2D float32 x, kernels, D2H ciphertext words "
                                    f"({N * W * 4 / 2**20:.0f} MiB), pageable host memory",
-              "host_buffers_bit_identical": bool(np.array_equal(hct[: len(ct_host_check)], ct_host_check))}
+              "host_buffers_bit_identical": bool(np.array_equal(hct[: len(ct_timed_check)], ct_timed_check))}
         from flex.crypto.paillier import _runtime
         from flex.crypto.paillier.encryptor import PaillierEncryptor
         _runtime.register_private(pk, sk)        # this process holds the key (CRT path, as above)
@@ -247,8 +289,12 @@ def main():
 
     value = world * N * args.steps / elapsed
     if use_crt:
-        names = ["k_crt_a", "k_crt_b", "k_crt_fin"]
-        works = work_crt(args.nb)
+        if use_fb:
+            names = ["k_fb_digits", "k_fb", "k_crt_fin"]
+            works = work_fb(args.nb, fb_info[2])
+        else:
+            names = ["k_crt_a", "k_crt_b", "k_crt_fin"]
+            works = work_crt(args.nb)
         stages = {nm: {"kernel_ms": ms, "work_mac_per_elem": works[nm],
                        "achieved_tmac_s": N * works[nm] / (ms * 1e-3) / 1e12}
                   for nm, ms in zip(names, stage_avg)}
@@ -261,7 +307,10 @@ def main():
         total_work = dom_work
     achieved = N * dom_work / (dom_ms * 1e-3)
     alg_bytes = 4 + W * 4 + 4     # x in, ciphertext out, exponent out (r generated on the device)
-    extra["path"] = "crt" if use_crt else "public"
+    extra["path"] = ("crt-fixedbase" if use_fb else "crt") if use_crt else "public"
+    if use_fb:
+        extra["fixed_base"] = {"g_p": fb_info[0], "g_q": fb_info[1], "digits": fb_info[2],
+                               "window_bits": fb_info[3] if len(fb_info) > 3 else 8}
     extra["encrypt_call_ms"] = float(sum(stage_avg))
     extra["path_int_mac_frac"] = N * total_work / (sum(stage_avg) * 1e-3) / INT_MAC_PEAK
     extra["hbm_algorithmic_gbs"] = N * alg_bytes / (sum(stage_avg) * 1e-3) / 1e9
@@ -283,6 +332,17 @@ def main():
                    "gpu_bit_exact_on_sample": same}
             if not same:
                 raise SystemExit("GPU ciphertexts differ from the GMP oracle on the CPU sample")
+            if use_fb:
+                # the timed (fixed-base) ciphertexts against the oracle's restatement of the sampler
+                from oracle import paillier_oracle as O
+                okey = O.Key(pk.n, sk.p, sk.q)
+                idx = sorted({0, 1, S_chk // 2, S_chk - 1})
+                got = _native.words_to_ints(ct_timed_check[idx])
+                fb_ok = all(O.fb_encrypt_value(x_host[i], okey, rng_key, index_base + i, fb_info)
+                            == (got[j], int(ex_timed_check[i])) for j, i in enumerate(idx))
+                cpu["fixed_base_bit_exact_vs_oracle"] = {"elements": idx, "ok": fb_ok}
+                if not fb_ok:
+                    raise SystemExit("fixed-base ciphertexts differ from the oracle restatement")
 
     out = {
         "metric": "Paillier-2048 encrypts/sec (device-resident), 1M-elem float32 array" if args.nb == 2048
@@ -300,7 +360,7 @@ def main():
         "data": "synthetic: numpy default_rng(rank).standard_normal float32; seeded key "
                 "generate_paillier_keypair(nb, seed=1); device ChaCha20 obfuscators keyed by global index",
         "config": {"workload": f"Paillier n={args.nb} encrypt of a {N}-element float32 vector per GPU, "
-                               f"device-resident, key holder ({'CRT' if use_crt else 'public-key'} path)"
+                               f"device-resident, key holder ({('CRT, fixed-base r^n sampler' if use_fb else 'CRT') if use_crt else 'public-key'} path)"
                                + (", RCCL all-gather of ciphertext shards" if world > 1 else ""),
                    "key_bits": args.nb, "elements_per_gpu": N, "parallelism": f"dp{world}"},
         "roofline": {"bound": "valu-int-mac", "achieved": achieved / 1e12, "peak": INT_MAC_PEAK / 1e12,

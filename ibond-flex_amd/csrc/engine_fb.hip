@@ -1,0 +1,34 @@
+// Fixed-base obfuscation kernels (kernels_fb.hpp): instantiations and launches.
+#include "engine_fb.hpp"
+
+namespace fpai {
+
+int fb_occupancy(int sb, int* occ) {
+  hipError_t e;
+  if (sb == 37) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, k_fb<37>, LANE_BLOCK, 0);
+  else if (sb == 74) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, k_fb<74>, LANE_BLOCK, 0);
+  else return -1;
+  if (e != hipSuccess || *occ < 1) *occ = 1;
+  return 0;
+}
+
+hipError_t fb_launch(int sb, const FbParams& p, int gx, hipStream_t st) {
+  if (sb == 37) hipLaunchKernelGGL(k_fb<37>, dim3(gx, 2), dim3(LANE_BLOCK), 0, st, p);
+  else if (sb == 74) hipLaunchKernelGGL(k_fb<74>, dim3(gx, 2), dim3(LANE_BLOCK), 0, st, p);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t fb_launch_digits(const FbDigitParams& p, int gx, hipStream_t st) {
+  hipLaunchKernelGGL(k_fb_digits<FB_W>, dim3(gx, 2), dim3(LANE_BLOCK), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t fb_build_tables(int sb, const FbHalf* d_halves, uint4* t0, uint4* t1, int K, hipStream_t st) {
+  if (sb == 37) hipLaunchKernelGGL(k_fb_table<37>, dim3(K, 2), dim3(FB_ENT), 0, st, d_halves, t0, t1, K);
+  else if (sb == 74) hipLaunchKernelGGL(k_fb_table<74>, dim3(K, 2), dim3(FB_ENT), 0, st, d_halves, t0, t1, K);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+}  // namespace fpai

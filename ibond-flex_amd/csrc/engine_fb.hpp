@@ -1,0 +1,14 @@
+// Host interface of the fixed-base obfuscation translation unit (engine_fb.hip).
+#pragma once
+#include "kernels_fb.hpp"
+
+namespace fpai {
+
+// blocks per CU of k_fb<sb>; -1 if sb is unsupported (37: 1024-bit keys, 74: 2048-bit keys)
+int fb_occupancy(int sb, int* occ);
+hipError_t fb_launch(int sb, const FbParams& p, int gx, hipStream_t st);
+hipError_t fb_launch_digits(const FbDigitParams& p, int gx, hipStream_t st);
+// builds both halves' tables (K digit positions) on `st`
+hipError_t fb_build_tables(int sb, const FbHalf* d_halves, uint4* t0, uint4* t1, int K, hipStream_t st);
+
+}  // namespace fpai

@@ -11,6 +11,7 @@
 #include "kernels_crt.hpp"
 #include "engine_dec.hpp"
 #include "engine_lane.hpp"
+#include "engine_fb.hpp"
 
 using namespace fpai;
 
@@ -59,6 +60,12 @@ struct pai_ctx {
   CrtHalf* d_dec_pow = nullptr;   // [2] exponentiation halves: p_h^2, op list for p_h - 1
   uint32_t *d_dec_p = nullptr, *d_dec_q = nullptr, *d_dec_qinvR = nullptr, *d_dec_nl = nullptr, *d_dec_maxint = nullptr;
   uint32_t dec_pprime = 0;
+  // fixed-base obfuscation (kernels_fb.hpp): device-RNG encryption for key holders
+  bool fb_ok = false;
+  bool fb_enabled = true;
+  int fb_K = 0;
+  FbHalf* d_fb_halves = nullptr;
+  uint32_t fb_g[2] = {0, 0};   // the bases g_p, g_q (generators of Z_p*, Z_q*)
   std::vector<void*> allocs;
   // scratch (exponent tables), grown on demand
   void* d_scratch = nullptr;
@@ -294,6 +301,65 @@ int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** ou
   return 0;
 }
 
+// Fixed-base obfuscation setup (kernels_fb.hpp): the smallest g >= 2 that generates Z_P* as far as
+// the prime factors of P - 1 below 2^16 can tell (g^((P-1)/l) != 1 for each); a large prime
+// factor l of P - 1 that g misses has probability < 2^-16 each. G = g^n mod P^2.
+static uint32_t fb_base(const HBig& P) {
+  static const std::vector<uint32_t> primes = small_primes(1u << 16);
+  const HBig pm1 = sub(P, HBig(1));
+  std::vector<HBig> cof;
+  for (uint32_t l : primes)
+    if (mod_small(pm1, l) == 0) cof.push_back(div_small(pm1, l));
+  HMont M(P);
+  for (uint32_t g = 2; g < 1000000u; ++g) {
+    bool ok = true;
+    for (const HBig& e : cof)
+      if (cmp(M.pow(HBig(g), e), HBig(1)) == 0) {
+        ok = false;
+        break;
+      }
+    if (ok) return g;
+  }
+  return 0;
+}
+
+static int setup_fb(pai_ctx* c, const HBig primes[2], const HBig sq[2], int sb, size_t RB,
+                    const std::vector<uint32_t>* coef_limbs) {
+  c->fb_ok = false;
+  if (sb != 37 && sb != 74) return 0;
+  const size_t eb = std::max(primes[0].bits(), primes[1].bits()) + 64;
+  const int K = (int)((eb + FB_W - 1) / FB_W);
+  if (K > FB_MAX_K) return 0;
+  const int TQ = (sb + 3) / 4;
+  FbHalf hv[2];
+  int rc;
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t g = fb_base(primes[h]);
+    if (!g) return 0;
+    c->fb_g[h] = g;
+    HMont M2(sq[h]);
+    const HBig G = M2.pow(HBig(g), c->n);
+    uint32_t *dm, *dc1, *dgR, *done;
+    uint4* dtab;
+    if ((rc = upload(c, sq[h].limbs(sb, LB), &dm)) || (rc = upload(c, coef_limbs[h], &dc1)) ||
+        (rc = upload(c, mul_pow2_mod(G, RB, sq[h]).limbs(sb, LB), &dgR)) ||
+        (rc = upload(c, mul_pow2_mod(HBig(1), RB, sq[h]).limbs(sb, LB), &done)))
+      return rc;
+    void* t = nullptr;
+    HIPCHK(hipMalloc(&t, (size_t)K * FB_ENT * TQ * sizeof(uint4)));
+    c->allocs.push_back(t);
+    dtab = (uint4*)t;
+    hv[h] = FbHalf{dtab, dm, dc1, dgR, done, mont_prime(sq[h], LB)};
+  }
+  std::vector<FbHalf> v(hv, hv + 2);
+  if ((rc = upload(c, v, &c->d_fb_halves))) return rc;
+  HIPCHK(fb_build_tables(sb, c->d_fb_halves, (uint4*)hv[0].table, (uint4*)hv[1].table, K, nullptr));
+  HIPCHK(hipDeviceSynchronize());
+  c->fb_K = K;
+  c->fb_ok = true;
+  return 0;
+}
+
 // CRT encryption constants (kernels_crt.hpp). p < q here (sorted like keypair.py:57-62).
 static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
   c->crt_ok = false;
@@ -311,6 +377,7 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
   const HBig primes[2] = {p, q};
   const HBig sq[2] = {mul(p, p), mul(q, q)};
   CrtHalf ha[2], hb[2];
+  std::vector<uint32_t> coef_limbs[2];
   int rc;
   for (int h = 0; h < 2; ++h) {
     const HBig& ph = primes[h];
@@ -335,6 +402,7 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
     const HBig& m2 = sq[h];
     HBig coef = inv_mod(sq[1 - h], m2);
     if (coef.is_zero()) return 0;
+    coef_limbs[h] = coef.limbs(sb, LB);
     uint32_t *dm2, *dr2, *dcoef, *dpb;
     if ((rc = upload(c, m2.limbs(sb, LB), &dm2)) ||
         (rc = upload(c, mul_pow2_mod(HBig(1), 2 * RB, m2).limbs(sb, LB), &dr2)) ||
@@ -351,6 +419,7 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
   c->crt_sa = sa;
   c->crt_sb = sb;
   c->crt_ok = true;
+  if ((rc = setup_fb(c, primes, sq, sb, RB, coef_limbs))) return rc;
   // lane-engine decryption: x_h = c^(p_h - 1) mod p_h^2, L_h, m_h = L_h h_h mod p_h; CRT + decode
   {
     const int kd = (int)((32 * (size_t)c->ct_words + RB - 1) / RB);
@@ -463,6 +532,7 @@ int pai_ctx_set_option(pai_ctx* c, int option, int value) {
     case PAI_OPT_CRT_ENCRYPT: c->crt_enabled = value != 0; return 0;
     case PAI_OPT_STAGE_TIMING: c->timing = value != 0; c->nev = 0; return 0;
     case PAI_OPT_LANE_DECRYPT: c->dec_lane_enabled = value != 0; return 0;
+    case PAI_OPT_FIXED_BASE: c->fb_enabled = value != 0; return 0;
   }
   return fail(PAI_ERR_ARG, "pai_ctx_set_option: unknown option");
 }
@@ -474,6 +544,7 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
     case PAI_OPT_CRT_AVAILABLE: *value = c->crt_ok ? 1 : 0; return 0;
     case PAI_OPT_STAGE_TIMING: *value = c->timing ? 1 : 0; return 0;
     case PAI_OPT_LANE_DECRYPT: *value = (c->dec_lane_ok && c->dec_lane_enabled) ? 1 : 0; return 0;
+    case PAI_OPT_FIXED_BASE: *value = (c->fb_ok && c->fb_enabled) ? 1 : 0; return 0;
   }
   return fail(PAI_ERR_ARG, "pai_ctx_get_option: unknown option");
 }
@@ -487,6 +558,15 @@ int pai_ctx_stage_times(pai_ctx* c, float* ms_out, int max_out, int* count) {
   const int k = std::min(c->nev - 1, max_out);
   for (int i = 0; i < k; ++i) HIPCHK(hipEventElapsedTime(&ms_out[i], c->ev[i], c->ev[i + 1]));
   *count = k;
+  return 0;
+}
+
+int pai_ctx_fixed_base_info(const pai_ctx* c, uint32_t* g_p, uint32_t* g_q, int* digits) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (!c->fb_ok) return fail(PAI_ERR_NOPRIV, "fixed-base obfuscation not available (needs the private key)");
+  if (g_p) *g_p = c->fb_g[0];
+  if (g_q) *g_q = c->fb_g[1];
+  if (digits) *digits = c->fb_K;
   return 0;
 }
 
@@ -548,39 +628,67 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
   const size_t scrB = (size_t)2 * gxB * LANE_BLOCK * lane_scratch_words<SB>() * 4;
   int rc = ensure_scratch(c, std::max(scrA, scrB));
   if (rc) return rc;
-  if ((rc = ensure_work(c, (size_t)2 * (SA + SB) * chunk * 4))) return rc;
+  // fixed-base obfuscation (kernels_fb.hpp) replaces stages A and B for the device RNG
+  const bool fb = e.obf == PAI_OBF_RNG && c->fb_ok && c->fb_enabled;
+  const int DQ = (c->fb_K + 15) / 16;
+  int occF = 1;
+  if (fb && fb_occupancy(SB, &occF)) return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
+  const int gxF = (int)std::max<long long>(1, std::min<long long>(lanes_blocks, (long long)occF * c->cus / 2));
+  const size_t ybytes = std::max((size_t)2 * SA * 4, fb ? (size_t)2 * DQ * 16 : 0);   // per element
+  if ((rc = ensure_work(c, (ybytes + (size_t)2 * SB * 4) * chunk))) return rc;
   uint32_t* y = (uint32_t*)c->d_work;
-  uint32_t* u = y + (size_t)2 * SA * chunk;
+  uint32_t* u = (uint32_t*)((char*)c->d_work + ybytes * chunk);
   const size_t esz = e.dtype == PAI_F32 ? 4 : 8;
   for (long long off = 0; off < N; off += chunk) {
     const long long n = std::min(chunk, N - off);
-    CrtParams pa{};
-    pa.halves = c->d_crt_a;
-    pa.n = n;
-    pa.obf = e.obf;
-    pa.r = e.r ? e.r + (size_t)off * e.r_stride : nullptr;
-    pa.r_stride = e.r_stride;
-    pa.r_words = r_words;
-    std::memcpy(pa.rng_key, e.rng_key, sizeof(pa.rng_key));
-    pa.index_base = e.index_base + (unsigned long long)off;
-    pa.kchunks = kchunks;
-    pa.out = y;
-    pa.scratch = (uint32_t*)c->d_scratch;
-    const int gA = (int)std::min<long long>(gxA, (n + LANE_BLOCK - 1) / LANE_BLOCK);
-    stage_mark(c, 0, st);
-    HIPCHK(crt_launch_a(SA, pa, gA, st));
-    stage_mark(c, 1, st);
-    HIPCHK(hipGetLastError());
-    CrtParams pb{};
-    pb.halves = c->d_crt_b;
-    pb.n = n;
-    pb.yin = y;
-    pb.out = u;
-    pb.scratch = (uint32_t*)c->d_scratch;
-    const int gB = (int)std::min<long long>(gxB, (n + LANE_BLOCK - 1) / LANE_BLOCK);
-    HIPCHK(crt_launch_b(SA, pb, gB, st));
-    HIPCHK(hipGetLastError());
-    stage_mark(c, 2, st);
+    if (fb) {
+      FbDigitParams pd{};
+      pd.n = n;
+      std::memcpy(pd.rng_key, e.rng_key, sizeof(pd.rng_key));
+      pd.index_base = e.index_base + (unsigned long long)off;
+      pd.K = c->fb_K;
+      pd.digits = (uint4*)y;
+      const int gD = (int)std::min<long long>((long long)4 * c->cus, (n + LANE_BLOCK - 1) / LANE_BLOCK);
+      stage_mark(c, 0, st);
+      HIPCHK(fb_launch_digits(pd, gD, st));
+      stage_mark(c, 1, st);
+      FbParams pf{};
+      pf.halves = c->d_fb_halves;
+      pf.n = n;
+      pf.K = c->fb_K;
+      pf.digits = (const uint4*)y;
+      pf.out = u;
+      HIPCHK(fb_launch(SB, pf, (int)std::min<long long>(gxF, (n + LANE_BLOCK - 1) / LANE_BLOCK), st));
+      stage_mark(c, 2, st);
+    } else {
+      CrtParams pa{};
+      pa.halves = c->d_crt_a;
+      pa.n = n;
+      pa.obf = e.obf;
+      pa.r = e.r ? e.r + (size_t)off * e.r_stride : nullptr;
+      pa.r_stride = e.r_stride;
+      pa.r_words = r_words;
+      std::memcpy(pa.rng_key, e.rng_key, sizeof(pa.rng_key));
+      pa.index_base = e.index_base + (unsigned long long)off;
+      pa.kchunks = kchunks;
+      pa.out = y;
+      pa.scratch = (uint32_t*)c->d_scratch;
+      const int gA = (int)std::min<long long>(gxA, (n + LANE_BLOCK - 1) / LANE_BLOCK);
+      stage_mark(c, 0, st);
+      HIPCHK(crt_launch_a(SA, pa, gA, st));
+      stage_mark(c, 1, st);
+      HIPCHK(hipGetLastError());
+      CrtParams pb{};
+      pb.halves = c->d_crt_b;
+      pb.n = n;
+      pb.yin = y;
+      pb.out = u;
+      pb.scratch = (uint32_t*)c->d_scratch;
+      const int gB = (int)std::min<long long>(gxB, (n + LANE_BLOCK - 1) / LANE_BLOCK);
+      HIPCHK(crt_launch_b(SA, pb, gB, st));
+      HIPCHK(hipGetLastError());
+      stage_mark(c, 2, st);
+    }
     CrtFinParams f{};
     f.x = (const char*)e.x + (size_t)off * esz;
     f.dtype = e.dtype;

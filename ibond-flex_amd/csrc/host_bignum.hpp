@@ -195,3 +195,83 @@ inline HBig pow2(size_t k) {
   return r;
 }
 }  // namespace fpai
+
+namespace fpai {
+// a mod d for a small divisor d
+inline uint32_t mod_small(const HBig& a, uint32_t d) {
+  uint64_t r = 0;
+  for (size_t i = a.w.size(); i-- > 0;) r = ((r << 32) | a.w[i]) % d;
+  return (uint32_t)r;
+}
+
+// Word-level (32-bit) Montgomery arithmetic modulo an odd m, for the one-time host work that needs
+// real modular exponentiations (fixed-base obfuscation setup): ~1000x faster than mod().
+struct HMont {
+  HBig m;
+  size_t s = 0;          // words
+  uint32_t mp = 0;       // -m^-1 mod 2^32
+  HBig r2;               // R^2 mod m, R = 2^(32 s)
+  explicit HMont(const HBig& mod_) : m(mod_), s(mod_.w.size()) {
+    uint32_t x = 1;
+    for (int i = 0; i < 6; ++i) x *= 2u - m.w[0] * x;
+    mp = 0u - x;
+    r2 = mul_pow2_mod(HBig(1), 64 * s, m);
+  }
+  // CIOS: a b R^-1 mod m (a, b < m)
+  HBig mul(const HBig& a, const HBig& b) const {
+    std::vector<uint64_t> t(s + 2, 0);
+    for (size_t i = 0; i < s; ++i) {
+      const uint64_t ai = i < a.w.size() ? a.w[i] : 0;
+      uint64_t c = 0;
+      for (size_t j = 0; j < s; ++j) {
+        const uint64_t v = t[j] + ai * (j < b.w.size() ? b.w[j] : 0) + c;
+        t[j] = (uint32_t)v;
+        c = v >> 32;
+      }
+      uint64_t v = t[s] + c;
+      t[s] = (uint32_t)v;
+      t[s + 1] = v >> 32;
+      const uint64_t q = (uint32_t)((uint32_t)t[0] * mp);
+      v = t[0] + q * m.w[0];
+      c = v >> 32;
+      for (size_t j = 1; j < s; ++j) {
+        v = t[j] + q * m.w[j] + c;
+        t[j - 1] = (uint32_t)v;
+        c = v >> 32;
+      }
+      v = t[s] + c;
+      t[s - 1] = (uint32_t)v;
+      t[s] = t[s + 1] + (v >> 32);
+    }
+    HBig r;
+    r.w.assign(s + 1, 0);
+    for (size_t i = 0; i <= s; ++i) r.w[i] = (uint32_t)t[i];
+    r.trim();
+    if (cmp(r, m) >= 0) r = sub(r, m);
+    return r;
+  }
+  HBig to(const HBig& a) const { return mul(mod(a, m), r2); }
+  HBig from(const HBig& a) const { return mul(a, HBig(1)); }
+  // a^e mod m (plain in, plain out)
+  HBig pow(const HBig& a, const HBig& e) const {
+    HBig x = to(a), acc = to(HBig(1));
+    for (size_t i = e.bits(); i-- > 0;) {
+      acc = mul(acc, acc);
+      if (e.bit(i)) acc = mul(acc, x);
+    }
+    return from(acc);
+  }
+};
+
+// primes below `bound` (sieve)
+inline std::vector<uint32_t> small_primes(uint32_t bound) {
+  std::vector<uint8_t> comp(bound, 0);
+  std::vector<uint32_t> out;
+  for (uint32_t i = 2; i < bound; ++i) {
+    if (comp[i]) continue;
+    out.push_back(i);
+    for (uint64_t j = (uint64_t)i * i; j < bound; j += i) comp[j] = 1;
+  }
+  return out;
+}
+}  // namespace fpai

@@ -21,9 +21,10 @@ PAI_EXP_AUTO, PAI_EXP_FIXED = 0, 1
 EL_OK, EL_INT, EL_INT_BIG, EL_OVERFLOW, EL_FLOAT_OVF, EL_ENC_RANGE = 0, 1, 2, 3, 4, 5
 
 PAI_OPT_CRT_ENCRYPT, PAI_OPT_CRT_AVAILABLE, PAI_OPT_STAGE_TIMING, PAI_OPT_LANE_DECRYPT = 1, 2, 3, 4
+PAI_OPT_FIXED_BASE = 5
 
 EXPORTED = ("pai_ctx_create", "pai_ctx_set_private", "pai_ctx_destroy", "pai_ctx_info", "pai_last_error",
-            "pai_ctx_set_option", "pai_ctx_get_option", "pai_ctx_stage_times",
+            "pai_ctx_set_option", "pai_ctx_get_option", "pai_ctx_stage_times", "pai_ctx_fixed_base_info",
             "pai_encrypt", "pai_add", "pai_decrypt", "pai_encrypt_dev", "pai_add_dev", "pai_decrypt_dev")
 
 _lib = None
@@ -54,6 +55,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.pai_ctx_set_option.argtypes = [P, I, I]
         lib.pai_ctx_get_option.argtypes = [P, I, P]
         lib.pai_ctx_stage_times.argtypes = [P, P, I, P]
+        lib.pai_ctx_fixed_base_info.argtypes = [P, P, P, P]
         lib.pai_encrypt.argtypes = [P, I, P, S, I, ctypes.c_int32, I, P, S, S, P, U64, P, P, P]
         lib.pai_add.argtypes = [P, P, P, I, S, P, P]
         lib.pai_decrypt.argtypes = [P, P, P, S, P, P, P, P]
@@ -148,6 +150,20 @@ class Context:
 
     def set_lane_decrypt(self, enabled: bool):
         _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_LANE_DECRYPT, 1 if enabled else 0))
+
+    @property
+    def fixed_base(self) -> bool:
+        """True when device-RNG encryption samples r^n through the fixed bases (kernels_fb.hpp)."""
+        return bool(self._get_option(PAI_OPT_FIXED_BASE))
+
+    def set_fixed_base(self, enabled: bool):
+        _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_FIXED_BASE, 1 if enabled else 0))
+
+    def fixed_base_info(self):
+        """(g_p, g_q, K): the generators and the exponent digit count of the fixed-base path."""
+        gp, gq, k = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int()
+        _check(self.lib.pai_ctx_fixed_base_info(self._h, ctypes.byref(gp), ctypes.byref(gq), ctypes.byref(k)))
+        return gp.value, gq.value, k.value
 
     def close(self):
         if getattr(self, "_h", None):

@@ -73,6 +73,10 @@ typedef struct pai_ctx pai_ctx;
 #define PAI_OPT_STAGE_TIMING 3   /* 1: record HIP events between the kernels of each encrypt/decrypt call */
 #define PAI_OPT_LANE_DECRYPT 4   /* 1 (default): decrypt on the lane engine when the key halves fit it;
                                     0: lane-group kernel. Read back: 1 when the lane path is in use  */
+#define PAI_OPT_FIXED_BASE 5     /* 1 (default): PAI_OBF_RNG encryption with the private key set samples
+                                    r^n through fixed bases (G_p^a_p, G_q^a_q: same distribution as
+                                    r^n for uniform r, see pai_ctx_fixed_base_info); 0: r from the
+                                    ChaCha20 stream and r^n by exponentiation. Read back: 1 when used */
 
 int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** out);
 int pai_ctx_set_private(pai_ctx* ctx, const uint8_t* p_le, const uint8_t* q_le, size_t half_bytes);
@@ -87,6 +91,11 @@ int pai_ctx_stage_times(pai_ctx* ctx, float* ms_out, int max_out, int* count);
 /* key bits, 32-bit words per ciphertext (2*key_bits/32), words per plaintext (key_bits/32) */
 int pai_ctx_info(const pai_ctx* ctx, int* key_bits, int* ct_words, int* pt_words);
 const char* pai_last_error(void);
+/* Fixed-base obfuscation parameters (PAI_OPT_FIXED_BASE): the bases g_p, g_q (generators of Z_p*,
+ * Z_q*, p < q) with G_h = g_h^n mod h^2, and the digit count K: element i's exponent a_h is the
+ * little-endian integer of bytes [0, K) of the ChaCha20 stream (rng_key, counter 0..,
+ * nonce = (index lo, index hi, 0x66786230 + h)); r^n mod h^2 is G_h^a_h.                        */
+int pai_ctx_fixed_base_info(const pai_ctx* ctx, uint32_t* g_p, uint32_t* g_q, int* digits);
 
 /* Encrypt N plaintexts. dtype PAI_F32/F64/I64. obf_mode PAI_OBF_*.
  *   r_le:      PAI_OBF_GIVEN only: r values as little-endian byte strings of r_bytes each, element i

@@ -27,6 +27,7 @@ def pairs(golden):
     for nb in (1024, 2048):
         key = _key(golden, nb)
         crt = N.Context(key.n, 0, key.p, key.q)
+        crt.set_fixed_base(False)   # generic r^n path here; the fixed-base sampler: test_gpu_fixed_base
         pub = N.Context(key.n, 0)
         out[nb] = (crt, pub, key)
     return out
@@ -114,11 +115,13 @@ def test_crt_toggle(pairs, nb):
     crt, _, _ = pairs[nb]
     x = np.arange(300, dtype=np.float32) - 150.5
     rk = b"k" * 32
-    a = crt.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk)
-    crt.set_crt(False)
+    crt.set_fixed_base(False)
     try:
+        a = crt.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk)
+        crt.set_crt(False)
         assert not crt.crt_enabled
         b = crt.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk)
     finally:
         crt.set_crt(True)
+        crt.set_fixed_base(True)
     assert np.array_equal(a[0], b[0])

@@ -88,7 +88,14 @@ def test_device_rng_matches_oracle_stream(ctxs, nb):
     ctx, key = ctxs[nb]
     rng_key = bytes(range(32))
     x = np.random.default_rng(5).standard_normal(40).astype(np.float32)
-    ct, ex, st = ctx.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rng_key, index_base=1000)
+    fb = ctx.has_private
+    if fb:
+        ctx.set_fixed_base(False)   # r from the ChaCha stream (fixed-base sampler: test_gpu_fixed_base)
+    try:
+        ct, ex, st = ctx.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rng_key, index_base=1000)
+    finally:
+        if fb:
+            ctx.set_fixed_base(True)
     got = N.words_to_ints(ct)
     rbytes = ((nb + 64 + 31) // 32) * 4
     for i in range(len(x)):

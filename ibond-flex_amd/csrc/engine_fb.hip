@@ -20,14 +20,21 @@ hipError_t fb_launch(int sb, const FbParams& p, int gx, hipStream_t st) {
 }
 
 hipError_t fb_launch_digits(const FbDigitParams& p, int gx, hipStream_t st) {
-  hipLaunchKernelGGL(k_fb_digits<FB_W>, dim3(gx, 2), dim3(LANE_BLOCK), 0, st, p);
+  hipLaunchKernelGGL(k_fb_digits<0>, dim3(gx, 2), dim3(LANE_BLOCK), 0, st, p);
   return hipGetLastError();
 }
 
-hipError_t fb_build_tables(int sb, const FbHalf* d_halves, uint4* t0, uint4* t1, int K, hipStream_t st) {
-  if (sb == 37) hipLaunchKernelGGL(k_fb_table<37>, dim3(K, 2), dim3(FB_ENT), 0, st, d_halves, t0, t1, K);
-  else if (sb == 74) hipLaunchKernelGGL(k_fb_table<74>, dim3(K, 2), dim3(FB_ENT), 0, st, d_halves, t0, t1, K);
-  else return hipErrorInvalidValue;
+hipError_t fb_build_tables(int sb, const FbHalf* d_halves, uint4* t0, uint4* t1, int K, int W, hipStream_t st) {
+  const int per = ((1 << W) + LANE_BLOCK - 1) / LANE_BLOCK;
+  if (sb == 37) {
+    hipLaunchKernelGGL(k_fb_lohi<37>, dim3(K, 2), dim3(LANE_BLOCK), 0, st, d_halves, K, W);
+    hipLaunchKernelGGL(k_fb_fill<37>, dim3(K * per, 2), dim3(LANE_BLOCK), 0, st, d_halves, K, W, t0, t1);
+  } else if (sb == 74) {
+    hipLaunchKernelGGL(k_fb_lohi<74>, dim3(K, 2), dim3(LANE_BLOCK), 0, st, d_halves, K, W);
+    hipLaunchKernelGGL(k_fb_fill<74>, dim3(K * per, 2), dim3(LANE_BLOCK), 0, st, d_halves, K, W, t0, t1);
+  } else {
+    return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -8,7 +8,7 @@ namespace fpai {
 int fb_occupancy(int sb, int* occ);
 hipError_t fb_launch(int sb, const FbParams& p, int gx, hipStream_t st);
 hipError_t fb_launch_digits(const FbDigitParams& p, int gx, hipStream_t st);
-// builds both halves' tables (K digit positions) on `st`
-hipError_t fb_build_tables(int sb, const FbHalf* d_halves, uint4* t0, uint4* t1, int K, hipStream_t st);
+// builds both halves' tables (K digit positions of W bits) on `st`
+hipError_t fb_build_tables(int sb, const FbHalf* d_halves, uint4* t0, uint4* t1, int K, int W, hipStream_t st);
 
 }  // namespace fpai

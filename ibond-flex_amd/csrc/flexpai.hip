@@ -1,6 +1,7 @@
 // flexpai: host context + C ABI for the MI355X Paillier engine (see include/flexpai.h).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -64,8 +65,14 @@ struct pai_ctx {
   bool fb_ok = false;
   bool fb_enabled = true;
   int fb_K = 0;
+  int fb_W = 0;                 // digit window (bits); 0 = not chosen yet ($FLEXPAI_FB_WINDOW, default 16)
   FbHalf* d_fb_halves = nullptr;
   uint32_t fb_g[2] = {0, 0};   // the bases g_p, g_q (generators of Z_p*, Z_q*)
+  std::vector<void*> fb_mem;    // tables and their constants (rebuilt when the window changes)
+  HBig fb_primes[2], fb_sq[2];
+  std::vector<uint32_t> fb_coef[2];
+  int fb_sb = 0;
+  size_t fb_RB = 0;
   std::vector<void*> allocs;
   // scratch (exponent tables), grown on demand
   void* d_scratch = nullptr;
@@ -82,6 +89,7 @@ struct pai_ctx {
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
     for (void* p : allocs) (void)hipFree(p);
+    for (void* p : fb_mem) (void)hipFree(p);
     if (d_scratch) (void)hipFree(d_scratch);
     if (d_work) (void)hipFree(d_work);
   }
@@ -323,41 +331,82 @@ static uint32_t fb_base(const HBig& P) {
   return 0;
 }
 
-static int setup_fb(pai_ctx* c, const HBig primes[2], const HBig sq[2], int sb, size_t RB,
-                    const std::vector<uint32_t>* coef_limbs) {
+template <typename T>
+static int upload_fb(pai_ctx* c, const std::vector<T>& v, T** out) {
+  void* p = nullptr;
+  HIPCHK(hipMalloc(&p, std::max<size_t>(v.size(), 1) * sizeof(T)));
+  c->fb_mem.push_back(p);
+  if (!v.empty()) HIPCHK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  *out = (T*)p;
+  return 0;
+}
+
+static int fb_default_window() {
+  const char* e = getenv("FLEXPAI_FB_WINDOW");
+  const int w = e ? atoi(e) : 16;
+  return (w == 8 || w == 12 || w == 16) ? w : 16;
+}
+
+// (Re)builds the fixed-base tables for window c->fb_W from the key material saved by setup_fb.
+static int build_fb(pai_ctx* c) {
   c->fb_ok = false;
-  if (sb != 37 && sb != 74) return 0;
-  const size_t eb = std::max(primes[0].bits(), primes[1].bits()) + 64;
-  const int K = (int)((eb + FB_W - 1) / FB_W);
-  if (K > FB_MAX_K) return 0;
+  for (void* p : c->fb_mem) (void)hipFree(p);
+  c->fb_mem.clear();
+  const int sb = c->fb_sb, W = c->fb_W;
+  const size_t RB = c->fb_RB;
+  const size_t eb = std::max(c->fb_primes[0].bits(), c->fb_primes[1].bits()) + 64;
+  const int K = (int)((eb + W - 1) / W);
+  if ((size_t)K * W > 32 * (size_t)FB_MAX_WORDS) return 0;
   const int TQ = (sb + 3) / 4;
   FbHalf hv[2];
   int rc;
+  void* t[2] = {nullptr, nullptr};
   for (int h = 0; h < 2; ++h) {
-    const uint32_t g = fb_base(primes[h]);
-    if (!g) return 0;
-    c->fb_g[h] = g;
-    HMont M2(sq[h]);
-    const HBig G = M2.pow(HBig(g), c->n);
-    uint32_t *dm, *dc1, *dgR, *done;
-    uint4* dtab;
-    if ((rc = upload(c, sq[h].limbs(sb, LB), &dm)) || (rc = upload(c, coef_limbs[h], &dc1)) ||
-        (rc = upload(c, mul_pow2_mod(G, RB, sq[h]).limbs(sb, LB), &dgR)) ||
-        (rc = upload(c, mul_pow2_mod(HBig(1), RB, sq[h]).limbs(sb, LB), &done)))
+    const HBig& m2 = c->fb_sq[h];
+    HMont M2(m2);
+    // B_k = G^(2^(W k)), G = g^n mod p_h^2
+    std::vector<uint32_t> bl((size_t)K * sb);
+    HBig x = M2.to(M2.pow(HBig(c->fb_g[h]), c->n));
+    for (int k = 0; k < K; ++k) {
+      const std::vector<uint32_t> v = M2.from(x).limbs(sb, LB);
+      std::copy(v.begin(), v.end(), bl.begin() + (size_t)k * sb);
+      for (int q = 0; q < W; ++q) x = M2.mul(x, x);
+    }
+    uint32_t *dm, *dc1, *dR2, *done, *dbases, *dlohi;
+    if ((rc = upload_fb(c, m2.limbs(sb, LB), &dm)) || (rc = upload_fb(c, c->fb_coef[h], &dc1)) ||
+        (rc = upload_fb(c, mul_pow2_mod(HBig(1), 2 * RB, m2).limbs(sb, LB), &dR2)) ||
+        (rc = upload_fb(c, mul_pow2_mod(HBig(1), RB, m2).limbs(sb, LB), &done)) || (rc = upload_fb(c, bl, &dbases)) ||
+        (rc = upload_fb(c, std::vector<uint32_t>((size_t)K * 2 * FB_LO * sb, 0u), &dlohi)))
       return rc;
-    void* t = nullptr;
-    HIPCHK(hipMalloc(&t, (size_t)K * FB_ENT * TQ * sizeof(uint4)));
-    c->allocs.push_back(t);
-    dtab = (uint4*)t;
-    hv[h] = FbHalf{dtab, dm, dc1, dgR, done, mont_prime(sq[h], LB)};
+    HIPCHK(hipMalloc(&t[h], ((size_t)K << W) * TQ * sizeof(uint4)));
+    c->fb_mem.push_back(t[h]);
+    hv[h] = FbHalf{(const uint4*)t[h], dm, dc1, dR2, done, dbases, dlohi, mont_prime(m2, LB)};
   }
   std::vector<FbHalf> v(hv, hv + 2);
-  if ((rc = upload(c, v, &c->d_fb_halves))) return rc;
-  HIPCHK(fb_build_tables(sb, c->d_fb_halves, (uint4*)hv[0].table, (uint4*)hv[1].table, K, nullptr));
+  if ((rc = upload_fb(c, v, &c->d_fb_halves))) return rc;
+  HIPCHK(fb_build_tables(sb, c->d_fb_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr));
   HIPCHK(hipDeviceSynchronize());
   c->fb_K = K;
   c->fb_ok = true;
   return 0;
+}
+
+static int setup_fb(pai_ctx* c, const HBig primes[2], const HBig sq[2], int sb, size_t RB,
+                    const std::vector<uint32_t>* coef_limbs) {
+  c->fb_ok = false;
+  if (sb != 37 && sb != 74) return 0;
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t g = fb_base(primes[h]);
+    if (!g) return 0;
+    c->fb_g[h] = g;
+    c->fb_primes[h] = primes[h];
+    c->fb_sq[h] = sq[h];
+    c->fb_coef[h] = coef_limbs[h];
+  }
+  c->fb_sb = sb;
+  c->fb_RB = RB;
+  if (!c->fb_W) c->fb_W = fb_default_window();
+  return build_fb(c);
 }
 
 // CRT encryption constants (kernels_crt.hpp). p < q here (sorted like keypair.py:57-62).
@@ -533,6 +582,13 @@ int pai_ctx_set_option(pai_ctx* c, int option, int value) {
     case PAI_OPT_STAGE_TIMING: c->timing = value != 0; c->nev = 0; return 0;
     case PAI_OPT_LANE_DECRYPT: c->dec_lane_enabled = value != 0; return 0;
     case PAI_OPT_FIXED_BASE: c->fb_enabled = value != 0; return 0;
+    case PAI_OPT_FB_WINDOW:
+      if (value != 8 && value != 12 && value != 16) return fail(PAI_ERR_ARG, "fixed-base window must be 8, 12 or 16");
+      if (value == c->fb_W) return 0;
+      c->fb_W = value;
+      if (!c->fb_sb) return 0;   // applied when the private key is set
+      HIPCHK(hipSetDevice(c->device));
+      return build_fb(c);
   }
   return fail(PAI_ERR_ARG, "pai_ctx_set_option: unknown option");
 }
@@ -545,6 +601,7 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
     case PAI_OPT_STAGE_TIMING: *value = c->timing ? 1 : 0; return 0;
     case PAI_OPT_LANE_DECRYPT: *value = (c->dec_lane_ok && c->dec_lane_enabled) ? 1 : 0; return 0;
     case PAI_OPT_FIXED_BASE: *value = (c->fb_ok && c->fb_enabled) ? 1 : 0; return 0;
+    case PAI_OPT_FB_WINDOW: *value = c->fb_W ? c->fb_W : fb_default_window(); return 0;
   }
   return fail(PAI_ERR_ARG, "pai_ctx_get_option: unknown option");
 }
@@ -561,12 +618,13 @@ int pai_ctx_stage_times(pai_ctx* c, float* ms_out, int max_out, int* count) {
   return 0;
 }
 
-int pai_ctx_fixed_base_info(const pai_ctx* c, uint32_t* g_p, uint32_t* g_q, int* digits) {
+int pai_ctx_fixed_base_info(const pai_ctx* c, uint32_t* g_p, uint32_t* g_q, int* digits, int* window) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
   if (!c->fb_ok) return fail(PAI_ERR_NOPRIV, "fixed-base obfuscation not available (needs the private key)");
   if (g_p) *g_p = c->fb_g[0];
   if (g_q) *g_q = c->fb_g[1];
   if (digits) *digits = c->fb_K;
+  if (window) *window = c->fb_W;
   return 0;
 }
 
@@ -630,11 +688,10 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
   if (rc) return rc;
   // fixed-base obfuscation (kernels_fb.hpp) replaces stages A and B for the device RNG
   const bool fb = e.obf == PAI_OBF_RNG && c->fb_ok && c->fb_enabled;
-  const int DQ = (c->fb_K + 15) / 16;
   int occF = 1;
   if (fb && fb_occupancy(SB, &occF)) return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
   const int gxF = (int)std::max<long long>(1, std::min<long long>(lanes_blocks, (long long)occF * c->cus / 2));
-  const size_t ybytes = std::max((size_t)2 * SA * 4, fb ? (size_t)2 * DQ * 16 : 0);   // per element
+  const size_t ybytes = std::max((size_t)2 * SA * 4, fb ? (size_t)2 * c->fb_K * 2 : 0);   // per element
   if ((rc = ensure_work(c, (ybytes + (size_t)2 * SB * 4) * chunk))) return rc;
   uint32_t* y = (uint32_t*)c->d_work;
   uint32_t* u = (uint32_t*)((char*)c->d_work + ybytes * chunk);
@@ -647,7 +704,8 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
       std::memcpy(pd.rng_key, e.rng_key, sizeof(pd.rng_key));
       pd.index_base = e.index_base + (unsigned long long)off;
       pd.K = c->fb_K;
-      pd.digits = (uint4*)y;
+      pd.W = c->fb_W;
+      pd.digits = (uint16_t*)y;
       const int gD = (int)std::min<long long>((long long)4 * c->cus, (n + LANE_BLOCK - 1) / LANE_BLOCK);
       stage_mark(c, 0, st);
       HIPCHK(fb_launch_digits(pd, gD, st));
@@ -656,7 +714,8 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
       pf.halves = c->d_fb_halves;
       pf.n = n;
       pf.K = c->fb_K;
-      pf.digits = (const uint4*)y;
+      pf.W = c->fb_W;
+      pf.digits = (const uint16_t*)y;
       pf.out = u;
       HIPCHK(fb_launch(SB, pf, (int)std::min<long long>(gxF, (n + LANE_BLOCK - 1) / LANE_BLOCK), st));
       stage_mark(c, 2, st);

@@ -21,7 +21,7 @@ PAI_EXP_AUTO, PAI_EXP_FIXED = 0, 1
 EL_OK, EL_INT, EL_INT_BIG, EL_OVERFLOW, EL_FLOAT_OVF, EL_ENC_RANGE = 0, 1, 2, 3, 4, 5
 
 PAI_OPT_CRT_ENCRYPT, PAI_OPT_CRT_AVAILABLE, PAI_OPT_STAGE_TIMING, PAI_OPT_LANE_DECRYPT = 1, 2, 3, 4
-PAI_OPT_FIXED_BASE = 5
+PAI_OPT_FIXED_BASE, PAI_OPT_FB_WINDOW = 5, 6
 
 EXPORTED = ("pai_ctx_create", "pai_ctx_set_private", "pai_ctx_destroy", "pai_ctx_info", "pai_last_error",
             "pai_ctx_set_option", "pai_ctx_get_option", "pai_ctx_stage_times", "pai_ctx_fixed_base_info",
@@ -55,7 +55,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.pai_ctx_set_option.argtypes = [P, I, I]
         lib.pai_ctx_get_option.argtypes = [P, I, P]
         lib.pai_ctx_stage_times.argtypes = [P, P, I, P]
-        lib.pai_ctx_fixed_base_info.argtypes = [P, P, P, P]
+        lib.pai_ctx_fixed_base_info.argtypes = [P, P, P, P, P]
         lib.pai_encrypt.argtypes = [P, I, P, S, I, ctypes.c_int32, I, P, S, S, P, U64, P, P, P]
         lib.pai_add.argtypes = [P, P, P, I, S, P, P]
         lib.pai_decrypt.argtypes = [P, P, P, S, P, P, P, P]
@@ -160,10 +160,20 @@ class Context:
         _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_FIXED_BASE, 1 if enabled else 0))
 
     def fixed_base_info(self):
-        """(g_p, g_q, K): the generators and the exponent digit count of the fixed-base path."""
-        gp, gq, k = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int()
-        _check(self.lib.pai_ctx_fixed_base_info(self._h, ctypes.byref(gp), ctypes.byref(gq), ctypes.byref(k)))
-        return gp.value, gq.value, k.value
+        """(g_p, g_q, K, W): the generators, the exponent digit count and the digit window (bits) of
+        the fixed-base path."""
+        gp, gq, k, w = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int(), ctypes.c_int()
+        _check(self.lib.pai_ctx_fixed_base_info(self._h, ctypes.byref(gp), ctypes.byref(gq), ctypes.byref(k),
+                                                ctypes.byref(w)))
+        return gp.value, gq.value, k.value, w.value
+
+    @property
+    def fb_window(self) -> int:
+        return self._get_option(PAI_OPT_FB_WINDOW)
+
+    def set_fb_window(self, bits: int):
+        """Digit window of the fixed-base tables (8, 12 or 16); rebuilds them."""
+        _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_FB_WINDOW, int(bits)))
 
     def close(self):
         if getattr(self, "_h", None):

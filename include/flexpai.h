@@ -77,6 +77,8 @@ typedef struct pai_ctx pai_ctx;
                                     r^n through fixed bases (G_p^a_p, G_q^a_q: same distribution as
                                     r^n for uniform r, see pai_ctx_fixed_base_info); 0: r from the
                                     ChaCha20 stream and r^n by exponentiation. Read back: 1 when used */
+#define PAI_OPT_FB_WINDOW 6      /* digit window of the fixed-base tables: 8, 12 or 16 bits (default 16, or
+                                    $FLEXPAI_FB_WINDOW); setting it rebuilds the tables (K 2^W rows per half) */
 
 int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** out);
 int pai_ctx_set_private(pai_ctx* ctx, const uint8_t* p_le, const uint8_t* q_le, size_t half_bytes);
@@ -92,10 +94,10 @@ int pai_ctx_stage_times(pai_ctx* ctx, float* ms_out, int max_out, int* count);
 int pai_ctx_info(const pai_ctx* ctx, int* key_bits, int* ct_words, int* pt_words);
 const char* pai_last_error(void);
 /* Fixed-base obfuscation parameters (PAI_OPT_FIXED_BASE): the bases g_p, g_q (generators of Z_p*,
- * Z_q*, p < q) with G_h = g_h^n mod h^2, and the digit count K: element i's exponent a_h is the
- * little-endian integer of bytes [0, K) of the ChaCha20 stream (rng_key, counter 0..,
- * nonce = (index lo, index hi, 0x66786230 + h)); r^n mod h^2 is G_h^a_h.                        */
-int pai_ctx_fixed_base_info(const pai_ctx* ctx, uint32_t* g_p, uint32_t* g_q, int* digits);
+ * Z_q*, p < q) with G_h = g_h^n mod h^2, the digit count K and the window W: element i's exponent a_h
+ * is the little-endian integer of the first K*W bits of the ChaCha20 stream (rng_key, counter 0..,
+ * nonce = (index lo, index hi, 0x66786230 + h)); r^n mod h^2 is G_h^a_h.                         */
+int pai_ctx_fixed_base_info(const pai_ctx* ctx, uint32_t* g_p, uint32_t* g_q, int* digits, int* window);
 
 /* Encrypt N plaintexts. dtype PAI_F32/F64/I64. obf_mode PAI_OBF_*.
  *   r_le:      PAI_OBF_GIVEN only: r values as little-endian byte strings of r_bytes each, element i

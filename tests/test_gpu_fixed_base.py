@@ -50,9 +50,10 @@ def _jacobi(a: int, n: int) -> int:
 def test_fixed_base_params_match_oracle(ctxs, nb):
     ctx, key = ctxs[nb]
     assert ctx.fixed_base
-    gp, gq, K = ctx.fixed_base_info()
+    gp, gq, K, W = ctx.fixed_base_info()
     assert (gp, gq) == (O.fb_base(key.p), O.fb_base(key.q))
-    assert K == O.fb_digits(key.p.bit_length(), key.q.bit_length())
+    assert W == ctx.fb_window and W in (8, 12, 16)
+    assert K == O.fb_digits(key.p.bit_length(), key.q.bit_length(), W)
 
 
 def test_fixed_base_needs_private_key(golden):
@@ -68,14 +69,14 @@ def test_fixed_base_needs_private_key(golden):
 def test_fixed_base_bit_exact(ctxs, nb, count, base):
     N = _native()
     ctx, key = ctxs[nb]
-    bases = ctx.fixed_base_info()[:2]
+    params = ctx.fixed_base_info()
     rk = bytes(range(7, 39))
     x = (np.random.default_rng(count).standard_normal(count) * 100).astype(np.float32)
     x[::13] = 0.0
     ct, ex, st = ctx.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=base)
     got = N.words_to_ints(ct)
     for i in sorted({0, count // 3, count // 2, count - 1}):
-        c, e = O.fb_encrypt_value(x[i], key, rk, base + i, bases)
+        c, e = O.fb_encrypt_value(x[i], key, rk, base + i, params)
         assert got[i] == c and int(ex[i]) == e, f"element {i}"
     val, _, st2, _ = ctx.decrypt(ct, ex)
     assert np.array_equal(val, x.astype(np.float64))
@@ -114,3 +115,30 @@ def test_fixed_base_jacobi_statistics(ctxs):
     plus = sum(1 for j in js if j == 1)
     assert all(j in (1, -1) for j in js)
     assert abs(plus - M / 2) < 5 * (M / 4) ** 0.5       # 5 sigma
+
+
+@pytest.mark.parametrize("nb", [1024, 2048])
+def test_fixed_base_windows(ctxs, nb):
+    """Windows 8, 12, 16 rebuild the tables; each is bit-exact against the oracle, and 8 and 16
+    (same 1088-bit exponent for 2048-bit keys, 576-bit for 1024-bit) give identical ciphertexts."""
+    N = _native()
+    ctx, key = ctxs[nb]
+    w0 = ctx.fb_window
+    rk = bytes(range(40, 72))
+    x = np.random.default_rng(nb).standard_normal(300).astype(np.float32)
+    outs = {}
+    try:
+        for w in (8, 12, 16):
+            ctx.set_fb_window(w)
+            params = ctx.fixed_base_info()
+            assert params[3] == w
+            ct, ex, _ = ctx.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=99)
+            got = N.words_to_ints(ct)
+            for i in (0, 150, 299):
+                assert (got[i], int(ex[i])) == O.fb_encrypt_value(x[i], key, rk, 99 + i, params), (w, i)
+            outs[w] = ct
+        assert np.array_equal(outs[8], outs[16])
+    finally:
+        ctx.set_fb_window(w0)
+    with pytest.raises(RuntimeError):
+        ctx.set_fb_window(10)

@@ -13,6 +13,7 @@
 #include "engine_dec.hpp"
 #include "engine_lane.hpp"
 #include "engine_fb.hpp"
+#include "engine_mul.hpp"
 
 using namespace fpai;
 
@@ -79,6 +80,11 @@ struct pai_ctx {
   size_t scratch_bytes = 0;
   void* d_work = nullptr;       // CRT intermediates (y, u)
   size_t work_bytes = 0;
+  void* d_mul = nullptr;        // ciphertext x plaintext terms, flags, reduction partials
+  size_t mul_bytes = 0;
+  void* d_inv = nullptr;        // batch-inversion prefix products and segment products
+  size_t inv_bytes = 0;
+  std::vector<uint32_t> inv_host;   // top of the inversion tree (host side of an async copy)
   int cus = 0;
   // optional per-stage timing of the last encrypt call (PAI_OPT_STAGE_TIMING)
   bool timing = false;
@@ -92,6 +98,8 @@ struct pai_ctx {
     for (void* p : fb_mem) (void)hipFree(p);
     if (d_scratch) (void)hipFree(d_scratch);
     if (d_work) (void)hipFree(d_work);
+    if (d_mul) (void)hipFree(d_mul);
+    if (d_inv) (void)hipFree(d_inv);
   }
 };
 
@@ -229,6 +237,16 @@ static int ensure_scratch(pai_ctx* c, size_t bytes) {
   c->scratch_bytes = 0;
   HIPCHK(hipMalloc(&c->d_scratch, bytes));
   c->scratch_bytes = bytes;
+  return 0;
+}
+
+static int ensure_buf(void** buf, size_t* have, size_t bytes) {
+  if (bytes <= *have) return 0;
+  if (*buf) HIPCHK(hipFree(*buf));
+  *buf = nullptr;
+  *have = 0;
+  HIPCHK(hipMalloc(buf, bytes));
+  *have = bytes;
   return 0;
 }
 
@@ -967,6 +985,237 @@ struct DevScope {
     return (T*)p;
   }
 };
+
+// ------------------------------------------------------------------ ciphertext x plaintext
+static size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
+
+static int inv_grid(pai_ctx* c, long long nseg) {
+  int occ = 1;
+  if (mul_occupancy(c->tpi_e, &occ)) occ = 1;
+  const int gpb = BLOCK / c->tpi_e;
+  return (int)std::max<long long>(1, std::min<long long>((nseg + gpb - 1) / gpb, (long long)occ * c->cus));
+}
+
+// Batch inversion (Montgomery's trick, kernels_mul.hpp) of the flagged values of x [n][W] in place,
+// on `st`. Segment products are reduced level by level to ONE value, inverted on the host (the only
+// modular inversion mod n^2; gmpy_math.invert, gmpy_math.py:66-74), and expanded back down. The
+// host step synchronises `st` once. Not invertible -> PAI_ERR_NOINV ("no inverse exists").
+static int batch_invert(pai_ctx* c, uint32_t* x, const uint8_t* flag, long long n, hipStream_t st) {
+  const int S = c->S_e, W = c->ct_words;
+  std::vector<long long> ns{n};
+  do ns.push_back((ns.back() + INV_SEG - 1) / INV_SEG);
+  while (ns.back() > 1);
+  const int levels = (int)ns.size() - 1;
+  std::vector<size_t> pre_off(levels), seg_off(levels);
+  size_t off = 0;
+  for (int l = 0; l < levels; ++l) {
+    pre_off[l] = off;
+    off = align16(off + (size_t)ns[l] * S * 4);
+    seg_off[l] = off;
+    off = align16(off + (size_t)ns[l + 1] * W * 4);
+  }
+  int rc = ensure_buf(&c->d_inv, &c->inv_bytes, off);
+  if (rc) return rc;
+  char* base = (char*)c->d_inv;
+  auto params = [&](int l) {
+    InvParams p{};
+    p.x = l == 0 ? x : (uint32_t*)(base + seg_off[l - 1]);
+    p.flag = l == 0 ? flag : nullptr;
+    p.n = ns[l];
+    p.pre = (uint32_t*)(base + pre_off[l]);
+    p.seg = (uint32_t*)(base + seg_off[l]);
+    p.N = c->d_N;
+    p.R2 = c->d_R2;
+    p.oneR = c->d_oneR;
+    p.mprime = c->mprime_N;
+    p.ct_words = W;
+    return p;
+  };
+  for (int l = 0; l < levels; ++l) HIPCHK(inv_launch(c->tpi_e, true, params(l), inv_grid(c, ns[l + 1]), st));
+  uint32_t* top = (uint32_t*)(base + seg_off[levels - 1]);
+  c->inv_host.assign(W, 0);
+  HIPCHK(hipMemcpyAsync(c->inv_host.data(), top, (size_t)W * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  HBig v;
+  v.w = c->inv_host;
+  v.trim();
+  HBig inv = inv_mod(v, c->N);
+  if (inv.is_zero()) return fail(PAI_ERR_NOINV, "invert() no inverse exists");
+  c->inv_host = inv.words(W);
+  HIPCHK(hipMemcpyAsync(top, c->inv_host.data(), (size_t)W * 4, hipMemcpyHostToDevice, st));
+  for (int l = levels - 1; l >= 0; --l) HIPCHK(inv_launch(c->tpi_e, false, params(l), inv_grid(c, ns[l + 1]), st));
+  return 0;
+}
+
+// k_mul over n terms (p: index maps, scalars; outputs set by the caller)
+static int launch_mul(pai_ctx* c, MulParams& p, hipStream_t st) {
+  int occ = 1;
+  if (mul_occupancy(c->tpi_e, &occ)) return fail(PAI_ERR_KEY, "unsupported group size");
+  const int gpb = BLOCK / c->tpi_e;
+  const int grid = (int)std::max<long long>(1, std::min<long long>((p.n + gpb - 1) / gpb, (long long)occ * c->cus));
+  int rc = ensure_scratch(c, (size_t)grid * BLOCK * TILE_WORDS_PER_LANE * 4);
+  if (rc) return rc;
+  p.N = c->d_N;
+  p.R2 = c->d_R2;
+  p.oneR = c->d_oneR;
+  p.mprime = c->mprime_N;
+  p.ct_words = c->ct_words;
+  p.scratch = (uint32_t*)c->d_scratch;
+  HIPCHK(mul_launch(c->tpi_e, p, grid, st));
+  return 0;
+}
+
+static int add_dev(pai_ctx* c, const uint32_t* cts, const int32_t* exps, int k, long long N, uint32_t* out,
+                   int32_t* out_exp, hipStream_t st) {
+  AddParams p{cts, exps, k, out, out_exp, N, c->d_N, c->d_R2, c->d_oneR, c->mprime_N, c->ct_words, nullptr};
+  switch (c->tpi_e) {
+    case 2: return launch_add<2>(c, p, st);
+    case 4: return launch_add<4>(c, p, st);
+    case 8: return launch_add<8>(c, p, st);
+  }
+  return fail(PAI_ERR_KEY, "unsupported group size");
+}
+
+int pai_mul_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t N, int dtype, const void* d_x,
+                size_t x_stride, uint32_t* d_out, int32_t* d_exp_out, int32_t* d_status, void* stream) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (N == 0) return 0;
+  if (!d_ct || !d_exp || !d_x || !d_out || !d_exp_out || dtype < 0 || dtype > 2 || x_stride > 1)
+    return fail(PAI_ERR_ARG, "pai_mul_dev: bad arguments");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  int rc = ensure_buf(&c->d_mul, &c->mul_bytes, N);
+  if (rc) return rc;
+  MulParams p{};
+  p.ct = d_ct;
+  p.exp = d_exp;
+  p.m = (long long)N;
+  p.d = 1;
+  p.cs_i = 1;
+  p.xs_i = (long long)x_stride;
+  p.x = d_x;
+  p.dtype = dtype;
+  p.n = (long long)N;
+  p.out = d_out;
+  p.out_exp = d_exp_out;
+  p.status = d_status;
+  p.neg = (uint8_t*)c->d_mul;
+  if ((rc = launch_mul(c, p, st))) return rc;
+  return batch_invert(c, d_out, (const uint8_t*)c->d_mul, (long long)N, st);
+}
+
+constexpr int MATMUL_CHUNK = 16;   // operands per k_add pass of the reduction tree
+
+int pai_matmul_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t m, size_t K, int dtype,
+                   const void* d_x, size_t d, uint32_t* d_out, int32_t* d_exp_out, void* stream) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (m == 0 || d == 0) return 0;
+  if (K == 0 || !d_ct || !d_exp || !d_x || !d_out || !d_exp_out || dtype < 0 || dtype > 2)
+    return fail(PAI_ERR_ARG, "pai_matmul_dev: bad arguments");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t W = c->ct_words, Np = m * d, T = K * Np;
+  const int C = MATMUL_CHUNK;
+  const size_t Kp = K > (size_t)C ? (K + C - 1) / C * C : K;          // rows of the term buffer
+  const size_t Pr = (Kp + C - 1) / C + C;                              // rows of the partial buffer
+  const size_t o_terms = 0, o_texp = align16(o_terms + Kp * Np * W * 4), o_flag = align16(o_texp + Kp * Np * 4),
+               o_part = align16(o_flag + T), o_pexp = align16(o_part + Pr * Np * W * 4), total = align16(o_pexp + Pr * Np * 4);
+  int rc = ensure_buf(&c->d_mul, &c->mul_bytes, total);
+  if (rc) return rc;
+  char* b = (char*)c->d_mul;
+  uint32_t* terms = (uint32_t*)(b + o_terms);
+  int32_t* texp = (int32_t*)(b + o_texp);
+  uint8_t* flag = (uint8_t*)(b + o_flag);
+  uint32_t* part = (uint32_t*)(b + o_part);
+  int32_t* pexp = (int32_t*)(b + o_pexp);
+  // terms (k, i, j) = c[i][k] (x) x[k][j], k-major: the k_add layout of K operands over m d outputs
+  MulParams p{};
+  p.ct = d_ct;
+  p.exp = d_exp;
+  p.m = (long long)m;
+  p.d = (long long)d;
+  p.cs_i = (long long)K;
+  p.cs_k = 1;
+  p.xs_k = (long long)d;
+  p.xs_j = 1;
+  p.x = d_x;
+  p.dtype = dtype;
+  p.n = (long long)T;
+  p.out = terms;
+  p.out_exp = texp;
+  p.neg = flag;
+  if ((rc = launch_mul(c, p, st))) return rc;
+  if ((rc = batch_invert(c, terms, flag, (long long)T, st))) return rc;
+  // reduction over k: passes of C operands (padding operands: exponent PAD_EXP), then the rest
+  uint32_t* cur = terms;
+  int32_t* cur_e = texp;
+  size_t Kc = K;
+  bool in_terms = true;
+  while (Kc > (size_t)C) {
+    const size_t Kn = (Kc + C - 1) / C;
+    if (Kn * C > Kc) HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(cur_e + Kc * Np), PAD_EXP, (Kn * C - Kc) * Np, st));
+    uint32_t* nxt = in_terms ? part : terms;
+    int32_t* nxt_e = in_terms ? pexp : texp;
+    if ((rc = add_dev(c, cur, cur_e, C, (long long)(Kn * Np), nxt, nxt_e, st))) return rc;
+    cur = nxt;
+    cur_e = nxt_e;
+    Kc = Kn;
+    in_terms = !in_terms;
+  }
+  return add_dev(c, cur, cur_e, (int)Kc, (long long)Np, d_out, d_exp_out, st);
+}
+
+int pai_mul(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, int dtype, const void* x, size_t x_stride,
+            uint32_t* ct_out, int32_t* exp_out, int32_t* status_out) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (N == 0) return 0;
+  if (!ct || !exp || !x || !ct_out || !exp_out || x_stride > 1) return fail(PAI_ERR_ARG, "pai_mul: bad arguments");
+  HIPCHK(hipSetDevice(c->device));
+  const size_t W = c->ct_words, esz = dtype == PAI_F32 ? 4 : 8, nx = x_stride ? N : 1;
+  DevScope ds;
+  uint32_t* dct = ds.alloc<uint32_t>(N * W);
+  int32_t* dexp = ds.alloc<int32_t>(N);
+  void* dx = ds.alloc<uint8_t>(nx * esz);
+  uint32_t* dout = ds.alloc<uint32_t>(N * W);
+  int32_t* dexo = ds.alloc<int32_t>(N);
+  int32_t* dst = ds.alloc<int32_t>(N);
+  if (!dct || !dexp || !dx || !dout || !dexo || !dst) return fail(PAI_ERR_HIP, "pai_mul: device allocation failed");
+  HIPCHK(hipMemcpy(dct, ct, N * W * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dexp, exp, N * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dx, x, nx * esz, hipMemcpyHostToDevice));
+  int rc = pai_mul_dev(c, dct, dexp, N, dtype, dx, x_stride, dout, dexo, dst, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(ct_out, dout, N * W * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(exp_out, dexo, N * 4, hipMemcpyDeviceToHost));
+  if (status_out) HIPCHK(hipMemcpy(status_out, dst, N * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int pai_matmul(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t m, size_t K, int dtype, const void* x,
+               size_t d, uint32_t* ct_out, int32_t* exp_out) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (m == 0 || d == 0) return 0;
+  if (K == 0 || !ct || !exp || !x || !ct_out || !exp_out) return fail(PAI_ERR_ARG, "pai_matmul: bad arguments");
+  HIPCHK(hipSetDevice(c->device));
+  const size_t W = c->ct_words, esz = dtype == PAI_F32 ? 4 : 8;
+  DevScope ds;
+  uint32_t* dct = ds.alloc<uint32_t>(m * K * W);
+  int32_t* dexp = ds.alloc<int32_t>(m * K);
+  void* dx = ds.alloc<uint8_t>(K * d * esz);
+  uint32_t* dout = ds.alloc<uint32_t>(m * d * W);
+  int32_t* dexo = ds.alloc<int32_t>(m * d);
+  if (!dct || !dexp || !dx || !dout || !dexo) return fail(PAI_ERR_HIP, "pai_matmul: device allocation failed");
+  HIPCHK(hipMemcpy(dct, ct, m * K * W * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dexp, exp, m * K * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dx, x, K * d * esz, hipMemcpyHostToDevice));
+  int rc = pai_matmul_dev(c, dct, dexp, m, K, dtype, dx, d, dout, dexo, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(ct_out, dout, m * d * W * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(exp_out, dexo, m * d * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
 
 int pai_encrypt(pai_ctx* c, int dtype, const void* x, size_t N, int exp_mode, int32_t fixed_exp, int obf_mode,
                 const uint8_t* r_le, size_t r_stride_bytes, size_t r_bytes, const uint8_t* rng_key32,

@@ -9,6 +9,7 @@ namespace fpai {
 constexpr int BLOCK = 256;
 constexpr int TABLE_ODD = 16;   // sliding window k=5: odd powers x^1..x^31
 constexpr int TABLE_FIX = 32;   // fixed window k=5: x^0..x^31
+constexpr int32_t PAD_EXP = INT32_MIN;   // exponent of a padding operand of k_add (the value 1, skipped)
 
 struct EncParams {
   const void* x;
@@ -301,14 +302,21 @@ __global__ __launch_bounds__(BLOCK, 2) void k_add(AddParams p) {
     const long long inst = base + gib;
     const bool valid = inst < p.n;
     const long long ii = valid ? inst : p.n - 1;
-    int E = p.exps[ii];
-    for (int j = 1; j < p.k; ++j) E = max(E, p.exps[(long long)j * p.n + ii]);
+    // padding operands (exponent PAD_EXP, used by the chunked reductions of pai_matmul) count as 1
+    int E = PAD_EXP;
+    for (int j = 0; j < p.k; ++j) {
+      const int ej = p.exps[(long long)j * p.n + ii];
+      if (ej != PAD_EXP) E = max(E, ej);
+    }
     uint32_t a[L];
     for (int j = 0; j < p.k; ++j) {
-      words_to_limbs(p.cts + ((long long)j * p.n + ii) * p.ct_words, p.ct_words, a, tig);
+      const int ej = p.exps[(long long)j * p.n + ii];
+      const bool pad = ej == PAD_EXP;
+      words_to_limbs(p.cts + ((long long)j * p.n + ii) * p.ct_words, pad ? 0 : p.ct_words, a, tig);
+      if (pad && tig == 0) a[0] = 1u;
       copy_g_to_lds<TPI>(slot, p.R2, tig);
       montmul<TPI>(a, a, slot, TPI, m, p.mprime, lane, tig);           // Montgomery form
-      const int nsq = 4 * (E - p.exps[(long long)j * p.n + ii]);
+      const int nsq = pad ? 0 : 4 * (E - ej);
       for (int t = 0;; ++t) {                                            // wave-uniform trip count
         const bool need = t < nsq;
         if (ballot(need) == 0ull) break;

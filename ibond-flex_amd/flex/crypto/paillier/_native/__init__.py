@@ -25,7 +25,8 @@ PAI_OPT_FIXED_BASE, PAI_OPT_FB_WINDOW = 5, 6
 
 EXPORTED = ("pai_ctx_create", "pai_ctx_set_private", "pai_ctx_destroy", "pai_ctx_info", "pai_last_error",
             "pai_ctx_set_option", "pai_ctx_get_option", "pai_ctx_stage_times", "pai_ctx_fixed_base_info",
-            "pai_encrypt", "pai_add", "pai_decrypt", "pai_encrypt_dev", "pai_add_dev", "pai_decrypt_dev")
+            "pai_encrypt", "pai_add", "pai_decrypt", "pai_encrypt_dev", "pai_add_dev", "pai_decrypt_dev",
+            "pai_mul", "pai_mul_dev", "pai_matmul", "pai_matmul_dev")
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -62,6 +63,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.pai_encrypt_dev.argtypes = [P, I, P, S, I, ctypes.c_int32, I, P, S, S, P, U64, P, P, P, P]
         lib.pai_add_dev.argtypes = [P, P, P, I, S, P, P, P]
         lib.pai_decrypt_dev.argtypes = [P, P, P, S, P, P, P, P, P]
+        lib.pai_mul.argtypes = [P, P, P, S, I, P, S, P, P, P]
+        lib.pai_mul_dev.argtypes = [P, P, P, S, I, P, S, P, P, P, P]
+        lib.pai_matmul.argtypes = [P, P, P, S, S, I, P, S, P, P]
+        lib.pai_matmul_dev.argtypes = [P, P, P, S, S, I, P, S, P, P, P]
         for name in EXPORTED:
             if name not in ("pai_ctx_destroy", "pai_last_error"):
                 getattr(lib, name).restype = ctypes.c_int
@@ -72,6 +77,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
 def _check(rc: int):
     if rc != 0:
         msg = load_library().pai_last_error().decode(errors="replace")
+        if rc == -5:
+            raise ZeroDivisionError(msg)          # gmpy_math.invert (gmpy_math.py:71-72)
         if rc == -4 and ("does not match" in msg or "have to be different" in msg):
             raise ValueError(msg)
         raise NativeError(f"flexpai error {rc}: {msg}")
@@ -230,6 +237,34 @@ class Context:
         _check(self.lib.pai_add(self._h, ct_ptrs, ex_ptrs, k, N, _ptr(out), _ptr(oe)))
         return out, oe
 
+    def mul(self, ct: np.ndarray, exp: np.ndarray, x: np.ndarray):
+        """Element-wise ct_i (x) x_i (x of size 1: one scalar for every element); returns
+        (ciphertext words, exponents, statuses). PaillierEncryptedNumber.__mul__ semantics."""
+        ct = np.ascontiguousarray(ct, dtype=np.uint32)
+        exp = np.ascontiguousarray(exp, dtype=np.int32)
+        x = np.ascontiguousarray(x)
+        N = exp.size
+        if x.size not in (1, N):
+            raise ValueError("scalar operand must have 1 or N elements")
+        out = np.empty((N, self.ct_words), dtype=np.uint32)
+        oe = np.empty(N, dtype=np.int32)
+        st = np.empty(N, dtype=np.int32)
+        _check(self.lib.pai_mul(self._h, _ptr(ct), _ptr(exp), N, scalar_dtype(x), _ptr(x), 1 if x.size == N and N > 1 else 0,
+                                _ptr(out), _ptr(oe), _ptr(st)))
+        return out, oe, st
+
+    def matmul(self, ct: np.ndarray, exp: np.ndarray, m: int, K: int, x: np.ndarray, d: int):
+        """(m x K encrypted) @ (K x d plain) -> (m d ciphertext words, m d exponents), row-major."""
+        ct = np.ascontiguousarray(ct, dtype=np.uint32)
+        exp = np.ascontiguousarray(exp, dtype=np.int32)
+        x = np.ascontiguousarray(x)
+        if exp.size != m * K or x.size != K * d:
+            raise ValueError("matmul: shape mismatch")
+        out = np.empty((m * d, self.ct_words), dtype=np.uint32)
+        oe = np.empty(m * d, dtype=np.int32)
+        _check(self.lib.pai_matmul(self._h, _ptr(ct), _ptr(exp), m, K, scalar_dtype(x), _ptr(x), d, _ptr(out), _ptr(oe)))
+        return out, oe
+
     def decrypt(self, ct: np.ndarray, exp: np.ndarray, want_raw: bool = False):
         ct = np.ascontiguousarray(ct, dtype=np.uint32)
         exp = np.ascontiguousarray(exp, dtype=np.int32)
@@ -241,6 +276,16 @@ class Context:
         _check(self.lib.pai_decrypt(self._h, _ptr(ct), _ptr(exp), N, _ptr(val), _ptr(mant), _ptr(st),
                                     _ptr(raw) if raw is not None else None))
         return val, mant, st, raw
+
+
+def scalar_dtype(x: np.ndarray) -> int:
+    if x.dtype == np.float32:
+        return PAI_F32
+    if x.dtype == np.float64:
+        return PAI_F64
+    if x.dtype == np.int64:
+        return PAI_I64
+    raise TypeError(f"unsupported dtype {x.dtype}")
 
 
 def words_to_ints(words: np.ndarray):

@@ -9,7 +9,10 @@ indexes, reshapes or pickles the result keep working unchanged. Two additions:
   do not re-serialise Python ints;
 * ``a + b`` between two encrypted arrays (the HE_SA_FT coordinator's ``iterative_add``,
   he_sa_ft/train.py:64-71, and ``sum(...)`` callers) runs as ONE batched k-way add on the GPU
-  instead of numpy's per-object loop (encrypted_number.py:166-185).
+  instead of numpy's per-object loop (encrypted_number.py:166-185);
+* ``a * s``, ``s * a``, ``a / s`` with a plain scalar or array (encrypted_number.py:80-113) run as ONE
+  GPU launch (negative scalars: one batch inversion for the whole array), and ``a.dot(x)`` /
+  ``a @ x`` with a plain matrix (he_otp_lr_ft1/train.py:160) as one launch plus a reduction tree.
 
 Pickling produces a plain object ndarray (``__reduce__``), so unmodified FLEX peers can load it.
 """
@@ -77,6 +80,38 @@ class PaillierArray(np.ndarray):
         res = add_encrypted(self, other)
         if res is NotImplemented:
             return np.ndarray.__radd__(np.asarray(self), other)
+        return res
+
+    def __mul__(self, other):
+        res = mul_plain(self, other)
+        if res is NotImplemented:
+            return np.ndarray.__mul__(np.asarray(self), other)
+        return res
+
+    def __rmul__(self, other):
+        res = mul_plain(self, other)
+        if res is NotImplemented:
+            return np.ndarray.__rmul__(np.asarray(self), other)
+        return res
+
+    def __truediv__(self, other):
+        # PaillierEncryptedNumber.__truediv__ multiplies by 1 / scalar (encrypted_number.py:83-84)
+        if _plain_scalar(other) is not None and other != 0:
+            res = mul_plain(self, 1 / other)
+            if res is not NotImplemented:
+                return res
+        return np.ndarray.__truediv__(np.asarray(self), other)
+
+    def dot(self, b, out=None):
+        res = dot_plain(self, b) if out is None else NotImplemented
+        if res is NotImplemented:
+            return np.asarray(self).dot(b, out) if out is not None else np.asarray(self).dot(b)
+        return res
+
+    def __matmul__(self, b):
+        res = dot_plain(self, b)
+        if res is NotImplemented:
+            return np.ndarray.__matmul__(np.asarray(self), b)
         return res
 
 
@@ -148,3 +183,106 @@ def add_encrypted(a, b):
     out, oe = ctx.add([wa, wb], [ea, eb])
     # __raw_add builds fresh, not-yet-obfuscated numbers (encrypted_number.py:180-185)
     return materialize(pk, out, oe, Ab.shape, obfuscated=False)
+
+
+# ------------------------------------------------------------------ ciphertext x plaintext
+_DEV_FLOAT = {np.dtype(np.float64): np.float64, np.dtype(np.float32): np.float32, np.dtype(np.float16): np.float32}
+_DEV_INT = (np.dtype(np.int16), np.dtype(np.int32), np.dtype(np.int64))
+
+
+def _plain_scalar(y):
+    """The device dtype for a plain scalar operand, following FixedPointNumber.encode's type rules
+    (fixedpoint_number.py:63-77), or None (bools, unsigned, big ints, other objects: host path)."""
+    if isinstance(y, (bool, np.bool_)):
+        return None
+    if type(y) is float or isinstance(y, np.float64):
+        return np.float64
+    if isinstance(y, (np.float32, np.float16)):
+        return np.float32
+    if (type(y) is int and -(1 << 63) < y < (1 << 63)) or isinstance(y, (np.int16, np.int32, np.int64)):
+        return np.int64
+    return None
+
+
+def _plain_array(y: np.ndarray):
+    if y.dtype in _DEV_FLOAT:
+        return y.astype(_DEV_FLOAT[y.dtype])
+    if y.dtype in _DEV_INT:
+        return y.astype(np.int64)
+    return None
+
+
+def _encrypted_operand(a):
+    """(flat object array, public key) when `a` is entirely PaillierEncryptedNumber of one key."""
+    A = np.asarray(a, dtype=object)
+    flat = A.reshape(-1)
+    if flat.size == 0 or not _all_encrypted(flat):
+        return None, None
+    pk = flat[0].public_key
+    for e in flat:
+        if e.public_key != pk:
+            return None, None
+    return A, pk
+
+
+def mul_plain(a, y):
+    """Encrypted array times a plain scalar or array on the GPU (PaillierEncryptedNumber.__mul__
+    per element, encrypted_number.py:86-113, with numpy broadcasting). NotImplemented when an
+    operand is not of a device type (the caller then falls back to the per-element operators)."""
+    from . import _runtime
+    if isinstance(y, PaillierEncryptedNumber):
+        raise ValueError("PaillierEncryptedNumber * PaillierEncryptedNumber is not allowed.")
+    A, pk = _encrypted_operand(a)
+    if A is None:
+        return NotImplemented
+    if isinstance(y, np.ndarray):
+        if y.dtype == object:
+            return NotImplemented
+        x = _plain_array(y)
+        if x is None:
+            return NotImplemented
+        try:
+            Ab, xb = np.broadcast_arrays(A, x)
+        except ValueError:
+            return NotImplemented
+        shape = Ab.shape
+        if shape != A.shape:
+            A = np.ascontiguousarray(Ab)
+        xs = np.ascontiguousarray(xb).reshape(-1)
+    else:
+        dt = _plain_scalar(y)
+        if dt is None:
+            return NotImplemented
+        shape = A.shape
+        xs = np.array([y], dtype=dt)
+    words, exps, _ = pack(a if A is a else A, pk)
+    ctx = _runtime.context(pk)
+    out, oe, st = ctx.mul(words, exps, xs)
+    # __mul__ returns fresh, not-yet-obfuscated numbers (encrypted_number.py:113)
+    return materialize(pk, out, oe, shape, obfuscated=False)
+
+
+def dot_plain(a, b):
+    """numpy dot / matmul of an encrypted (K,) or (m, K) array with a plain (K,) or (K, d) array on
+    the GPU: every output is sum_k a[.., k] * b[k, ..] with the reference's exponent alignment
+    (bit-identical to numpy's object loop over __mul__ and __add__). NotImplemented otherwise."""
+    from . import _runtime
+    if not isinstance(b, np.ndarray) or b.dtype == object or b.ndim not in (1, 2):
+        return NotImplemented
+    A, pk = _encrypted_operand(a)
+    if A is None or A.ndim not in (1, 2):
+        return NotImplemented
+    x = _plain_array(b)
+    if x is None:
+        return NotImplemented
+    K = A.shape[-1]
+    if K == 0 or x.shape[0] != K:
+        return NotImplemented
+    m = A.shape[0] if A.ndim == 2 else 1
+    d = x.shape[1] if x.ndim == 2 else 1
+    words, exps, _ = pack(a if A is a else A, pk)
+    ctx = _runtime.context(pk)
+    out, oe = ctx.matmul(words, exps, m, K, np.ascontiguousarray(x).reshape(-1), d)
+    shape = tuple(([m] if A.ndim == 2 else []) + ([d] if x.ndim == 2 else []))
+    res = materialize(pk, out, oe, shape if shape else (1,), obfuscated=False)
+    return res.reshape(-1)[0] if not shape else res

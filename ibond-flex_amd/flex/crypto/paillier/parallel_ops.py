@@ -1,13 +1,13 @@
 """parallel_ops — same API as flex/crypto/paillier/parallel_ops.py:23-129.
 
-enc + enc arrays run as one batched GPU add (cipher_array.add_encrypted) instead of one
-ProcessPoolExecutor task per element; enc + plain and enc * plain keep the reference's
-per-element semantics (scalar object operators)."""
+enc + enc arrays run as one batched GPU add (cipher_array.add_encrypted) and enc * plain as one
+batched GPU multiply (cipher_array.mul_plain) instead of one ProcessPoolExecutor task per element;
+enc + plain keeps the reference's per-element semantics (scalar object operators)."""
 from typing import Union
 
 import numpy as np
 
-from .cipher_array import PaillierArray, add_encrypted
+from .cipher_array import PaillierArray, add_encrypted, mul_plain
 
 
 def mul(x: np.ndarray, y: Union[np.ndarray, float, int]) -> np.ndarray:
@@ -40,6 +40,10 @@ def calculate(x: np.ndarray, y: Union[np.ndarray, float, int], method: str) -> n
         raise TypeError(f"{x.shape} != {y.shape}")
     if method == 'add' and isinstance(y, np.ndarray) and y.dtype == object:
         res = add_encrypted(x, y)
+        if res is not NotImplemented:
+            return res.reshape(x.shape)
+    if method == 'mul' and (isinstance(y, (int, float)) or (isinstance(y, np.ndarray) and y.dtype != object)):
+        res = mul_plain(x, y)                    # one GPU launch instead of a task per element
         if res is not NotImplemented:
             return res.reshape(x.shape)
     xf = np.asarray(x).reshape(-1)

@@ -15,6 +15,11 @@
  *                            115-137, 166-185 (k-way, order independent)
  *   pai_decrypt[_dev]     <- PaillierDecryptor.decrypt(ndarray)    flex/crypto/paillier/decryptor.py:33-127
  *                            (+ FixedPointNumber.decode fixedpoint_number.py:92-107)
+ *   pai_mul[_dev]         <- PaillierEncryptedNumber.__mul__ / __rmul__ over arrays (encrypted_number.py:80-113;
+ *                            parallel_ops.mul parallel_ops.py:23-44): c^s, or invert(c)^(n-s) for negatives
+ *   pai_matmul[_dev]      <- ndarray.dot of encrypted by plain (he_otp_lr_ft1/train.py:160,
+ *                            he_otp_lr_ft2/train.py:188): per output sum_k c_ik (x) x_kj, i.e. __mul__ then
+ *                            __add__ (encrypted_number.py:65-69, 86-113, 166-185)
  *
  * Conventions
  *   - Integers cross the boundary as little-endian bytes (key material) or little-endian 32-bit
@@ -44,6 +49,7 @@ typedef struct pai_ctx pai_ctx;
 #define PAI_ERR_HIP (-2)
 #define PAI_ERR_NOPRIV (-3)
 #define PAI_ERR_KEY (-4)
+#define PAI_ERR_NOINV (-5)  /* a ciphertext has no inverse mod n^2 (gmpy_math.invert ZeroDivisionError) */
 
 /* input dtypes for pai_encrypt */
 #define PAI_F32 0
@@ -119,7 +125,20 @@ int pai_add(pai_ctx* ctx, const uint32_t* const* cts, const int32_t* const* exps
 int pai_decrypt(pai_ctx* ctx, const uint32_t* ct, const int32_t* exp, size_t N, double* val_out,
                 int64_t* mant_out, int32_t* status_out, uint32_t* raw_out);
 
-/* Device-resident variants (device pointers, asynchronous on `stream`, a hipStream_t). */
+/* Ciphertext x plaintext, element-wise: out_i = ct_i (x) x_(i*x_stride) (x_stride 0: one scalar for all,
+ * 1: one per element), x of dtype PAI_F32/F64/I64 encoded like FixedPointNumber.encode; exponent
+ * exp_i + e(x). Negative scalars: invert(ct)^|m|, computed as ONE batch inversion for the array.
+ * status_out (nullable): PAI_EL_ENC_RANGE where the scalar does not fit the 64-bit encoder.      */
+int pai_mul(pai_ctx* ctx, const uint32_t* ct, const int32_t* exp, size_t N, int dtype, const void* x, size_t x_stride,
+            uint32_t* ct_out, int32_t* exp_out, int32_t* status_out);
+/* Encrypted (m x K, row-major ciphertexts + exponents) times plain (K x d, row-major, dtype as above):
+ * out[i][j] = sum_k ct[i][k] (x) x[k][j] with the reference's exponent alignment (bit-identical to
+ * numpy's object dot over PaillierEncryptedNumber, whose sums are order independent). */
+int pai_matmul(pai_ctx* ctx, const uint32_t* ct, const int32_t* exp, size_t m, size_t K, int dtype, const void* x,
+               size_t d, uint32_t* ct_out, int32_t* exp_out);
+
+/* Device-resident variants (device pointers, asynchronous on `stream`, a hipStream_t; pai_mul_dev and
+ * pai_matmul_dev synchronise `stream` once, for the single host-side inversion of the batch). */
 int pai_encrypt_dev(pai_ctx* ctx, int dtype, const void* d_x, size_t N, int exp_mode, int32_t fixed_exp,
                     int obf_mode, const uint32_t* d_r_words, size_t r_stride_words, size_t r_words,
                     const uint8_t* rng_key32, uint64_t index_base,
@@ -129,6 +148,10 @@ int pai_add_dev(pai_ctx* ctx, const uint32_t* d_cts, const int32_t* d_exps, int 
                 uint32_t* d_out, int32_t* d_exp_out, void* stream);
 int pai_decrypt_dev(pai_ctx* ctx, const uint32_t* d_ct, const int32_t* d_exp, size_t N, double* d_val,
                     int64_t* d_mant, int32_t* d_status, uint32_t* d_raw, void* stream);
+int pai_mul_dev(pai_ctx* ctx, const uint32_t* d_ct, const int32_t* d_exp, size_t N, int dtype, const void* d_x,
+                size_t x_stride, uint32_t* d_out, int32_t* d_exp_out, int32_t* d_status, void* stream);
+int pai_matmul_dev(pai_ctx* ctx, const uint32_t* d_ct, const int32_t* d_exp, size_t m, size_t K, int dtype,
+                   const void* d_x, size_t d, uint32_t* d_out, int32_t* d_exp_out, void* stream);
 
 #ifdef __cplusplus
 }

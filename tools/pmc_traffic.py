@@ -8,6 +8,7 @@ in KiB. Writes profiles/pmc_<kernel>_latest.json, which bench.py reports as roof
 """
 import argparse
 import csv
+import re
 import json
 import os
 
@@ -17,7 +18,7 @@ def per_launch(path, counter, kernel):
     same kernel come from the host-boundary legs). Rows of one dispatch are summed."""
     per = {}
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]:
+        if r["Counter_Name"] == counter and re.search(r"\b%s\b" % re.escape(kernel), r["Kernel_Name"]):
             d = r["Dispatch_Id"]
             per[d] = per.get(d, 0.0) + float(r["Counter_Value"])
     if not per:

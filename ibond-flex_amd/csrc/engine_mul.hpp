@@ -9,6 +9,7 @@ constexpr size_t mul_lds_bytes() { return (size_t)BLOCK * L * 4; }
 // blocks per CU of k_mul<tpi> (-1: unsupported group size)
 int mul_occupancy(int tpi, int* occ);
 hipError_t mul_launch(int tpi, const MulParams& p, int grid, hipStream_t st);
+hipError_t plain_launch(int tpi, const PlainParams& p, long long units, int cus, hipStream_t st);
 hipError_t inv_launch(int tpi, bool up, const InvParams& p, int grid, hipStream_t st);
 
 }  // namespace fpai

@@ -82,6 +82,8 @@ struct pai_ctx {
   size_t work_bytes = 0;
   void* d_mul = nullptr;        // ciphertext x plaintext terms, flags, reduction partials
   size_t mul_bytes = 0;
+  void* d_plain = nullptr;      // ciphertext + plaintext: the two k_add operands and their exponents
+  size_t plain_bytes = 0;
   void* d_inv = nullptr;        // batch-inversion prefix products and segment products
   size_t inv_bytes = 0;
   std::vector<uint32_t> inv_host;   // top of the inversion tree (host side of an async copy)
@@ -100,6 +102,7 @@ struct pai_ctx {
     if (d_work) (void)hipFree(d_work);
     if (d_mul) (void)hipFree(d_mul);
     if (d_inv) (void)hipFree(d_inv);
+    if (d_plain) (void)hipFree(d_plain);
   }
 };
 
@@ -1104,6 +1107,40 @@ int pai_mul_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t N
   return batch_invert(c, d_out, (const uint8_t*)c->d_mul, (long long)N, st);
 }
 
+// E(x) + y over arrays (encrypted_number.py:139-164): k_plain encodes y_i with max_exponent e_i into
+// c0_i = 1 + n M_i (r = 1) and E_i, then ONE 2-way k_add aligns E(x_i) to E_i and multiplies.
+int pai_add_plain_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t N, int dtype, const void* d_x,
+                      size_t x_stride, uint32_t* d_out, int32_t* d_exp_out, int32_t* d_status, void* stream) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (N == 0) return 0;
+  if (!d_ct || !d_exp || !d_x || !d_out || !d_exp_out || dtype < 0 || dtype > 2 || x_stride > 1)
+    return fail(PAI_ERR_ARG, "pai_add_plain_dev: bad arguments");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t W = c->ct_words, cbytes = align16(2 * N * W * 4);
+  int rc = ensure_buf(&c->d_plain, &c->plain_bytes, cbytes + 2 * N * 4);
+  if (rc) return rc;
+  uint32_t* ops = (uint32_t*)c->d_plain;
+  int32_t* oexp = (int32_t*)((char*)c->d_plain + cbytes);
+  HIPCHK(hipMemcpyAsync(ops, d_ct, N * W * 4, hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipMemcpyAsync(oexp, d_exp, N * 4, hipMemcpyDeviceToDevice, st));
+  PlainParams p{};
+  p.exp = d_exp;
+  p.x = d_x;
+  p.dtype = dtype;
+  p.xs = (long long)x_stride;
+  p.n = (long long)N;
+  p.c0 = ops + N * W;
+  p.e0 = oexp + N;
+  p.status = d_status;
+  p.N = c->d_N;
+  p.nl = c->d_nl;
+  p.ct_words = c->ct_words;
+  p.max_bits = c->nb - 3;
+  HIPCHK(plain_launch(c->tpi_e, p, (long long)N, c->cus, st));
+  return add_dev(c, ops, oexp, 2, (long long)N, d_out, d_exp_out, st);
+}
+
 constexpr int MATMUL_CHUNK = 16;   // operands per k_add pass of the reduction tree
 
 int pai_matmul_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t m, size_t K, int dtype,
@@ -1184,6 +1221,33 @@ int pai_mul(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, int dt
   HIPCHK(hipMemcpy(dexp, exp, N * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(dx, x, nx * esz, hipMemcpyHostToDevice));
   int rc = pai_mul_dev(c, dct, dexp, N, dtype, dx, x_stride, dout, dexo, dst, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(ct_out, dout, N * W * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(exp_out, dexo, N * 4, hipMemcpyDeviceToHost));
+  if (status_out) HIPCHK(hipMemcpy(status_out, dst, N * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int pai_add_plain(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, int dtype, const void* x,
+                  size_t x_stride, uint32_t* ct_out, int32_t* exp_out, int32_t* status_out) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (N == 0) return 0;
+  if (!ct || !exp || !x || !ct_out || !exp_out || x_stride > 1) return fail(PAI_ERR_ARG, "pai_add_plain: bad arguments");
+  HIPCHK(hipSetDevice(c->device));
+  const size_t W = c->ct_words, esz = dtype == PAI_F32 ? 4 : 8, nx = x_stride ? N : 1;
+  DevScope ds;
+  uint32_t* dct = ds.alloc<uint32_t>(N * W);
+  int32_t* dexp = ds.alloc<int32_t>(N);
+  void* dx = ds.alloc<uint8_t>(nx * esz);
+  uint32_t* dout = ds.alloc<uint32_t>(N * W);
+  int32_t* dexo = ds.alloc<int32_t>(N);
+  int32_t* dst = ds.alloc<int32_t>(N);
+  if (!dct || !dexp || !dx || !dout || !dexo || !dst) return fail(PAI_ERR_HIP, "pai_add_plain: device allocation failed");
+  HIPCHK(hipMemcpy(dct, ct, N * W * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dexp, exp, N * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(dx, x, nx * esz, hipMemcpyHostToDevice));
+  int rc = pai_add_plain_dev(c, dct, dexp, N, dtype, dx, x_stride, dout, dexo, dst, nullptr);
   if (rc) return rc;
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(ct_out, dout, N * W * 4, hipMemcpyDeviceToHost));

@@ -116,6 +116,120 @@ __global__ __launch_bounds__(BLOCK, 2) void k_mul(MulParams p) {
   }
 }
 
+// ---------------------------------------------------------------- ciphertext + plaintext
+// E(x) + y (PaillierEncryptedNumber.__add_scalar / __add_fixpointnumber, encrypted_number.py:139-164):
+// y is encoded with max_exponent = e_x (fixedpoint_number.py:81-84), giving (M, E >= e_x), and
+// raw-encrypted with r = 1: c0 = 1 + n M mod n^2 (raw_encrypt.py:37-45). k_plain writes (c0, E) as
+// the second operand of a 2-way k_add, whose alignment raises E(x) to E exactly like
+// __align_exponent / __increase_exponent_to (:115-137), then multiplies (__raw_add :180-185).
+//
+// M is exact for any exponent: M = +-mag 2^sh with mag < 2^64, so c0 needs only a shifted 4-limb
+// multiplier of n. Elements the device cannot decide bit-exactly get a status instead:
+//   ST_FLOAT_OVF  float scalar * 16^E overflows a double (OverflowError in the reference);
+//   ST_ENC_RANGE  |M| has more than max_bits (= nb - 3) bits (the reference's exact |M| > max_int test
+//                 is then made by the host).
+struct PlainParams {
+  const int32_t* exp;     // ciphertext exponents [n]: the max_exponent of each element's encode
+  const void* x;          // scalars
+  int dtype;              // PAI_F32 / PAI_F64 / PAI_I64
+  long long xs;           // scalar index = i xs (0: one scalar for every element)
+  long long n;
+  uint32_t* c0;           // [n][W] out
+  int32_t* e0;            // [n] out
+  int32_t* status;        // [n] out (nullable)
+  const uint32_t* N;      // n^2, limbs (S)
+  const uint32_t* nl;     // n, limbs (S, zero padded)
+  int ct_words;
+  int max_bits;
+};
+
+__device__ __forceinline__ int encode_plain_max(int dtype, const void* x, long long xi, int me, uint64_t& mag,
+                                                int& sh, bool& neg, int& E, int max_bits) {
+  mag = 0;
+  sh = 0;
+  neg = false;
+  if (dtype != 2) {
+    const double v = dtype == 0 ? (double)((const float*)x)[xi] : ((const double*)x)[xi];
+    if (fabs(v) < 1e-200) {            // scalar = 0, an int: exponent 0 (fixedpoint_number.py:56-57, 67-69)
+      E = max(me, 0);
+      return ST_OK;
+    }
+    int fe;
+    const double f = frexp(v, &fe);
+    const int e0 = floor_div(53 - fe, 4);
+    E = max(me, e0);
+    neg = v < 0;
+    if (E == e0) {
+      const double s = rint(ldexp(fabs(v), 4 * E));   // < 2^58: exact scaling, ties-to-even
+      mag = (uint64_t)s;
+      return ST_OK;
+    }
+    if (E >= 256 || fe + 4 * E > 1024) return ST_FLOAT_OVF;   // v * 16^E is not a finite double
+    mag = (uint64_t)ldexp(fabs(f), 53);                        // v 16^E = (f 2^53) 2^(fe - 53 + 4E)
+    sh = fe - 53 + 4 * E;                                      // > 0 since E > e0
+  } else {
+    const int64_t v = ((const int64_t*)x)[xi];
+    E = max(me, 0);
+    neg = v < 0;
+    mag = neg ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
+    if (mag == 0) return ST_OK;
+    sh = 4 * E;     // exact: numpy casts int arrays to object (Python ints) for the object add loop
+  }
+  if (mag != 0 && (64 - __clzll(mag)) + sh > max_bits) return ST_ENC_RANGE;
+  return ST_OK;
+}
+
+template <int TPI>
+__global__ __launch_bounds__(BLOCK) void k_plain(PlainParams p) {
+  constexpr int S = TPI * L;
+  constexpr int GPB = BLOCK / TPI;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int tig = threadIdx.x % TPI;
+  const int gib = threadIdx.x / TPI;
+  uint32_t* slot = smem + gib * S;
+  uint32_t m[L];
+  load_limbs_g<TPI>(p.N, m, tig);
+
+  for (long long base = (long long)blockIdx.x * GPB; base < p.n; base += (long long)gridDim.x * GPB) {
+    const long long inst = base + gib;
+    const bool valid = inst < p.n;
+    const long long ii = valid ? inst : p.n - 1;
+    uint64_t mag;
+    int sh, E;
+    bool neg;
+    const int st = encode_plain_max(p.dtype, p.x, ii * p.xs, p.exp[ii], mag, sh, neg, E, p.max_bits);
+    if (st != ST_OK) mag = 0;
+    // |M| = mag 2^sh as four LB-bit digits starting at limb q
+    const int q = sh / LB;
+    const unsigned __int128 t = (unsigned __int128)mag << (sh % LB);
+    const uint64_t D0 = (uint64_t)t & LMASK, D1 = (uint64_t)(t >> LB) & LMASK, D2 = (uint64_t)(t >> (2 * LB)) & LMASK,
+                   D3 = (uint64_t)(t >> (3 * LB));
+    uint64_t P[L];
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      const int k = tig * L + i - q;
+      uint64_t acc = 0;
+      if (k >= 0) acc += (uint64_t)p.nl[k] * D0;
+      if (k >= 1) acc += (uint64_t)p.nl[k - 1] * D1;
+      if (k >= 2) acc += (uint64_t)p.nl[k - 2] * D2;
+      if (k >= 3) acc += (uint64_t)p.nl[k - 3] * D3;
+      P[i] = acc;
+    }
+    uint32_t X[L], Dn[L], a[L];
+    normalize<TPI>(P, X, lane, tig);                    // n |M| < n^2 / 4
+    (void)sub_limbs<TPI>(m, X, Dn, lane, tig);          // n^2 - n |M|
+#pragma unroll
+    for (int i = 0; i < L; ++i) P[i] = (uint64_t)((neg && mag) ? Dn[i] : X[i]) + ((tig == 0 && i == 0) ? 1u : 0u);
+    normalize<TPI>(P, a, lane, tig);
+    emit_words<TPI>(slot, a, p.c0 + ii * p.ct_words, p.ct_words, valid, tig);
+    if (valid && tig == 0) {
+      p.e0[ii] = E;
+      if (p.status) p.status[ii] = st;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- batch inversion
 struct InvParams {
   uint32_t* x;            // [n][W] values; the down-sweep replaces flagged ones by their inverses

@@ -26,7 +26,7 @@ PAI_OPT_FIXED_BASE, PAI_OPT_FB_WINDOW = 5, 6
 EXPORTED = ("pai_ctx_create", "pai_ctx_set_private", "pai_ctx_destroy", "pai_ctx_info", "pai_last_error",
             "pai_ctx_set_option", "pai_ctx_get_option", "pai_ctx_stage_times", "pai_ctx_fixed_base_info",
             "pai_encrypt", "pai_add", "pai_decrypt", "pai_encrypt_dev", "pai_add_dev", "pai_decrypt_dev",
-            "pai_mul", "pai_mul_dev", "pai_matmul", "pai_matmul_dev")
+            "pai_mul", "pai_mul_dev", "pai_matmul", "pai_matmul_dev", "pai_add_plain", "pai_add_plain_dev")
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -65,6 +65,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.pai_decrypt_dev.argtypes = [P, P, P, S, P, P, P, P, P]
         lib.pai_mul.argtypes = [P, P, P, S, I, P, S, P, P, P]
         lib.pai_mul_dev.argtypes = [P, P, P, S, I, P, S, P, P, P, P]
+        lib.pai_add_plain.argtypes = [P, P, P, S, I, P, S, P, P, P]
+        lib.pai_add_plain_dev.argtypes = [P, P, P, S, I, P, S, P, P, P, P]
         lib.pai_matmul.argtypes = [P, P, P, S, S, I, P, S, P, P]
         lib.pai_matmul_dev.argtypes = [P, P, P, S, S, I, P, S, P, P, P]
         for name in EXPORTED:
@@ -251,6 +253,22 @@ class Context:
         st = np.empty(N, dtype=np.int32)
         _check(self.lib.pai_mul(self._h, _ptr(ct), _ptr(exp), N, scalar_dtype(x), _ptr(x), 1 if x.size == N and N > 1 else 0,
                                 _ptr(out), _ptr(oe), _ptr(st)))
+        return out, oe, st
+
+    def add_plain(self, ct: np.ndarray, exp: np.ndarray, x: np.ndarray):
+        """Element-wise ct_i (+) x_i (x of size 1: one scalar for every element); returns (ciphertext
+        words, exponents, statuses). PaillierEncryptedNumber.__add__(scalar) semantics."""
+        ct = np.ascontiguousarray(ct, dtype=np.uint32)
+        exp = np.ascontiguousarray(exp, dtype=np.int32)
+        x = np.ascontiguousarray(x)
+        N = exp.size
+        if x.size not in (1, N):
+            raise ValueError("plain operand must have 1 or N elements")
+        out = np.empty((N, self.ct_words), dtype=np.uint32)
+        oe = np.empty(N, dtype=np.int32)
+        st = np.empty(N, dtype=np.int32)
+        _check(self.lib.pai_add_plain(self._h, _ptr(ct), _ptr(exp), N, scalar_dtype(x), _ptr(x),
+                                      1 if x.size == N and N > 1 else 0, _ptr(out), _ptr(oe), _ptr(st)))
         return out, oe, st
 
     def matmul(self, ct: np.ndarray, exp: np.ndarray, m: int, K: int, x: np.ndarray, d: int):

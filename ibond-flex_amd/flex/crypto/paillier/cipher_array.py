@@ -10,6 +10,9 @@ indexes, reshapes or pickles the result keep working unchanged. Two additions:
 * ``a + b`` between two encrypted arrays (the HE_SA_FT coordinator's ``iterative_add``,
   he_sa_ft/train.py:64-71, and ``sum(...)`` callers) runs as ONE batched k-way add on the GPU
   instead of numpy's per-object loop (encrypted_number.py:166-185);
+* ``a + y``, ``y + a``, ``a - y``, ``y - a`` with a plain scalar or array (encrypted_number.py:65-78,
+  139-164: encode y with max_exponent = e_x, raw-encrypt with r = 1, align, multiply) run as ONE encode
+  launch plus ONE 2-way k_add;
 * ``a * s``, ``s * a``, ``a / s`` with a plain scalar or array (encrypted_number.py:80-113) run as ONE
   GPU launch (negative scalars: one batch inversion for the whole array), and ``a.dot(x)`` /
   ``a @ x`` with a plain matrix (he_otp_lr_ft1/train.py:160) as one launch plus a reduction tree.
@@ -73,13 +76,37 @@ class PaillierArray(np.ndarray):
     def __add__(self, other):
         res = add_encrypted(self, other)
         if res is NotImplemented:
+            res = add_plain(self, other)
+        if res is NotImplemented:
             return np.ndarray.__add__(np.asarray(self), other)
         return res
 
     def __radd__(self, other):
         res = add_encrypted(self, other)
         if res is NotImplemented:
+            res = add_plain(self, other)
+        if res is NotImplemented:
             return np.ndarray.__radd__(np.asarray(self), other)
+        return res
+
+    def __sub__(self, other):
+        # PaillierEncryptedNumber.__sub__: self + (other * -1) (encrypted_number.py:74-75)
+        res = NotImplemented
+        if _plain_operand(other):
+            res = add_plain(self, other * -1)
+        if res is NotImplemented:
+            return np.ndarray.__sub__(np.asarray(self), other)
+        return res
+
+    def __rsub__(self, other):
+        # other + (self * -1) (encrypted_number.py:77-78)
+        res = NotImplemented
+        if _plain_operand(other):
+            neg = mul_plain(self, -1)
+            if neg is not NotImplemented:
+                res = add_plain(neg, other)
+        if res is NotImplemented:
+            return np.ndarray.__rsub__(np.asarray(self), other)
         return res
 
     def __mul__(self, other):
@@ -286,3 +313,59 @@ def dot_plain(a, b):
     shape = tuple(([m] if A.ndim == 2 else []) + ([d] if x.ndim == 2 else []))
     res = materialize(pk, out, oe, shape if shape else (1,), obfuscated=False)
     return res.reshape(-1)[0] if not shape else res
+
+
+# ------------------------------------------------------------------ ciphertext + plaintext
+# numpy's object add loop casts int arrays to object, so every integer is a Python int (exact) and every
+# float a Python float; the device encoder is exact for both.
+_ADD_DEV = (np.dtype(np.float16), np.dtype(np.float32), np.dtype(np.float64),
+            np.dtype(np.int16), np.dtype(np.int32), np.dtype(np.int64))
+
+
+def _plain_operand(y) -> bool:
+    if isinstance(y, np.ndarray):
+        return y.dtype in _ADD_DEV
+    return _plain_scalar(y) is not None
+
+
+def add_plain(a, y):
+    """Encrypted array plus a plain scalar or array on the GPU (PaillierEncryptedNumber.__add__ with a
+    scalar per element, encrypted_number.py:65-72, 139-164, with numpy broadcasting). Elements the device
+    flags (see pai_add_plain in include/flexpai.h: float overflow, |M| near max_int) are
+    redone by the per-element operator, which raises the reference's exception where it does.
+    NotImplemented when an operand is not of a device type."""
+    from . import _runtime
+    if isinstance(y, PaillierEncryptedNumber) or not _plain_operand(y):
+        return NotImplemented
+    A, pk = _encrypted_operand(a)
+    if A is None:
+        return NotImplemented
+    if isinstance(y, np.ndarray):
+        x = y.astype(np.float32) if y.dtype == np.float16 else (y.astype(np.int64) if y.dtype.kind == "i" else y)
+        try:
+            Ab, xb = np.broadcast_arrays(A, x)
+            _, yb = np.broadcast_arrays(A, y)
+        except ValueError:
+            return NotImplemented
+        shape = Ab.shape
+        if shape != A.shape:
+            A = np.ascontiguousarray(Ab)
+        xs = np.ascontiguousarray(xb).reshape(-1)
+        ys = yb.reshape(-1)
+    else:
+        shape = A.shape
+        xs = np.array([y], dtype=_plain_scalar(y))
+        ys = None
+    words, exps, _ = pack(a if A is a else A, pk)
+    ctx = _runtime.context(pk)
+    out, oe, st = ctx.add_plain(words, exps, xs)
+    # __raw_add returns a fresh, not-yet-obfuscated number (encrypted_number.py:180-185)
+    res = materialize(pk, out, oe, shape, obfuscated=False)
+    bad = np.flatnonzero(st)
+    if bad.size:
+        flat_a = np.asarray(A).reshape(-1)
+        flat_r = np.asarray(res).reshape(-1)
+        for i in bad.tolist():
+            flat_r[i] = flat_a[i] + (y if ys is None else ys[i])
+        res._packed = None
+    return res

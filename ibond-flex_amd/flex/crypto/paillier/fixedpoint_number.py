@@ -18,6 +18,10 @@ def _scaled_round(scalar, exponent: int) -> int:
             return int(scalar) * 16 ** exponent
         return int(round(int(scalar) * pow(16, exponent)))
     fr = float(scalar)
+    # numpy 1.x multiplies floats in double (float32/float16 promote): a product that is not a finite
+    # double ends in OverflowError (round(inf), or int -> float of 16^E >= 2^1024)
+    if exponent >= 256 or (fr != 0.0 and math.frexp(fr)[1] + 4 * exponent > 1024):
+        raise OverflowError("cannot convert float infinity to integer")
     if exponent >= 0:
         num, den = fr.as_integer_ratio()
         num <<= 4 * exponent

@@ -2,12 +2,12 @@
 
 enc + enc arrays run as one batched GPU add (cipher_array.add_encrypted) and enc * plain as one
 batched GPU multiply (cipher_array.mul_plain) instead of one ProcessPoolExecutor task per element;
-enc + plain keeps the reference's per-element semantics (scalar object operators)."""
+enc + plain as one batched GPU encode + add (cipher_array.add_plain)."""
 from typing import Union
 
 import numpy as np
 
-from .cipher_array import PaillierArray, add_encrypted, mul_plain
+from .cipher_array import PaillierArray, add_encrypted, add_plain, mul_plain
 
 
 def mul(x: np.ndarray, y: Union[np.ndarray, float, int]) -> np.ndarray:
@@ -40,6 +40,10 @@ def calculate(x: np.ndarray, y: Union[np.ndarray, float, int], method: str) -> n
         raise TypeError(f"{x.shape} != {y.shape}")
     if method == 'add' and isinstance(y, np.ndarray) and y.dtype == object:
         res = add_encrypted(x, y)
+        if res is not NotImplemented:
+            return res.reshape(x.shape)
+    if method == 'add' and (isinstance(y, (int, float)) or (isinstance(y, np.ndarray) and y.dtype != object)):
+        res = add_plain(x, y)                    # one encode launch + one 2-way k_add
         if res is not NotImplemented:
             return res.reshape(x.shape)
     if method == 'mul' and (isinstance(y, (int, float)) or (isinstance(y, np.ndarray) and y.dtype != object)):

@@ -17,6 +17,8 @@
  *                            (+ FixedPointNumber.decode fixedpoint_number.py:92-107)
  *   pai_mul[_dev]         <- PaillierEncryptedNumber.__mul__ / __rmul__ over arrays (encrypted_number.py:80-113;
  *                            parallel_ops.mul parallel_ops.py:23-44): c^s, or invert(c)^(n-s) for negatives
+ *   pai_add_plain[_dev]   <- PaillierEncryptedNumber + plain scalar over arrays (encrypted_number.py:65-72,
+ *                            139-164 __add_scalar/__add_fixpointnumber; parallel_ops.add parallel_ops.py:47-72)
  *   pai_matmul[_dev]      <- ndarray.dot of encrypted by plain (he_otp_lr_ft1/train.py:160,
  *                            he_otp_lr_ft2/train.py:188): per output sum_k c_ik (x) x_kj, i.e. __mul__ then
  *                            __add__ (encrypted_number.py:65-69, 86-113, 166-185)
@@ -131,6 +133,14 @@ int pai_decrypt(pai_ctx* ctx, const uint32_t* ct, const int32_t* exp, size_t N, 
  * status_out (nullable): PAI_EL_ENC_RANGE where the scalar does not fit the 64-bit encoder.      */
 int pai_mul(pai_ctx* ctx, const uint32_t* ct, const int32_t* exp, size_t N, int dtype, const void* x, size_t x_stride,
             uint32_t* ct_out, int32_t* exp_out, int32_t* status_out);
+/* Ciphertext + plaintext, element-wise: out_i = ct_i (+) x_(i*x_stride), x encoded like
+ * FixedPointNumber.encode(x, max_exponent=exp_i) (fixedpoint_number.py:81-84) and raw-encrypted with r = 1,
+ * exponent max(exp_i, e(x)). status_out (nullable): PAI_EL_FLOAT_OVF where x * 16^E is not a finite double
+ * (OverflowError), PAI_EL_ENC_RANGE where |M| >= 2^(nb-3) (the exact |M| > max_int test is the caller's);
+ * those outputs are undefined and the caller redoes them. Integers are exact (numpy's object add loop sees
+ * Python ints), so int64 * 16^E never wraps. */
+int pai_add_plain(pai_ctx* ctx, const uint32_t* ct, const int32_t* exp, size_t N, int dtype, const void* x,
+                  size_t x_stride, uint32_t* ct_out, int32_t* exp_out, int32_t* status_out);
 /* Encrypted (m x K, row-major ciphertexts + exponents) times plain (K x d, row-major, dtype as above):
  * out[i][j] = sum_k ct[i][k] (x) x[k][j] with the reference's exponent alignment (bit-identical to
  * numpy's object dot over PaillierEncryptedNumber, whose sums are order independent). */
@@ -150,6 +160,9 @@ int pai_decrypt_dev(pai_ctx* ctx, const uint32_t* d_ct, const int32_t* d_exp, si
                     int64_t* d_mant, int32_t* d_status, uint32_t* d_raw, void* stream);
 int pai_mul_dev(pai_ctx* ctx, const uint32_t* d_ct, const int32_t* d_exp, size_t N, int dtype, const void* d_x,
                 size_t x_stride, uint32_t* d_out, int32_t* d_exp_out, int32_t* d_status, void* stream);
+int pai_add_plain_dev(pai_ctx* ctx, const uint32_t* d_ct, const int32_t* d_exp, size_t N, int dtype,
+                      const void* d_x, size_t x_stride, uint32_t* d_out, int32_t* d_exp_out, int32_t* d_status,
+                      void* stream);
 int pai_matmul_dev(pai_ctx* ctx, const uint32_t* d_ct, const int32_t* d_exp, size_t m, size_t K, int dtype,
                    const void* d_x, size_t d, uint32_t* d_out, int32_t* d_exp_out, void* stream);
 

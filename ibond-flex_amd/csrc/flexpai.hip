@@ -82,6 +82,8 @@ struct pai_ctx {
   size_t work_bytes = 0;
   void* d_mul = nullptr;        // ciphertext x plaintext terms, flags, reduction partials
   size_t mul_bytes = 0;
+  void* d_seg = nullptr;        // segmented sums: gather rows and the partial sums of each level
+  size_t seg_bytes = 0;
   void* d_plain = nullptr;      // ciphertext + plaintext: the two k_add operands and their exponents
   size_t plain_bytes = 0;
   void* d_inv = nullptr;        // batch-inversion prefix products and segment products
@@ -103,6 +105,7 @@ struct pai_ctx {
     if (d_mul) (void)hipFree(d_mul);
     if (d_inv) (void)hipFree(d_inv);
     if (d_plain) (void)hipFree(d_plain);
+    if (d_seg) (void)hipFree(d_seg);
   }
 };
 
@@ -1141,6 +1144,88 @@ int pai_add_plain_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, si
   return add_dev(c, ops, oexp, 2, (long long)N, d_out, d_exp_out, st);
 }
 
+// Segmented k-way add (per-bin sums of IV_FFS, hetero_bin.py:28-36): a reduction tree of
+// 16-operand k_add passes whose operands are gathered through a row index (AddParams.gidx), so segments of
+// any length share one launch per level. Segment metadata (index, offsets) is host memory.
+constexpr int SEG_CHUNK = 16;
+
+int pai_segment_add_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t N, const int64_t* index,
+                        const int64_t* seg_off, size_t nseg, uint32_t* d_out, int32_t* d_exp_out, void* stream) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (nseg == 0) return 0;
+  if (!d_ct || !d_exp || !seg_off || !d_out || !d_exp_out) return fail(PAI_ERR_ARG, "pai_segment_add_dev: bad arguments");
+  if (seg_off[0] != 0) return fail(PAI_ERR_ARG, "pai_segment_add_dev: seg_off[0] must be 0");
+  for (size_t s = 0; s < nseg; ++s)
+    if (seg_off[s + 1] < seg_off[s]) return fail(PAI_ERR_ARG, "pai_segment_add_dev: offsets must not decrease");
+  const long long total = seg_off[nseg];
+  if (total > 0 && !index) return fail(PAI_ERR_ARG, "pai_segment_add_dev: index required");
+  for (long long t = 0; t < total; ++t)
+    if (index[t] < 0 || (size_t)index[t] >= N) return fail(PAI_ERR_ARG, "pai_segment_add_dev: index out of range");
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t W = c->ct_words;
+  const int C = SEG_CHUNK;
+  // members of every segment as source rows; each level maps them to ceil(len / C) partial sums
+  std::vector<long long> len(nseg), src(total);
+  for (size_t s = 0; s < nseg; ++s) len[s] = seg_off[s + 1] - seg_off[s];
+  for (long long t = 0; t < total; ++t) src[t] = index[t];
+  long long max_parts = 0;
+  for (size_t s = 0; s < nseg; ++s) max_parts += (len[s] + C - 1) / C;
+  const size_t o_a = 0, o_b = align16(o_a + (size_t)max_parts * W * 4), o_ea = align16(o_b + (size_t)max_parts * W * 4),
+               o_eb = align16(o_ea + (size_t)max_parts * 4), o_g = align16(o_eb + (size_t)max_parts * 4),
+               need = align16(o_g + (size_t)std::max<long long>(max_parts, (long long)nseg) * C * 8);
+  int rc = ensure_buf(&c->d_seg, &c->seg_bytes, need);
+  if (rc) return rc;
+  char* b = (char*)c->d_seg;
+  uint32_t* part[2] = {(uint32_t*)(b + o_a), (uint32_t*)(b + o_b)};
+  int32_t* pexp[2] = {(int32_t*)(b + o_ea), (int32_t*)(b + o_eb)};
+  long long* d_g = (long long*)(b + o_g);
+  const uint32_t* in = d_ct;
+  const int32_t* in_e = d_exp;
+  int side = 0;
+  std::vector<long long> g;
+  for (;;) {
+    long long maxlen = 0;
+    for (size_t s = 0; s < nseg; ++s) maxlen = std::max(maxlen, len[s]);
+    const bool last = maxlen <= C;
+    // one gather row of C sources per output (padding -1); the last level has one output per segment
+    g.clear();
+    std::vector<long long> nlen(nseg), nsrc;
+    long long pos = 0;
+    for (size_t s = 0; s < nseg; ++s) {
+      const long long parts = last ? 1 : (len[s] + C - 1) / C;
+      for (long long q = 0; q < parts; ++q) {
+        for (int j = 0; j < C; ++j) {
+          const long long t = q * C + j;
+          g.push_back(t < len[s] ? src[pos + t] : -1);
+        }
+        nsrc.push_back((long long)nsrc.size());
+      }
+      pos += len[s];
+      nlen[s] = parts;
+    }
+    const long long outs = (long long)nsrc.size();
+    HIPCHK(hipMemcpyAsync(d_g, g.data(), g.size() * 8, hipMemcpyHostToDevice, st));
+    uint32_t* o = last ? d_out : part[side];
+    int32_t* oe = last ? d_exp_out : pexp[side];
+    AddParams p{in, in_e, C, o, oe, outs, c->d_N, c->d_R2, c->d_oneR, c->mprime_N, c->ct_words, nullptr, d_g};
+    switch (c->tpi_e) {
+      case 2: rc = launch_add<2>(c, p, st); break;
+      case 4: rc = launch_add<4>(c, p, st); break;
+      case 8: rc = launch_add<8>(c, p, st); break;
+      default: rc = fail(PAI_ERR_KEY, "unsupported group size");
+    }
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(st));   // the gather rows (host vector) are reused by the next level
+    if (last) return 0;
+    in = o;
+    in_e = oe;
+    side ^= 1;
+    len.swap(nlen);
+    src.swap(nsrc);
+  }
+}
+
 constexpr int MATMUL_CHUNK = 16;   // operands per k_add pass of the reduction tree
 
 int pai_matmul_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t m, size_t K, int dtype,
@@ -1253,6 +1338,31 @@ int pai_add_plain(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, 
   HIPCHK(hipMemcpy(ct_out, dout, N * W * 4, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(exp_out, dexo, N * 4, hipMemcpyDeviceToHost));
   if (status_out) HIPCHK(hipMemcpy(status_out, dst, N * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int pai_segment_add(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, const int64_t* index,
+                    const int64_t* seg_off, size_t nseg, uint32_t* ct_out, int32_t* exp_out) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (nseg == 0) return 0;
+  if ((N && (!ct || !exp)) || !seg_off || !ct_out || !exp_out) return fail(PAI_ERR_ARG, "pai_segment_add: bad arguments");
+  HIPCHK(hipSetDevice(c->device));
+  const size_t W = c->ct_words;
+  DevScope ds;
+  uint32_t* dct = ds.alloc<uint32_t>(N * W);
+  int32_t* dexp = ds.alloc<int32_t>(N);
+  uint32_t* dout = ds.alloc<uint32_t>(nseg * W);
+  int32_t* dexo = ds.alloc<int32_t>(nseg);
+  if (!dct || !dexp || !dout || !dexo) return fail(PAI_ERR_HIP, "pai_segment_add: device allocation failed");
+  if (N) {
+    HIPCHK(hipMemcpy(dct, ct, N * W * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dexp, exp, N * 4, hipMemcpyHostToDevice));
+  }
+  int rc = pai_segment_add_dev(c, dct, dexp, N, index, seg_off, nseg, dout, dexo, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(ct_out, dout, nseg * W * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(exp_out, dexo, nseg * 4, hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -47,6 +47,9 @@ struct AddParams {
   uint32_t mprime;
   int ct_words;
   uint32_t* scratch;
+  // nullable: operand j of instance i is element gidx[i k + j] of the flat cts/exps arrays (-1: padding);
+  // segmented sums (pai_segment_add) gather their members this way
+  const long long* gidx;
 };
 
 // Per-half (p: h=0, q: h=1) constants for CRT decryption; all LB-bit limb arrays of S limbs.
@@ -305,14 +308,16 @@ __global__ __launch_bounds__(BLOCK, 2) void k_add(AddParams p) {
     // padding operands (exponent PAD_EXP, used by the chunked reductions of pai_matmul) count as 1
     int E = PAD_EXP;
     for (int j = 0; j < p.k; ++j) {
-      const int ej = p.exps[(long long)j * p.n + ii];
+      const long long src = p.gidx ? p.gidx[ii * p.k + j] : (long long)j * p.n + ii;
+      const int ej = src < 0 ? PAD_EXP : p.exps[src];
       if (ej != PAD_EXP) E = max(E, ej);
     }
     uint32_t a[L];
     for (int j = 0; j < p.k; ++j) {
-      const int ej = p.exps[(long long)j * p.n + ii];
+      const long long src = p.gidx ? p.gidx[ii * p.k + j] : (long long)j * p.n + ii;
+      const int ej = src < 0 ? PAD_EXP : p.exps[src];
       const bool pad = ej == PAD_EXP;
-      words_to_limbs(p.cts + ((long long)j * p.n + ii) * p.ct_words, pad ? 0 : p.ct_words, a, tig);
+      words_to_limbs(p.cts + (src < 0 ? 0 : src) * p.ct_words, pad ? 0 : p.ct_words, a, tig);
       if (pad && tig == 0) a[0] = 1u;
       copy_g_to_lds<TPI>(slot, p.R2, tig);
       montmul<TPI>(a, a, slot, TPI, m, p.mprime, lane, tig);           // Montgomery form

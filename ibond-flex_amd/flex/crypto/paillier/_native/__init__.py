@@ -26,7 +26,8 @@ PAI_OPT_FIXED_BASE, PAI_OPT_FB_WINDOW = 5, 6
 EXPORTED = ("pai_ctx_create", "pai_ctx_set_private", "pai_ctx_destroy", "pai_ctx_info", "pai_last_error",
             "pai_ctx_set_option", "pai_ctx_get_option", "pai_ctx_stage_times", "pai_ctx_fixed_base_info",
             "pai_encrypt", "pai_add", "pai_decrypt", "pai_encrypt_dev", "pai_add_dev", "pai_decrypt_dev",
-            "pai_mul", "pai_mul_dev", "pai_matmul", "pai_matmul_dev", "pai_add_plain", "pai_add_plain_dev")
+            "pai_mul", "pai_mul_dev", "pai_matmul", "pai_matmul_dev", "pai_add_plain", "pai_add_plain_dev",
+            "pai_segment_add", "pai_segment_add_dev")
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -67,6 +68,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.pai_mul_dev.argtypes = [P, P, P, S, I, P, S, P, P, P, P]
         lib.pai_add_plain.argtypes = [P, P, P, S, I, P, S, P, P, P]
         lib.pai_add_plain_dev.argtypes = [P, P, P, S, I, P, S, P, P, P, P]
+        lib.pai_segment_add.argtypes = [P, P, P, S, P, P, S, P, P]
+        lib.pai_segment_add_dev.argtypes = [P, P, P, S, P, P, S, P, P, P]
         lib.pai_matmul.argtypes = [P, P, P, S, S, I, P, S, P, P]
         lib.pai_matmul_dev.argtypes = [P, P, P, S, S, I, P, S, P, P, P]
         for name in EXPORTED:
@@ -270,6 +273,22 @@ class Context:
         _check(self.lib.pai_add_plain(self._h, _ptr(ct), _ptr(exp), N, scalar_dtype(x), _ptr(x),
                                       1 if x.size == N and N > 1 else 0, _ptr(out), _ptr(oe), _ptr(st)))
         return out, oe, st
+
+    def segment_add(self, ct: np.ndarray, exp: np.ndarray, index: np.ndarray, seg_off: np.ndarray):
+        """Per-segment k-way sums: segment s = ct[index[seg_off[s]:seg_off[s+1]]]. Returns (words [nseg, W],
+        exponents [nseg]); an empty segment gives ciphertext 1 and exponent INT32_MIN."""
+        ct = np.ascontiguousarray(ct, dtype=np.uint32)
+        exp = np.ascontiguousarray(exp, dtype=np.int32)
+        index = np.ascontiguousarray(index, dtype=np.int64)
+        seg_off = np.ascontiguousarray(seg_off, dtype=np.int64)
+        nseg = seg_off.size - 1
+        out = np.empty((max(nseg, 0), self.ct_words), dtype=np.uint32)
+        oe = np.empty(max(nseg, 0), dtype=np.int32)
+        if nseg <= 0:
+            return out, oe
+        _check(self.lib.pai_segment_add(self._h, _ptr(ct), _ptr(exp), exp.size, _ptr(index), _ptr(seg_off), nseg,
+                                        _ptr(out), _ptr(oe)))
+        return out, oe
 
     def matmul(self, ct: np.ndarray, exp: np.ndarray, m: int, K: int, x: np.ndarray, d: int):
         """(m x K encrypted) @ (K x d plain) -> (m d ciphertext words, m d exponents), row-major."""

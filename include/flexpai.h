@@ -19,6 +19,8 @@
  *                            parallel_ops.mul parallel_ops.py:23-44): c^s, or invert(c)^(n-s) for negatives
  *   pai_add_plain[_dev]   <- PaillierEncryptedNumber + plain scalar over arrays (encrypted_number.py:65-72,
  *                            139-164 __add_scalar/__add_fixpointnumber; parallel_ops.add parallel_ops.py:47-72)
+ *   pai_segment_add[_dev] <- per-bin sums sum(y[i]) over index lists (hetero_bin.py:28-36, IV_FFS
+ *                            iv_ffs/compute.py:77-93): one k-way aligned product per segment
  *   pai_matmul[_dev]      <- ndarray.dot of encrypted by plain (he_otp_lr_ft1/train.py:160,
  *                            he_otp_lr_ft2/train.py:188): per output sum_k c_ik (x) x_kj, i.e. __mul__ then
  *                            __add__ (encrypted_number.py:65-69, 86-113, 166-185)
@@ -141,6 +143,12 @@ int pai_mul(pai_ctx* ctx, const uint32_t* ct, const int32_t* exp, size_t N, int 
  * Python ints), so int64 * 16^E never wraps. */
 int pai_add_plain(pai_ctx* ctx, const uint32_t* ct, const int32_t* exp, size_t N, int dtype, const void* x,
                   size_t x_stride, uint32_t* ct_out, int32_t* exp_out, int32_t* status_out);
+/* Segmented k-way add: out_s = prod over t in [seg_off[s], seg_off[s+1]) of ct[index[t]] aligned to the
+ * segment's maximum exponent (same as pai_add over the members). index and seg_off (nseg + 1 offsets,
+ * seg_off[0] = 0, non-decreasing) are host arrays in both variants. An empty segment yields ciphertext 1
+ * with exponent INT32_MIN. The _dev variant synchronises `stream` once per reduction level. */
+int pai_segment_add(pai_ctx* ctx, const uint32_t* ct, const int32_t* exp, size_t N, const int64_t* index,
+                    const int64_t* seg_off, size_t nseg, uint32_t* ct_out, int32_t* exp_out);
 /* Encrypted (m x K, row-major ciphertexts + exponents) times plain (K x d, row-major, dtype as above):
  * out[i][j] = sum_k ct[i][k] (x) x[k][j] with the reference's exponent alignment (bit-identical to
  * numpy's object dot over PaillierEncryptedNumber, whose sums are order independent). */
@@ -163,6 +171,8 @@ int pai_mul_dev(pai_ctx* ctx, const uint32_t* d_ct, const int32_t* d_exp, size_t
 int pai_add_plain_dev(pai_ctx* ctx, const uint32_t* d_ct, const int32_t* d_exp, size_t N, int dtype,
                       const void* d_x, size_t x_stride, uint32_t* d_out, int32_t* d_exp_out, int32_t* d_status,
                       void* stream);
+int pai_segment_add_dev(pai_ctx* ctx, const uint32_t* d_ct, const int32_t* d_exp, size_t N, const int64_t* index,
+                        const int64_t* seg_off, size_t nseg, uint32_t* d_out, int32_t* d_exp_out, void* stream);
 int pai_matmul_dev(pai_ctx* ctx, const uint32_t* d_ct, const int32_t* d_exp, size_t m, size_t K, int dtype,
                    const void* d_x, size_t d, uint32_t* d_out, int32_t* d_exp_out, void* stream);
 

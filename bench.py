@@ -111,6 +111,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-decrypt", action="store_true")
     ap.add_argument("--no-public", action="store_true", help="skip timing the public-key path beside CRT")
+    ap.add_argument("--no-add8", action="store_true", help="skip the configs[2] leg (encrypt 8 arrays, 8-way add, decrypt)")
     ap.add_argument("--no-host", action="store_true", help="skip the host-boundary (PCIe, Python objects) rates")
     ap.add_argument("--host-sample", type=int, default=1 << 16,
                     help="elements for the Python-object (PaillierEncryptor.encrypt) rate")
@@ -256,6 +257,58 @@ def main():
         extra["roundtrip_exact"] = ok
         if not ok:
             raise SystemExit("decrypt(encrypt(x)) != x on the device")
+
+    # configs[2]: encrypt 8 arrays (default_rng(k), k = 0..7), one 8-way homomorphic add (k_add), decrypt the
+    # sum; device-resident, HIP events on the launch stream; the decrypted sum is checked against float64
+    if not args.no_add8 and not args.no_decrypt:
+        K8 = 8
+        xs8 = torch.stack([torch.from_numpy(np.random.default_rng(k).standard_normal(N, dtype=np.float32))
+                           for k in range(K8)]).to(dev)
+        cts8 = torch.empty((K8, N, W), dtype=torch.int32, device=dev)
+        exs8 = torch.empty((K8, N), dtype=torch.int32, device=dev)
+        sum_ct = torch.empty((N, W), dtype=torch.int32, device=dev)
+        sum_ex = torch.empty(N, dtype=torch.int32, device=dev)
+        val8 = torch.empty(N, dtype=torch.float64, device=dev)
+        st8 = torch.empty(N, dtype=torch.int32, device=dev)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        torch.cuda.synchronize()
+        t8 = time.perf_counter()
+        ev[0].record(stream)
+        for k in range(K8):
+            rc = lib.pai_encrypt_dev(ctx.handle, _native.PAI_F32, xs8[k].data_ptr(), N, 0, 0, _native.PAI_OBF_RNG,
+                                     None, 0, 0, rng_key, index_base + (k + 1) * total, cts8[k].data_ptr(),
+                                     exs8[k].data_ptr(), st.data_ptr(), stream.cuda_stream)
+            if rc != 0:
+                raise RuntimeError(lib.pai_last_error().decode())
+        ev[1].record(stream)
+        rc = lib.pai_add_dev(ctx.handle, cts8.data_ptr(), exs8.data_ptr(), K8, N, sum_ct.data_ptr(),
+                             sum_ex.data_ptr(), stream.cuda_stream)
+        if rc != 0:
+            raise RuntimeError(lib.pai_last_error().decode())
+        ev[2].record(stream)
+        rc = lib.pai_decrypt_dev(ctx.handle, sum_ct.data_ptr(), sum_ex.data_ptr(), N, val8.data_ptr(), None,
+                                 st8.data_ptr(), None, stream.cuda_stream)
+        if rc != 0:
+            raise RuntimeError(lib.pai_last_error().decode())
+        ev[3].record(stream)
+        torch.cuda.synchronize()
+        wall8 = time.perf_counter() - t8
+        ref = xs8.double().sum(0)
+        err = float((val8 - ref).abs().max().item())
+        add_ms = ev[1].elapsed_time(ev[2])
+        # canonical add work: (k-1) products + 4 d squarings per operand aligned by d
+        E = exs8.max(0).values
+        sq = int((4 * (E.unsqueeze(0) - exs8)).sum().item())
+        add_work = (N * (K8 - 1) + sq) * _M(args.nb // 16)
+        extra["config3_add8"] = {
+            "workload": "configs[2]: encrypt 8 x 1M float32 arrays, one 8-way add, decrypt the sum (device-resident)",
+            "elements_per_s": N / wall8, "wall_s": wall8,
+            "encrypt8_ms": ev[0].elapsed_time(ev[1]), "k_add_ms": add_ms, "decrypt_ms": ev[2].elapsed_time(ev[3]),
+            "k_add_int_mac_frac": add_work / (add_ms * 1e-3) / INT_MAC_PEAK,
+            "k_add_alignment_squarings_per_elem": sq / N,
+            "max_abs_err_vs_float64_sum": err, "statuses_ok": int((st8 > 1).sum().item()) == 0}
+        del xs8, cts8, exs8, sum_ct, sum_ex, val8, st8
+        torch.cuda.empty_cache()
 
     # host boundary (DESIGN.md §Host boundary): plaintexts start in host numpy and ciphertexts leave as
     # host buffers / PaillierEncryptedNumber objects; never part of `value`

@@ -36,3 +36,24 @@ def gather_shards(local, total: int, world: int, group=None):
         dist.all_gather(parts, local.contiguous(), group=group)
         out = torch.cat(parts)
     return out[:total]
+
+
+def gather_shards_async(local, total: int, world: int, group=None):
+    """Like gather_shards, but the collective is issued asynchronously: returns (out, work). On GPUs
+    the RCCL all-gather runs on the process group's own stream (ordered after the work already queued
+    on the current stream), so the caller can launch the next shard's kernels on the compute stream
+    while it runs, and calls work.wait() before reusing `local` or reading `out`. work is None when
+    the gather completed synchronously (CPU tensors)."""
+    import torch
+    import torch.distributed as dist
+    per = -(-total // world)
+    if local.shape[0] > per:
+        raise ValueError("shard larger than ceil(total / world)")
+    if not local.is_cuda:
+        return gather_shards(local, total, world, group), None
+    if local.shape[0] < per:
+        pad = torch.zeros((per - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        local = torch.cat([local, pad])
+    out = torch.empty((world * per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    work = dist.all_gather_into_tensor(out, local.contiguous(), group=group, async_op=True)
+    return out[:total], work

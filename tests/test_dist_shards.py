@@ -40,11 +40,15 @@ def _worker(rank, world, port, keyt, x, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from flex.crypto.paillier.sharding import gather_shards, shard_bounds
+        from flex.crypto.paillier.sharding import gather_shards, gather_shards_async, shard_bounds
         key = O.Key(*keyt)
         s0, s1 = shard_bounds(TOTAL, world, rank)
         local = torch.from_numpy(_encrypt_range(key, x, s0, s1).view(np.int32).copy())
         full = gather_shards(local, TOTAL, world)
+        full2, work = gather_shards_async(local, TOTAL, world)
+        if work is not None:
+            work.wait()
+        assert torch.equal(full, full2)
         if rank == 0:
             q.put(full.numpy().view(np.uint32).copy())
     finally:

@@ -106,6 +106,8 @@ def main():
     ap.add_argument("--path", choices=("crt", "public"), default="crt")
     ap.add_argument("--obf", choices=("fixedbase", "generic"), default="fixedbase",
                     help="device-RNG sampler of r^n on the CRT path (kernels_fb.hpp vs r from ChaCha20)")
+    ap.add_argument("--fb-window", type=int, default=20, choices=(8, 12, 16, 20),
+                    help="digit window of the fixed-base tables (20: 55 products per half, 17.5 GB table per half)")
     ap.add_argument("--cpu-sample", type=int, default=16384)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -138,6 +140,8 @@ def main():
     use_fb = use_crt and args.obf == "fixedbase"
     ctx.set_fixed_base(use_fb)
     use_fb = use_fb and ctx.fixed_base
+    if use_fb:
+        ctx.set_fb_window(args.fb_window)     # a dedicated encrypt GPU: 2 x 17.5 GB of tables at W = 20
     fb_info = ctx.fixed_base_info() if use_fb else None
     ctx.set_stage_timing(True)
     lib = _native.load_library()

@@ -368,7 +368,7 @@ static int upload_fb(pai_ctx* c, const std::vector<T>& v, T** out) {
 static int fb_default_window() {
   const char* e = getenv("FLEXPAI_FB_WINDOW");
   const int w = e ? atoi(e) : 16;
-  return (w == 8 || w == 12 || w == 16) ? w : 16;
+  return (w == 8 || w == 12 || w == 16 || w == 20) ? w : 16;
 }
 
 // (Re)builds the fixed-base tables for window c->fb_W from the key material saved by setup_fb.
@@ -607,7 +607,8 @@ int pai_ctx_set_option(pai_ctx* c, int option, int value) {
     case PAI_OPT_LANE_DECRYPT: c->dec_lane_enabled = value != 0; return 0;
     case PAI_OPT_FIXED_BASE: c->fb_enabled = value != 0; return 0;
     case PAI_OPT_FB_WINDOW:
-      if (value != 8 && value != 12 && value != 16) return fail(PAI_ERR_ARG, "fixed-base window must be 8, 12 or 16");
+      if (value != 8 && value != 12 && value != 16 && value != 20)
+        return fail(PAI_ERR_ARG, "fixed-base window must be 8, 12, 16 or 20");
       if (value == c->fb_W) return 0;
       c->fb_W = value;
       if (!c->fb_sb) return 0;   // applied when the private key is set
@@ -715,7 +716,7 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
   int occF = 1;
   if (fb && fb_occupancy(SB, &occF)) return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
   const int gxF = (int)std::max<long long>(1, std::min<long long>(lanes_blocks, (long long)occF * c->cus / 2));
-  const size_t ybytes = std::max((size_t)2 * SA * 4, fb ? (size_t)2 * c->fb_K * 2 : 0);   // per element
+  const size_t ybytes = std::max((size_t)2 * SA * 4, fb ? (size_t)2 * c->fb_K * 4 : 0);   // per element
   if ((rc = ensure_work(c, (ybytes + (size_t)2 * SB * 4) * chunk))) return rc;
   uint32_t* y = (uint32_t*)c->d_work;
   uint32_t* u = (uint32_t*)((char*)c->d_work + ybytes * chunk);
@@ -729,7 +730,7 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
       pd.index_base = e.index_base + (unsigned long long)off;
       pd.K = c->fb_K;
       pd.W = c->fb_W;
-      pd.digits = (uint16_t*)y;
+      pd.digits = y;
       const int gD = (int)std::min<long long>((long long)4 * c->cus, (n + LANE_BLOCK - 1) / LANE_BLOCK);
       stage_mark(c, 0, st);
       HIPCHK(fb_launch_digits(pd, gD, st));
@@ -739,7 +740,7 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
       pf.n = n;
       pf.K = c->fb_K;
       pf.W = c->fb_W;
-      pf.digits = (const uint16_t*)y;
+      pf.digits = y;
       pf.out = u;
       HIPCHK(fb_launch(SB, pf, (int)std::min<long long>(gxF, (n + LANE_BLOCK - 1) / LANE_BLOCK), st));
       stage_mark(c, 2, st);

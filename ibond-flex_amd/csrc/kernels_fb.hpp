@@ -27,7 +27,7 @@ namespace fpai {
 
 constexpr uint32_t FB_NONCE = 0x66786230u;   // ChaCha20 nonce word 2 (+ half) of the exponent stream
 constexpr int FB_MAX_WORDS = 48;             // exponent words per element (3 ChaCha blocks): K W <= 1536
-constexpr int FB_LO = 256;                   // entries of the per-position small tables (k_fb_lohi)
+constexpr int FB_LO = 1024;                  // entries of the per-position small tables (k_fb_lohi): W <= 20
 
 struct FbHalf {
   const uint4* table;      // [K][2^W][TQ] quads: G^(d 2^(W k)) R mod p_h^2, canonical (rows contiguous)
@@ -44,7 +44,7 @@ struct FbParams {
   const FbHalf* halves;    // [2]
   long long n;             // elements
   int K, W;                // digit positions, digit bits
-  const uint16_t* digits;  // [2][K][n] (k_fb_digits)
+  const uint32_t* digits;  // [2][K][n] (k_fb_digits)
   uint32_t* out;           // u [2][SB][n]
 };
 
@@ -53,7 +53,7 @@ struct FbDigitParams {
   uint32_t rng_key[8];
   unsigned long long index_base;
   int K, W;
-  uint16_t* digits;        // [2][K][n]
+  uint32_t* digits;        // [2][K][n]
 };
 
 // Exponent digits of both halves: a_h = the first K W bits (little-endian) of the ChaCha20 stream
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_fb_digits(FbDigitParams p) {
     for (int k = 0; k < p.K; ++k) {
       const int bit = k * p.W, wi = bit >> 5, sh = bit & 31;
       const uint64_t v = (((uint64_t)my[wi + 1] << 32) | my[wi]) >> sh;
-      p.digits[((size_t)half * p.K + k) * p.n + i] = (uint16_t)(v & mask);
+      p.digits[((size_t)half * p.K + k) * p.n + i] = (uint32_t)(v & mask);
     }
   }
 }
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_fb(FbParams p) {
   for (long long base = (long long)blockIdx.x * LANE_BLOCK; base < p.n; base += (long long)gridDim.x * LANE_BLOCK) {
     const long long i = base + threadIdx.x;
     const long long ii = i < p.n ? i : p.n - 1;
-    const uint16_t* dg = p.digits + (size_t)half * K * p.n + ii;   // digit k at dg[k * n]
+    const uint32_t* dg = p.digits + (size_t)half * K * p.n + ii;   // digit k at dg[k * n]
     // a = T_0[d_0] (Montgomery form)
     uint32_t a[SB];
     {
@@ -210,7 +210,6 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_fb_lohi(const FbHalf* halves, in
   const int k = blockIdx.x, half = blockIdx.y;
   const FbHalf* H = halves + half;
   const int LO = W / 2, HI = W - LO;
-  const uint32_t j = threadIdx.x;
   uint32_t m[SB], x[SB], t[SB], acc[SB];
 #pragma unroll
   for (int i = 0; i < SB; ++i) {
@@ -223,7 +222,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_fb_lohi(const FbHalf* halves, in
     const int bits = s ? HI : LO;
     if (s == 1)
       for (int q = 0; q < LO; ++q) lane::mont_sqr<SB>(x, m, H->mprime);   // B_k^(2^LO) R
-    if (j < (1u << bits)) {
+    for (uint32_t j = threadIdx.x; j < (1u << bits); j += blockDim.x) {
 #pragma unroll
       for (int i = 0; i < SB; ++i) acc[i] = H->oneR[i];
       for (int b = bits - 1; b >= 0; --b) {

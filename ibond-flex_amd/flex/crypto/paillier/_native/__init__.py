@@ -184,7 +184,7 @@ class Context:
         return self._get_option(PAI_OPT_FB_WINDOW)
 
     def set_fb_window(self, bits: int):
-        """Digit window of the fixed-base tables (8, 12 or 16); rebuilds them."""
+        """Digit window of the fixed-base tables (8, 12, 16 or 20); rebuilds them."""
         _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_FB_WINDOW, int(bits)))
 
     def close(self):

@@ -87,7 +87,7 @@ typedef struct pai_ctx pai_ctx;
                                     r^n through fixed bases (G_p^a_p, G_q^a_q: same distribution as
                                     r^n for uniform r, see pai_ctx_fixed_base_info); 0: r from the
                                     ChaCha20 stream and r^n by exponentiation. Read back: 1 when used */
-#define PAI_OPT_FB_WINDOW 6      /* digit window of the fixed-base tables: 8, 12 or 16 bits (default 16, or
+#define PAI_OPT_FB_WINDOW 6      /* digit window of the fixed-base tables: 8, 12, 16 or 20 bits (default 16, or
                                     $FLEXPAI_FB_WINDOW); setting it rebuilds the tables (K 2^W rows per half) */
 
 int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** out);

@@ -119,7 +119,7 @@ def test_fixed_base_jacobi_statistics(ctxs):
 
 @pytest.mark.parametrize("nb", [1024, 2048])
 def test_fixed_base_windows(ctxs, nb):
-    """Windows 8, 12, 16 rebuild the tables; each is bit-exact against the oracle, and 8 and 16
+    """Windows 8, 12, 16, 20 rebuild the tables; each is bit-exact against the oracle, and 8 and 16
     (same 1088-bit exponent for 2048-bit keys, 576-bit for 1024-bit) give identical ciphertexts."""
     N = _native()
     ctx, key = ctxs[nb]
@@ -128,7 +128,7 @@ def test_fixed_base_windows(ctxs, nb):
     x = np.random.default_rng(nb).standard_normal(300).astype(np.float32)
     outs = {}
     try:
-        for w in (8, 12, 16):
+        for w in (8, 12, 16, 20):
             ctx.set_fb_window(w)
             params = ctx.fixed_base_info()
             assert params[3] == w

@@ -369,3 +369,60 @@ def add_plain(a, y):
             flat_r[i] = flat_a[i] + (y if ys is None else ys[i])
         res._packed = None
     return res
+
+
+# ------------------------------------------------------------------ bulk wire format
+# The reference ships ciphertext arrays as pickled object ndarrays (Ion._send, ion.py:150-178): ~543 B
+# and one Python object per element at nb = 2048. The bulk format is the packed device layout itself:
+#   magic "FPAW1\0" | u32 ndim | i64 shape[ndim] | u32 n_bytes | n (little-endian) | u32 W |
+#   i32 exponents[N] | u8 obfuscated[N] | u32 words[N][W]
+# i.e. 4 W + 5 bytes per element plus a header; ciphertext i = int.from_bytes(words[i], "little").
+# Pickling a PaillierArray still yields a plain object ndarray, so unmodified peers are unaffected.
+_WIRE_MAGIC = b"FPAW1\0"
+
+
+def to_wire(arr) -> bytes:
+    """Serialise an array of PaillierEncryptedNumber (one public key) into the bulk format."""
+    A, pk = _encrypted_operand(arr)
+    if A is None:
+        raise TypeError("to_wire needs a non-empty array of PaillierEncryptedNumber with one public key")
+    words, exps, _ = pack(arr if isinstance(arr, PaillierArray) else A, pk)
+    obf = np.fromiter((e._is_obfuscated() for e in A.reshape(-1)), dtype=np.uint8, count=A.size)
+    nb = (pk.n.bit_length() + 7) // 8
+    head = [_WIRE_MAGIC, np.uint32(A.ndim).tobytes(), np.asarray(A.shape, dtype="<i8").tobytes(),
+            np.uint32(nb).tobytes(), pk.n.to_bytes(nb, "little"), np.uint32(words.shape[1]).tobytes()]
+    return b"".join(head + [np.ascontiguousarray(exps, dtype="<i4").tobytes(), obf.tobytes(),
+                            np.ascontiguousarray(words, dtype="<u4").tobytes()])
+
+
+def from_wire(buf, public_key=None) -> PaillierArray:
+    """Inverse of to_wire. `public_key` (optional) must match the key in the buffer (ValueError
+    otherwise, like encrypted_number.py:169-170); without it a PaillierPublicKey is rebuilt from n."""
+    from .keypair import PaillierPublicKey
+    mv = memoryview(buf)
+    if bytes(mv[:6]) != _WIRE_MAGIC:
+        raise ValueError("not a flexpai ciphertext array")
+    o = 6
+    ndim = int(np.frombuffer(mv, "<u4", 1, o)[0]); o += 4
+    shape = tuple(int(v) for v in np.frombuffer(mv, "<i8", ndim, o)); o += 8 * ndim
+    nb = int(np.frombuffer(mv, "<u4", 1, o)[0]); o += 4
+    n = int.from_bytes(mv[o:o + nb], "little"); o += nb
+    W = int(np.frombuffer(mv, "<u4", 1, o)[0]); o += 4
+    N = int(np.prod(shape)) if shape else 1
+    exps = np.frombuffer(mv, "<i4", N, o).astype(np.int32); o += 4 * N
+    obf = np.frombuffer(mv, np.uint8, N, o); o += N
+    words = np.frombuffer(mv, "<u4", N * W, o).reshape(N, W).copy(); o += 4 * N * W
+    if o != len(mv):
+        raise ValueError("corrupted ciphertext array (length mismatch)")
+    if public_key is None:
+        public_key = PaillierPublicKey(n)
+    elif public_key.n != n:
+        raise ValueError("ciphertext array was encrypted under a different public key")
+    res = materialize(public_key, words, exps, shape, obfuscated=False)
+    flat = np.asarray(res).reshape(-1)
+    for i in np.flatnonzero(obf).tolist():
+        e = flat[i]
+        flat[i] = PaillierEncryptedNumber._make(public_key, e.ciphertext(False), e.exponent, True)
+    if obf.any():
+        res._packed = None
+    return res

@@ -7,11 +7,16 @@ encode -> c0 = 1 + n*m -> c0 * r^n mod n^2 with a device ChaCha20 obfuscator r p
 the ciphertext shards so every rank holds the whole encrypted vector (weak scaling).
 
 The workload (BASELINE.json configs[1]: "encrypt+decrypt on 1 MI355X") holds the private key, so
-the default path is the CRT encryption (kernels_crt.hpp: r^n via half-size exponentiations mod p,
-p^2, q, q^2; bit-identical ciphertexts). The public-key-only kernel is timed on the same input in
-the same run and reported as `public_key_path`; `--path public` makes it the timed path.
+the default path is the key holder's: r^n sampled through fixed-base tables per CRT half
+(kernels_fb.hpp, `--obf fixedbase`, digit window `--fb-window`, default 20) and recombined with c0
+(k_crt_fin). The generic CRT path (`--obf generic`: r from the ChaCha20 stream, r^n by half-size
+exponentiations, bit-identical to the public-key kernel and GMP), the public-key-only kernel,
+device decryption, the configs[2] leg (8 arrays, 8-way add, decrypt) and the host-boundary rates
+are measured on the same input in the same run, outside the timed region, under `extra`.
+For N > 1 the ciphertext and exponent shards are double-buffered and step i's all-gather overlaps
+step i+1's encryption.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--path crt|public]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--path crt|public] [--obf fixedbase|generic]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU)
 
 Rank 0 prints ONE JSON line. `value` = encrypts/s over all ranks (max-over-ranks wall clock of the

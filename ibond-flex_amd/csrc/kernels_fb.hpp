@@ -141,10 +141,13 @@ __device__ __forceinline__ void fb_row_to_lds(const uint4* __restrict__ table, s
                                      (__attribute__((address_space(3))) void*)(wave_row0 + g * LANE_BLOCK), 16, 0, 0);
 }
 
+// One LDS row buffer per wave (78 KB per 4-wave block): two blocks -- two waves per SIMD -- fit a CU,
+// so a wave waiting for its next table row is covered by the other wave's product instead of by a
+// second buffer (which would hold the CU to one wave per SIMD: measured 18 % wait cycles).
 template <int SB>
-__global__ __launch_bounds__(LANE_BLOCK, 1) void k_fb(FbParams p) {
+__global__ __launch_bounds__(LANE_BLOCK, 2) void k_fb(FbParams p) {
   constexpr int TQ = tile_quads<SB>();
-  __shared__ uint4 lbuf[2 * TQ * LANE_BLOCK];
+  __shared__ uint4 lbuf[TQ * LANE_BLOCK];
   const int half = blockIdx.y;
   const FbHalf* H = p.halves + half;
   uint32_t m[SB];
@@ -153,10 +156,9 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_fb(FbParams p) {
   const uint32_t mprime = H->mprime;
   const uint4* table = H->table;
   const int K = p.K, W = p.W;
-  uint4* brow[2] = {lbuf + (threadIdx.x & ~63u), lbuf + TQ * LANE_BLOCK + (threadIdx.x & ~63u)};
+  uint4* brow = lbuf + (threadIdx.x & ~63u);
   typedef __attribute__((address_space(3))) uint4 lds_uint4;
-  const uint32_t addr0 = (uint32_t)(size_t)(lds_uint4*)(lbuf + threadIdx.x);                   // LDS byte offsets
-  const uint32_t addr1 = (uint32_t)(size_t)(lds_uint4*)(lbuf + TQ * LANE_BLOCK + threadIdx.x);
+  const uint32_t addr0 = (uint32_t)(size_t)(lds_uint4*)(lbuf + threadIdx.x);                   // LDS byte offset
   for (long long base = (long long)blockIdx.x * LANE_BLOCK; base < p.n; base += (long long)gridDim.x * LANE_BLOCK) {
     const long long i = base + threadIdx.x;
     const long long ii = i < p.n ? i : p.n - 1;
@@ -173,26 +175,26 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_fb(FbParams p) {
     uint32_t dn = dg[p.n];                                 // digit 1
     asm volatile("" : "+v"(dn));
     uint32_t dn2 = K > 2 ? dg[2 * p.n] : 0u;               // digit 2, in flight
-    fb_row_to_lds<SB>(table, ((size_t)1 << W) + dn, brow[0]);
+    fb_row_to_lds<SB>(table, ((size_t)1 << W) + dn, brow);
     for (int k = 1; k < K; ++k) {
-      lds_dma_wait();                                   // row k landed in buffer (k-1)&1, digit k+1 loaded
+      lds_dma_wait();                                   // row k landed, digit k+1 loaded
+      fb_mont_mul<SB>(a, addr0, m, mprime);             // every read of the row completes inside
       if (k + 1 < K) {
         const uint32_t dk1 = dn2;
         if (k + 2 < K) dn2 = dg[(size_t)(k + 2) * p.n];
-        fb_row_to_lds<SB>(table, ((size_t)(k + 1) << W) + dk1, brow[k & 1]);
+        fb_row_to_lds<SB>(table, ((size_t)(k + 1) << W) + dk1, brow);
       }
-      fb_mont_mul<SB>(a, (k & 1) ? addr0 : addr1, m, mprime);
     }
-    // u_h = G^a * coef (leaves the Montgomery domain); no DMA is in flight and every read of
-    // either buffer has completed, so buffer K&1 takes the coefficient
+    // u_h = G^a * coef (leaves the Montgomery domain); no DMA is in flight and every read of the
+    // buffer has completed, so it takes the coefficient
     {
-      uint4* col = (K & 1) ? lbuf + TQ * LANE_BLOCK + threadIdx.x : lbuf + threadIdx.x;
+      uint4* col = lbuf + threadIdx.x;
       uint32_t cv[SB];
 #pragma unroll
       for (int j = 0; j < SB; ++j) cv[j] = H->c1[j];
 #pragma unroll
       for (int g = 0; g < TQ; ++g) col[g * LANE_BLOCK] = pack_quad<SB>(cv, g);
-      fb_mont_mul<SB>(a, (K & 1) ? addr1 : addr0, m, mprime);
+      fb_mont_mul<SB>(a, addr0, m, mprime);
     }
     if (i < p.n) {
 #pragma unroll

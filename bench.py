@@ -73,16 +73,19 @@ def work_crt(nb: int) -> dict:
 
 
 def fb_digit_count(nb: int, window: int) -> int:
-    """Exponent digits K of the fixed-base sampler: window-bit digits of an (nb/2 + 64)-bit exponent."""
-    return -(-(nb // 2 + 64) // window)
+    """Exponent digits K of the fixed-base sampler: window-bit digits of a_h mod (p_h - 1) (nb/2 bits)."""
+    return -(-(nb // 2) // window)
 
 
 def work_fb(nb: int, digits: int) -> dict:
-    """Per-element canonical MACs of the fixed-base path (kernels_fb.hpp): per half K - 1 table
-    products + 1 coefficient product mod p_h^2, no squarings; the ChaCha digit kernel does no MACs."""
+    """Per-element MACs of the fixed-base path (kernels_fb.hpp), counted like SURVEY.md §8d (32-bit limbs,
+    M(s) = 2 s^2 + s per Montgomery product): k_fb = K table products mod p_h^2 per half (the first one
+    takes c0), no squarings; k_fb_fin (Garner) = one product mod p^2 + one plain (nb/32)^2 product; the
+    ChaCha digit kernel does no MACs. This is NOT the public-key W_enc of §8d (a different algorithm)."""
+    s = nb // 32
     return {"k_fb_digits": 0.0,
-            "k_fb": float(2 * digits * _M(nb // 32)),
-            "k_crt_fin": float(3 * _M(nb // 16))}
+            "k_fb": float(2 * digits * _M(s)),
+            "k_fb_fin": float(_M(s) + s * s)}
 
 
 def work_dec(nb: int) -> float:
@@ -374,7 +377,7 @@ def main():
     value = world * N * args.steps / elapsed
     if use_crt:
         if use_fb:
-            names = ["k_fb_digits", "k_fb", "k_crt_fin"]
+            names = ["k_fb_digits", "k_fb", "k_fb_fin"]
             works = work_fb(args.nb, fb_info[2])
         else:
             names = ["k_crt_a", "k_crt_b", "k_crt_fin"]

@@ -3,12 +3,19 @@
 
 namespace fpai {
 
-int fb_occupancy(int sb, int* occ) {
-  hipError_t e;
-  if (sb == 37) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, k_fb<37>, LANE_BLOCK, 0);
-  else if (sb == 74) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, k_fb<74>, LANE_BLOCK, 0);
-  else return -1;
-  if (e != hipSuccess || *occ < 1) *occ = 1;
+int fb_occupancy(int sb, int* occ_fb, int* occ_fin) {
+  hipError_t e1, e2;
+  if (sb == 37) {
+    e1 = hipOccupancyMaxActiveBlocksPerMultiprocessor(occ_fb, k_fb<37>, LANE_BLOCK, 0);
+    e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(occ_fin, k_fb_fin<37>, LANE_BLOCK, 0);
+  } else if (sb == 74) {
+    e1 = hipOccupancyMaxActiveBlocksPerMultiprocessor(occ_fb, k_fb<74>, LANE_BLOCK, 0);
+    e2 = hipOccupancyMaxActiveBlocksPerMultiprocessor(occ_fin, k_fb_fin<74>, LANE_BLOCK, 0);
+  } else {
+    return -1;
+  }
+  if (e1 != hipSuccess || *occ_fb < 1) *occ_fb = 1;
+  if (e2 != hipSuccess || *occ_fin < 1) *occ_fin = 1;
   return 0;
 }
 
@@ -20,7 +27,14 @@ hipError_t fb_launch(int sb, const FbParams& p, int gx, hipStream_t st) {
 }
 
 hipError_t fb_launch_digits(const FbDigitParams& p, int gx, hipStream_t st) {
-  hipLaunchKernelGGL(k_fb_digits<0>, dim3(gx, 2), dim3(LANE_BLOCK), 0, st, p);
+  hipLaunchKernelGGL(k_fb_digits<0>, dim3(gx, 2), dim3(FB_DIG_BLOCK), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t fb_launch_fin(int sb, const FbFinParams& p, int gx, hipStream_t st) {
+  if (sb == 37) hipLaunchKernelGGL(k_fb_fin<37>, dim3(gx), dim3(LANE_BLOCK), 0, st, p);
+  else if (sb == 74) hipLaunchKernelGGL(k_fb_fin<74>, dim3(gx), dim3(LANE_BLOCK), 0, st, p);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

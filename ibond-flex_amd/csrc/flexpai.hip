@@ -1,6 +1,8 @@
 // flexpai: host context + C ABI for the MI355X Paillier engine (see include/flexpai.h).
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -62,19 +64,29 @@ struct pai_ctx {
   CrtHalf* d_dec_pow = nullptr;   // [2] exponentiation halves: p_h^2, op list for p_h - 1
   uint32_t *d_dec_p = nullptr, *d_dec_q = nullptr, *d_dec_qinvR = nullptr, *d_dec_nl = nullptr, *d_dec_maxint = nullptr;
   uint32_t dec_pprime = 0;
-  // fixed-base obfuscation (kernels_fb.hpp): device-RNG encryption for key holders
-  bool fb_ok = false;
+  // fixed-base obfuscation (kernels_fb.hpp): device-RNG encryption for key holders. Built lazily on
+  // the first PAI_OBF_RNG encryption (or pai_ctx_fixed_base_prepare); any failure (key shape, table
+  // memory) leaves the generic CRT path in charge and never affects decryption.
+  enum { FB_UNTRIED = 0, FB_READY = 1, FB_UNAVAILABLE = 2 };
+  int fb_state = FB_UNTRIED;
+  std::string fb_reason;        // why the fixed-base path is unavailable
   bool fb_enabled = true;
   int fb_K = 0;
   int fb_W = 0;                 // digit window (bits); 0 = not chosen yet ($FLEXPAI_FB_WINDOW, default 16)
+  int fb_W_used = 0;            // window of the resident tables (may be below fb_W under a memory cap)
+  int fb_raw_bits = 0;
   FbHalf* d_fb_halves = nullptr;
+  FbRed* d_fb_red = nullptr;
+  uint32_t *d_fb_m8 = nullptr, *d_fb_coefR = nullptr, *d_fb_q2 = nullptr, *d_fb_m0 = nullptr;
+  uint32_t fb_mprime0 = 0;      // p^2 (Garner)
   uint32_t fb_g[2] = {0, 0};   // the bases g_p, g_q (generators of Z_p*, Z_q*)
   std::vector<void*> fb_mem;    // tables and their constants (rebuilt when the window changes)
-  HBig fb_primes[2], fb_sq[2];
-  std::vector<uint32_t> fb_coef[2];
-  int fb_sb = 0;
-  size_t fb_RB = 0;
+  HBig fb_p, fb_q;              // p < q
+  float fb_host_ms = 0.f, fb_dev_ms = 0.f;
+  uint64_t fb_table_bytes = 0;
   std::vector<void*> allocs;
+  std::vector<void*> priv_allocs;   // private-key constants: all freed together if set_private fails
+  bool in_priv = false;             // upload() targets priv_allocs
   // scratch (exponent tables), grown on demand
   void* d_scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -99,6 +111,7 @@ struct pai_ctx {
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
     for (void* p : allocs) (void)hipFree(p);
+    for (void* p : priv_allocs) (void)hipFree(p);
     for (void* p : fb_mem) (void)hipFree(p);
     if (d_scratch) (void)hipFree(d_scratch);
     if (d_work) (void)hipFree(d_work);
@@ -113,7 +126,7 @@ template <typename T>
 static int upload(pai_ctx* c, const std::vector<T>& v, T** out) {
   void* p = nullptr;
   HIPCHK(hipMalloc(&p, std::max<size_t>(v.size(), 1) * sizeof(T)));
-  c->allocs.push_back(p);
+  (c->in_priv ? c->priv_allocs : c->allocs).push_back(p);
   if (!v.empty()) HIPCHK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
   *out = (T*)p;
   return 0;
@@ -334,10 +347,12 @@ int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** ou
 }
 
 // Fixed-base obfuscation setup (kernels_fb.hpp): the smallest g >= 2 that generates Z_P* as far as
-// the prime factors of P - 1 below 2^16 can tell (g^((P-1)/l) != 1 for each); a large prime
-// factor l of P - 1 that g misses has probability < 2^-16 each. G = g^n mod P^2.
+// the prime factors of P - 1 below 2^24 can tell (g^((P-1)/l) != 1 for each); a prime factor l of
+// P - 1 above the bound that g misses has probability about 1/l < 2^-24. G = g^n mod P^2.
+constexpr uint32_t FB_TRIAL_BOUND = 1u << 24;   // = oracle/paillier_oracle.py FB_TRIAL_BOUND
+
 static uint32_t fb_base(const HBig& P) {
-  static const std::vector<uint32_t> primes = small_primes(1u << 16);
+  static const std::vector<uint32_t> primes = small_primes(FB_TRIAL_BOUND);
   const HBig pm1 = sub(P, HBig(1));
   std::vector<HBig> cof;
   for (uint32_t l : primes)
@@ -353,6 +368,25 @@ static uint32_t fb_base(const HBig& P) {
     if (ok) return g;
   }
   return 0;
+}
+
+// floor(a / m) by binary long division (host, one-time)
+static HBig div_big(const HBig& a, const HBig& m) {
+  HBig r, q;
+  q.w.assign(a.w.size() + 1, 0);
+  for (size_t i = a.bits(); i-- > 0;) {
+    r = shl1(r);
+    if (a.bit(i)) {
+      if (r.w.empty()) r.w.push_back(0);
+      r.w[0] |= 1;
+    }
+    if (cmp(r, m) >= 0) {
+      r = sub(r, m);
+      q.w[i / 32] |= 1u << (i % 32);
+    }
+  }
+  q.trim();
+  return q;
 }
 
 template <typename T>
@@ -371,22 +405,83 @@ static int fb_default_window() {
   return (w == 8 || w == 12 || w == 16 || w == 20) ? w : 16;
 }
 
-// (Re)builds the fixed-base tables for window c->fb_W from the key material saved by setup_fb.
-static int build_fb(pai_ctx* c) {
-  c->fb_ok = false;
+static int fb_row_words(int sb) { return sb == 37 ? FbGeom<37>::TW : sb == 74 ? FbGeom<74>::TW : 0; }
+
+static int fb_digit_count(const pai_ctx* c, int W) {
+  const size_t kb = std::max(sub(c->fb_p, HBig(1)).bits(), sub(c->fb_q, HBig(1)).bits());
+  return (int)((kb + W - 1) / W);
+}
+
+static uint64_t fb_bytes(const pai_ctx* c, int W) {
+  return 2ull * (uint64_t)fb_digit_count(c, W) * (1ull << W) * (uint64_t)fb_row_words(c->crt_sb) * 4ull;
+}
+
+// Budget for the two tables: $FLEXPAI_FB_MAX_BYTES, else the free device memory less a 4 GiB reserve.
+static uint64_t fb_budget(const pai_ctx* c) {
+  if (const char* e = getenv("FLEXPAI_FB_MAX_BYTES")) return (uint64_t)strtod(e, nullptr);
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 0;
+  const uint64_t reserve = 4ull << 30;
+  return fr > reserve ? fr - reserve : 0;
+}
+
+static void fb_release(pai_ctx* c) {
   for (void* p : c->fb_mem) (void)hipFree(p);
   c->fb_mem.clear();
-  const int sb = c->fb_sb, W = c->fb_W;
-  const size_t RB = c->fb_RB;
-  const size_t eb = std::max(c->fb_primes[0].bits(), c->fb_primes[1].bits()) + 64;
-  const int K = (int)((eb + W - 1) / W);
-  if ((size_t)K * W > 32 * (size_t)FB_MAX_WORDS) return 0;
-  const int TQ = (sb + 3) / 4;
+  c->d_fb_halves = nullptr;
+  c->d_fb_red = nullptr;
+}
+
+static int fb_unavailable(pai_ctx* c, const std::string& why) {
+  fb_release(c);
+  (void)hipGetLastError();   // clear a failed allocation / launch so later calls start clean
+  c->fb_state = pai_ctx::FB_UNAVAILABLE;
+  c->fb_reason = why;
+  static bool warned = false;
+  if (!warned && !getenv("FLEXPAI_QUIET")) {
+    fprintf(stderr, "flexpai: fixed-base obfuscation unavailable (%s); encrypting through the generic CRT path\n",
+            why.c_str());
+    warned = true;
+  }
+  return 0;
+}
+
+// Builds everything the fixed-base path needs for window c->fb_W (or the largest smaller window within
+// the memory budget). Returns 1 when the path is ready, 0 when it is unavailable (reason in fb_reason);
+// never fails the caller.
+static int ensure_fb(pai_ctx* c) {
+  if (c->fb_state == pai_ctx::FB_READY) return 1;
+  if (c->fb_state == pai_ctx::FB_UNAVAILABLE) return 0;
+  if (!c->crt_ok) return fb_unavailable(c, "needs the private key and the CRT kernels");
+  const int sb = c->crt_sb, TW = fb_row_words(sb);
+  if (!TW) return fb_unavailable(c, "key size not supported by the fixed-base kernels");
+  const HBig sq[2] = {mul(c->fb_p, c->fb_p), mul(c->fb_q, c->fb_q)};
+  if (sq[0].bits() > (size_t)32 * TW || sq[1].bits() > (size_t)32 * TW || c->ct_words != 2 * TW)
+    return fb_unavailable(c, "unbalanced primes: p^2 or q^2 exceeds the table row");
+  if (!c->fb_W) c->fb_W = fb_default_window();
+  const uint64_t budget = fb_budget(c);
+  int W = 0;
+  for (int w : {20, 16, 12, 8})
+    if (w <= c->fb_W && fb_bytes(c, w) <= budget) {
+      W = w;
+      break;
+    }
+  if (!W) return fb_unavailable(c, "tables do not fit the device memory budget");
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t kb[2] = {sub(c->fb_p, HBig(1)).bits(), sub(c->fb_q, HBig(1)).bits()};
+  const int raw_bits = (int)std::max(kb[0], kb[1]) + 64;
+  if ((raw_bits + 31) / 32 > FB_RAW_MAX - 2) return fb_unavailable(c, "exponent too wide");
+  const int K = fb_digit_count(c, W);
+  const size_t RB = (size_t)LB * sb;
+  const HBig primes[2] = {c->fb_p, c->fb_q};
   FbHalf hv[2];
+  FbRed red[2];
+  std::memset(red, 0, sizeof(red));
   int rc;
   void* t[2] = {nullptr, nullptr};
   for (int h = 0; h < 2; ++h) {
-    const HBig& m2 = c->fb_sq[h];
+    if (!c->fb_g[h] && !(c->fb_g[h] = fb_base(primes[h]))) return fb_unavailable(c, "no base found");
+    const HBig& m2 = sq[h];
     HMont M2(m2);
     // B_k = G^(2^(W k)), G = g^n mod p_h^2
     std::vector<uint32_t> bl((size_t)K * sb);
@@ -396,41 +491,62 @@ static int build_fb(pai_ctx* c) {
       std::copy(v.begin(), v.end(), bl.begin() + (size_t)k * sb);
       for (int q = 0; q < W; ++q) x = M2.mul(x, x);
     }
-    uint32_t *dm, *dc1, *dR2, *done, *dbases, *dlohi;
-    if ((rc = upload_fb(c, m2.limbs(sb, LB), &dm)) || (rc = upload_fb(c, c->fb_coef[h], &dc1)) ||
+    // c0 folding: n 2^(CB c) mod p_h^2 (c < NC) and 2^PB p_h^2
+    const int CB = sb == 37 ? FbGeom<37>::CB : FbGeom<74>::CB, NC = sb == 37 ? FbGeom<37>::NC : FbGeom<74>::NC;
+    const int PB = sb == 37 ? FbGeom<37>::PB : FbGeom<74>::PB;
+    std::vector<uint32_t> nm;
+    const HBig nmod = mod(c->n, m2);
+    for (int k = 0; k < NC; ++k) {
+      const std::vector<uint32_t> v = mul_pow2_mod(nmod, (size_t)CB * k, m2).limbs(sb, LB);
+      nm.insert(nm.end(), v.begin(), v.end());
+    }
+    uint32_t *dm, *dR2, *done, *dbases, *dlohi, *dnm, *dpbig;
+    if ((rc = upload_fb(c, m2.limbs(sb, LB), &dm)) ||
         (rc = upload_fb(c, mul_pow2_mod(HBig(1), 2 * RB, m2).limbs(sb, LB), &dR2)) ||
         (rc = upload_fb(c, mul_pow2_mod(HBig(1), RB, m2).limbs(sb, LB), &done)) || (rc = upload_fb(c, bl, &dbases)) ||
-        (rc = upload_fb(c, std::vector<uint32_t>((size_t)K * 2 * FB_LO * sb, 0u), &dlohi)))
-      return rc;
-    HIPCHK(hipMalloc(&t[h], ((size_t)K << W) * TQ * sizeof(uint4)));
+        (rc = upload_fb(c, std::vector<uint32_t>((size_t)K * 2 * FB_LO * sb, 0u), &dlohi)) ||
+        (rc = upload_fb(c, nm, &dnm)) || (rc = upload_fb(c, mul(m2, pow2(PB)).limbs(sb, LB), &dpbig)))
+      return fb_unavailable(c, pai_last_error());
+    if (hipMalloc(&t[h], ((size_t)K << W) * (TW / 4) * sizeof(uint4)) != hipSuccess)
+      return fb_unavailable(c, "table allocation failed");
     c->fb_mem.push_back(t[h]);
-    hv[h] = FbHalf{(const uint4*)t[h], dm, dc1, dR2, done, dbases, dlohi, mont_prime(m2, LB)};
+    hv[h] = FbHalf{(const uint4*)t[h], dm, dR2, done, dbases, dlohi, dnm, dpbig, mont_prime(m2, LB)};
+    if (h == 0) {
+      c->d_fb_m0 = dm;
+      c->fb_mprime0 = mont_prime(m2, LB);
+    }
+    // exponent reduction mod D_h = p_h - 1
+    const HBig D = sub(primes[h], HBig(1));
+    const HBig mu = div_big(pow2((size_t)raw_bits), D);
+    const std::vector<uint32_t> dw = D.words((D.bits() + 31) / 32), muw = mu.words(4);
+    std::copy(dw.begin(), dw.end(), red[h].D);
+    std::copy(muw.begin(), muw.end(), red[h].mu);
+    red[h].dwords = (int)dw.size();
+    red[h].kbits = (int)D.bits();
   }
+  // Garner constants (mod p^2): 8 p^2, (q^2)^-1 R, q^2
+  const HBig coef = inv_mod(sq[1], sq[0]);
+  if (coef.is_zero()) return fb_unavailable(c, "q^2 not invertible mod p^2");
   std::vector<FbHalf> v(hv, hv + 2);
-  if ((rc = upload_fb(c, v, &c->d_fb_halves))) return rc;
-  HIPCHK(fb_build_tables(sb, c->d_fb_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr));
-  HIPCHK(hipDeviceSynchronize());
+  std::vector<FbRed> vr(red, red + 2);
+  if ((rc = upload_fb(c, v, &c->d_fb_halves)) || (rc = upload_fb(c, vr, &c->d_fb_red)) ||
+      (rc = upload_fb(c, mul(sq[0], HBig(8)).limbs(sb, LB), &c->d_fb_m8)) ||
+      (rc = upload_fb(c, mul_pow2_mod(coef, RB, sq[0]).limbs(sb, LB), &c->d_fb_coefR)) ||
+      (rc = upload_fb(c, sq[1].limbs(sb, LB), &c->d_fb_q2)))
+    return fb_unavailable(c, pai_last_error());
+  const auto t1 = std::chrono::steady_clock::now();
+  if (fb_build_tables(sb, c->d_fb_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess)
+    return fb_unavailable(c, "table construction failed");
+  const auto t2 = std::chrono::steady_clock::now();
+  c->fb_host_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
+  c->fb_dev_ms = std::chrono::duration<float, std::milli>(t2 - t1).count();
+  c->fb_table_bytes = fb_bytes(c, W);
   c->fb_K = K;
-  c->fb_ok = true;
-  return 0;
-}
-
-static int setup_fb(pai_ctx* c, const HBig primes[2], const HBig sq[2], int sb, size_t RB,
-                    const std::vector<uint32_t>* coef_limbs) {
-  c->fb_ok = false;
-  if (sb != 37 && sb != 74) return 0;
-  for (int h = 0; h < 2; ++h) {
-    const uint32_t g = fb_base(primes[h]);
-    if (!g) return 0;
-    c->fb_g[h] = g;
-    c->fb_primes[h] = primes[h];
-    c->fb_sq[h] = sq[h];
-    c->fb_coef[h] = coef_limbs[h];
-  }
-  c->fb_sb = sb;
-  c->fb_RB = RB;
-  if (!c->fb_W) c->fb_W = fb_default_window();
-  return build_fb(c);
+  c->fb_W_used = W;
+  c->fb_raw_bits = raw_bits;
+  c->fb_state = pai_ctx::FB_READY;
+  return 1;
 }
 
 // CRT encryption constants (kernels_crt.hpp). p < q here (sorted like keypair.py:57-62).
@@ -450,7 +566,6 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
   const HBig primes[2] = {p, q};
   const HBig sq[2] = {mul(p, p), mul(q, q)};
   CrtHalf ha[2], hb[2];
-  std::vector<uint32_t> coef_limbs[2];
   int rc;
   for (int h = 0; h < 2; ++h) {
     const HBig& ph = primes[h];
@@ -475,7 +590,6 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
     const HBig& m2 = sq[h];
     HBig coef = inv_mod(sq[1 - h], m2);
     if (coef.is_zero()) return 0;
-    coef_limbs[h] = coef.limbs(sb, LB);
     uint32_t *dm2, *dr2, *dcoef, *dpb;
     if ((rc = upload(c, m2.limbs(sb, LB), &dm2)) ||
         (rc = upload(c, mul_pow2_mod(HBig(1), 2 * RB, m2).limbs(sb, LB), &dr2)) ||
@@ -492,7 +606,8 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
   c->crt_sa = sa;
   c->crt_sb = sb;
   c->crt_ok = true;
-  if ((rc = setup_fb(c, primes, sq, sb, RB, coef_limbs))) return rc;
+  c->fb_p = p;   // the fixed-base tables are built lazily (ensure_fb)
+  c->fb_q = q;
   // lane-engine decryption: x_h = c^(p_h - 1) mod p_h^2, L_h, m_h = L_h h_h mod p_h; CRT + decode
   {
     const int kd = (int)((32 * (size_t)c->ct_words + RB - 1) / RB);
@@ -539,6 +654,11 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
   return 0;
 }
 
+static int set_private_impl(pai_ctx* c, HBig p, HBig q);
+
+// Transactional: on any failure every private-key allocation of this call is released and the
+// context is left exactly as before (public-key operations keep working, a retry starts clean).
+// The fixed-base tables are not built here (ensure_fb, on the first device-RNG encryption).
 int pai_ctx_set_private(pai_ctx* c, const uint8_t* p_le, const uint8_t* q_le, size_t half_bytes) {
   if (!c || !p_le || !q_le) return fail(PAI_ERR_ARG, "pai_ctx_set_private: null argument");
   HIPCHK(hipSetDevice(c->device));
@@ -546,6 +666,23 @@ int pai_ctx_set_private(pai_ctx* c, const uint8_t* p_le, const uint8_t* q_le, si
   if (cmp(mul(p, q), c->n) != 0) return fail(PAI_ERR_KEY, "given public key does not match the given p and q");
   if (cmp(p, q) == 0) return fail(PAI_ERR_KEY, "p and q have to be different");
   if (cmp(q, p) < 0) std::swap(p, q);   // keypair.py:57-62
+  if (c->has_priv) return 0;            // same key (p q == n): already set
+  c->in_priv = true;
+  const int rc = set_private_impl(c, p, q);
+  c->in_priv = false;
+  if (rc) {
+    const std::string msg = g_last_error;
+    for (void* a : c->priv_allocs) (void)hipFree(a);
+    c->priv_allocs.clear();
+    (void)hipGetLastError();
+    c->has_priv = c->crt_ok = c->dec_lane_ok = false;
+    c->fb_state = pai_ctx::FB_UNTRIED;
+    g_last_error = msg;
+  }
+  return rc;
+}
+
+static int set_private_impl(pai_ctx* c, HBig p, HBig q) {
   const int S = c->S_d;
   const size_t Rbits = (size_t)LB * S;
   HBig hp, hq;
@@ -611,9 +748,10 @@ int pai_ctx_set_option(pai_ctx* c, int option, int value) {
         return fail(PAI_ERR_ARG, "fixed-base window must be 8, 12, 16 or 20");
       if (value == c->fb_W) return 0;
       c->fb_W = value;
-      if (!c->fb_sb) return 0;   // applied when the private key is set
       HIPCHK(hipSetDevice(c->device));
-      return build_fb(c);
+      fb_release(c);                       // rebuilt lazily for the new window
+      c->fb_state = pai_ctx::FB_UNTRIED;
+      return 0;
   }
   return fail(PAI_ERR_ARG, "pai_ctx_set_option: unknown option");
 }
@@ -625,8 +763,12 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
     case PAI_OPT_CRT_AVAILABLE: *value = c->crt_ok ? 1 : 0; return 0;
     case PAI_OPT_STAGE_TIMING: *value = c->timing ? 1 : 0; return 0;
     case PAI_OPT_LANE_DECRYPT: *value = (c->dec_lane_ok && c->dec_lane_enabled) ? 1 : 0; return 0;
-    case PAI_OPT_FIXED_BASE: *value = (c->fb_ok && c->fb_enabled) ? 1 : 0; return 0;
-    case PAI_OPT_FB_WINDOW: *value = c->fb_W ? c->fb_W : fb_default_window(); return 0;
+    // 1 when device-RNG encryption will use the fixed bases (tables resident, or not yet tried)
+    case PAI_OPT_FIXED_BASE:
+      *value = (c->crt_ok && c->fb_enabled && c->fb_state != pai_ctx::FB_UNAVAILABLE) ? 1 : 0;
+      return 0;
+    case PAI_OPT_FB_WINDOW: *value = c->fb_W_used ? c->fb_W_used : c->fb_W ? c->fb_W : fb_default_window(); return 0;
+    case PAI_OPT_FB_READY: *value = c->fb_state == pai_ctx::FB_READY ? 1 : 0; return 0;
   }
   return fail(PAI_ERR_ARG, "pai_ctx_get_option: unknown option");
 }
@@ -643,13 +785,32 @@ int pai_ctx_stage_times(pai_ctx* c, float* ms_out, int max_out, int* count) {
   return 0;
 }
 
-int pai_ctx_fixed_base_info(const pai_ctx* c, uint32_t* g_p, uint32_t* g_q, int* digits, int* window) {
+int pai_ctx_fixed_base_info(pai_ctx* c, uint32_t* g_p, uint32_t* g_q, int* digits, int* window) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
-  if (!c->fb_ok) return fail(PAI_ERR_NOPRIV, "fixed-base obfuscation not available (needs the private key)");
+  if (!c->crt_ok) return fail(PAI_ERR_NOPRIV, "fixed-base obfuscation not available (needs the private key)");
+  HIPCHK(hipSetDevice(c->device));
+  if (!ensure_fb((pai_ctx*)c)) return fail(PAI_ERR_KEY, "fixed-base obfuscation not available: " + c->fb_reason);
   if (g_p) *g_p = c->fb_g[0];
   if (g_q) *g_q = c->fb_g[1];
   if (digits) *digits = c->fb_K;
-  if (window) *window = c->fb_W;
+  if (window) *window = c->fb_W_used;
+  return 0;
+}
+
+int pai_ctx_fixed_base_prepare(pai_ctx* c) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (!c->crt_ok) return fail(PAI_ERR_NOPRIV, "fixed-base obfuscation not available (needs the private key)");
+  HIPCHK(hipSetDevice(c->device));
+  if (!ensure_fb(c)) return fail(PAI_ERR_KEY, "fixed-base obfuscation not available: " + c->fb_reason);
+  return 0;
+}
+
+int pai_ctx_fixed_base_setup(const pai_ctx* c, float* host_ms, float* device_ms, uint64_t* table_bytes) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (c->fb_state != pai_ctx::FB_READY) return fail(PAI_ERR_KEY, "fixed-base tables are not resident");
+  if (host_ms) *host_ms = c->fb_host_ms;
+  if (device_ms) *device_ms = c->fb_dev_ms;
+  if (table_bytes) *table_bytes = c->fb_table_bytes;
   return 0;
 }
 
@@ -693,9 +854,73 @@ static int launch_crt_fin(pai_ctx* c, CrtFinParams& f, hipStream_t st) {
   return 0;
 }
 
+// Fixed-base encryption (kernels_fb.hpp), chunks of CRT_CHUNK elements: exponent digits, the per-half
+// table products with c0 folded in, Garner recombination into the ciphertext words.
+static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
+  const int SB = c->crt_sb;
+  const long long N = e.n;
+  const long long chunk = std::min(N, CRT_CHUNK);
+  int occF = 1, occG = 1;
+  if (fb_occupancy(SB, &occF, &occG)) return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
+  const long long lane_blocks = (chunk + LANE_BLOCK - 1) / LANE_BLOCK;
+  const int gxF = (int)std::max<long long>(1, std::min<long long>(lane_blocks, (long long)occF * c->cus / 2));
+  const int gxG = (int)std::max<long long>(1, std::min<long long>(lane_blocks, (long long)occG * c->cus));
+  const size_t dbytes = (size_t)2 * c->fb_K * 4, wbytes = (size_t)2 * SB * 4;   // per element
+  int rc;
+  if ((rc = ensure_work(c, (dbytes + wbytes) * chunk))) return rc;
+  uint32_t* digits = (uint32_t*)c->d_work;
+  uint32_t* w = (uint32_t*)((char*)c->d_work + dbytes * chunk);
+  const size_t esz = e.dtype == PAI_F32 ? 4 : 8;
+  for (long long off = 0; off < N; off += chunk) {
+    const long long n = std::min(chunk, N - off);
+    FbDigitParams pd{};
+    pd.n = n;
+    std::memcpy(pd.rng_key, e.rng_key, sizeof(pd.rng_key));
+    pd.index_base = e.index_base + (unsigned long long)off;
+    pd.K = c->fb_K;
+    pd.W = c->fb_W_used;
+    pd.raw_bits = c->fb_raw_bits;
+    pd.red = c->d_fb_red;
+    pd.digits = digits;
+    const int gD = (int)std::min<long long>((long long)8 * c->cus, (n + FB_DIG_BLOCK - 1) / FB_DIG_BLOCK);
+    stage_mark(c, 0, st);
+    HIPCHK(fb_launch_digits(pd, gD, st));
+    stage_mark(c, 1, st);
+    FbParams pf{};
+    pf.halves = c->d_fb_halves;
+    pf.n = n;
+    pf.K = c->fb_K;
+    pf.W = c->fb_W_used;
+    pf.digits = digits;
+    pf.out = w;
+    pf.x = (const char*)e.x + (size_t)off * esz;
+    pf.dtype = e.dtype;
+    pf.exp_mode = e.exp_mode;
+    pf.fexp = e.fexp;
+    pf.exp = e.exp + off;
+    pf.status = e.status ? e.status + off : nullptr;
+    HIPCHK(fb_launch(SB, pf, (int)std::min<long long>(gxF, (n + LANE_BLOCK - 1) / LANE_BLOCK), st));
+    stage_mark(c, 2, st);
+    FbFinParams pg{};
+    pg.w = w;
+    pg.n = n;
+    pg.m = c->d_fb_m0;
+    pg.mprime = c->fb_mprime0;
+    pg.m8 = c->d_fb_m8;
+    pg.coefR = c->d_fb_coefR;
+    pg.q2 = c->d_fb_q2;
+    pg.ct = e.ct + (size_t)off * c->ct_words;
+    pg.ct_words = c->ct_words;
+    HIPCHK(fb_launch_fin(SB, pg, (int)std::min<long long>(gxG, (n + LANE_BLOCK - 1) / LANE_BLOCK), st));
+    stage_mark(c, 3, st);
+  }
+  return 0;
+}
+
 template <int SA, int SB>
 static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
   static_assert(SB == 2 * SA || SB == 2 * SA - 1, "stage sizes");
+  if (e.obf == PAI_OBF_RNG && c->fb_enabled && ensure_fb(c)) return launch_fb(c, e, st);
   const long long N = e.n;
   const int r_words = e.obf == PAI_OBF_GIVEN ? e.r_words : e.rng_words;
   const int kchunks = (32 * r_words + LB * SA - 1) / (LB * SA);
@@ -711,68 +936,40 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
   const size_t scrB = (size_t)2 * gxB * LANE_BLOCK * lane_scratch_words<SB>() * 4;
   int rc = ensure_scratch(c, std::max(scrA, scrB));
   if (rc) return rc;
-  // fixed-base obfuscation (kernels_fb.hpp) replaces stages A and B for the device RNG
-  const bool fb = e.obf == PAI_OBF_RNG && c->fb_ok && c->fb_enabled;
-  int occF = 1;
-  if (fb && fb_occupancy(SB, &occF)) return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
-  const int gxF = (int)std::max<long long>(1, std::min<long long>(lanes_blocks, (long long)occF * c->cus / 2));
-  const size_t ybytes = std::max((size_t)2 * SA * 4, fb ? (size_t)2 * c->fb_K * 4 : 0);   // per element
+  const size_t ybytes = (size_t)2 * SA * 4;   // per element
   if ((rc = ensure_work(c, (ybytes + (size_t)2 * SB * 4) * chunk))) return rc;
   uint32_t* y = (uint32_t*)c->d_work;
   uint32_t* u = (uint32_t*)((char*)c->d_work + ybytes * chunk);
   const size_t esz = e.dtype == PAI_F32 ? 4 : 8;
   for (long long off = 0; off < N; off += chunk) {
     const long long n = std::min(chunk, N - off);
-    if (fb) {
-      FbDigitParams pd{};
-      pd.n = n;
-      std::memcpy(pd.rng_key, e.rng_key, sizeof(pd.rng_key));
-      pd.index_base = e.index_base + (unsigned long long)off;
-      pd.K = c->fb_K;
-      pd.W = c->fb_W;
-      pd.digits = y;
-      const int gD = (int)std::min<long long>((long long)4 * c->cus, (n + LANE_BLOCK - 1) / LANE_BLOCK);
-      stage_mark(c, 0, st);
-      HIPCHK(fb_launch_digits(pd, gD, st));
-      stage_mark(c, 1, st);
-      FbParams pf{};
-      pf.halves = c->d_fb_halves;
-      pf.n = n;
-      pf.K = c->fb_K;
-      pf.W = c->fb_W;
-      pf.digits = y;
-      pf.out = u;
-      HIPCHK(fb_launch(SB, pf, (int)std::min<long long>(gxF, (n + LANE_BLOCK - 1) / LANE_BLOCK), st));
-      stage_mark(c, 2, st);
-    } else {
-      CrtParams pa{};
-      pa.halves = c->d_crt_a;
-      pa.n = n;
-      pa.obf = e.obf;
-      pa.r = e.r ? e.r + (size_t)off * e.r_stride : nullptr;
-      pa.r_stride = e.r_stride;
-      pa.r_words = r_words;
-      std::memcpy(pa.rng_key, e.rng_key, sizeof(pa.rng_key));
-      pa.index_base = e.index_base + (unsigned long long)off;
-      pa.kchunks = kchunks;
-      pa.out = y;
-      pa.scratch = (uint32_t*)c->d_scratch;
-      const int gA = (int)std::min<long long>(gxA, (n + LANE_BLOCK - 1) / LANE_BLOCK);
-      stage_mark(c, 0, st);
-      HIPCHK(crt_launch_a(SA, pa, gA, st));
-      stage_mark(c, 1, st);
-      HIPCHK(hipGetLastError());
-      CrtParams pb{};
-      pb.halves = c->d_crt_b;
-      pb.n = n;
-      pb.yin = y;
-      pb.out = u;
-      pb.scratch = (uint32_t*)c->d_scratch;
-      const int gB = (int)std::min<long long>(gxB, (n + LANE_BLOCK - 1) / LANE_BLOCK);
-      HIPCHK(crt_launch_b(SA, pb, gB, st));
-      HIPCHK(hipGetLastError());
-      stage_mark(c, 2, st);
-    }
+    CrtParams pa{};
+    pa.halves = c->d_crt_a;
+    pa.n = n;
+    pa.obf = e.obf;
+    pa.r = e.r ? e.r + (size_t)off * e.r_stride : nullptr;
+    pa.r_stride = e.r_stride;
+    pa.r_words = r_words;
+    std::memcpy(pa.rng_key, e.rng_key, sizeof(pa.rng_key));
+    pa.index_base = e.index_base + (unsigned long long)off;
+    pa.kchunks = kchunks;
+    pa.out = y;
+    pa.scratch = (uint32_t*)c->d_scratch;
+    const int gA = (int)std::min<long long>(gxA, (n + LANE_BLOCK - 1) / LANE_BLOCK);
+    stage_mark(c, 0, st);
+    HIPCHK(crt_launch_a(SA, pa, gA, st));
+    stage_mark(c, 1, st);
+    HIPCHK(hipGetLastError());
+    CrtParams pb{};
+    pb.halves = c->d_crt_b;
+    pb.n = n;
+    pb.yin = y;
+    pb.out = u;
+    pb.scratch = (uint32_t*)c->d_scratch;
+    const int gB = (int)std::min<long long>(gxB, (n + LANE_BLOCK - 1) / LANE_BLOCK);
+    HIPCHK(crt_launch_b(SA, pb, gB, st));
+    HIPCHK(hipGetLastError());
+    stage_mark(c, 2, st);
     CrtFinParams f{};
     f.x = (const char*)e.x + (size_t)off * esz;
     f.dtype = e.dtype;

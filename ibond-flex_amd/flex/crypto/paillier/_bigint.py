@@ -1,9 +1,15 @@
 """Host-side big-integer helpers for one-time key setup (keygen) and for the scalar object
-operators. Restates flex/crypto/gmpy_math.py:27-93 on Python ints (no gmpy2 dependency).
+operators. Restates flex/crypto/gmpy_math.py:27-93 on the package's own GMP binding (_gmp.so,
+csrc/hostgmp.c, the library gmpy2 wraps), or on Python ints where that binding is not built.
 Array paths never use these: they go to the GPU through _runtime.py."""
 from __future__ import annotations
 
 import random
+
+try:
+    from . import _gmp
+except ImportError:          # not built: same results through Python ints (slower)
+    _gmp = None
 
 POWMOD_GMP_SIZE = 1 << 64
 
@@ -20,16 +26,22 @@ def crt(mp: int, mq: int, p: int, q: int, q_inverse: int, n: int) -> int:   # gm
 
 
 def mulmod(a: int, b: int, c: int) -> int:           # gmpy_math.py:43-48
+    if _gmp is not None and c >= POWMOD_GMP_SIZE:
+        return _gmp.mulmod(a, b, c)
     return a * b % c
 
 
 def powmod(a: int, b: int, c: int) -> int:           # gmpy_math.py:51-63
     if a == 1:
         return 1
+    if _gmp is not None and max(a, b, c) >= POWMOD_GMP_SIZE:
+        return _gmp.powmod(a, b, c)
     return pow(a, b, c)
 
 
 def invert(a: int, b: int) -> int:                   # gmpy_math.py:66-74
+    if _gmp is not None:
+        return _gmp.invert(a, b)
     try:
         x = pow(a, -1, b)
     except ValueError:

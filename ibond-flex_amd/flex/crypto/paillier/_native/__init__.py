@@ -21,10 +21,11 @@ PAI_EXP_AUTO, PAI_EXP_FIXED = 0, 1
 EL_OK, EL_INT, EL_INT_BIG, EL_OVERFLOW, EL_FLOAT_OVF, EL_ENC_RANGE = 0, 1, 2, 3, 4, 5
 
 PAI_OPT_CRT_ENCRYPT, PAI_OPT_CRT_AVAILABLE, PAI_OPT_STAGE_TIMING, PAI_OPT_LANE_DECRYPT = 1, 2, 3, 4
-PAI_OPT_FIXED_BASE, PAI_OPT_FB_WINDOW = 5, 6
+PAI_OPT_FIXED_BASE, PAI_OPT_FB_WINDOW, PAI_OPT_FB_READY = 5, 6, 7
 
 EXPORTED = ("pai_ctx_create", "pai_ctx_set_private", "pai_ctx_destroy", "pai_ctx_info", "pai_last_error",
             "pai_ctx_set_option", "pai_ctx_get_option", "pai_ctx_stage_times", "pai_ctx_fixed_base_info",
+            "pai_ctx_fixed_base_prepare", "pai_ctx_fixed_base_setup",
             "pai_encrypt", "pai_add", "pai_decrypt", "pai_encrypt_dev", "pai_add_dev", "pai_decrypt_dev",
             "pai_mul", "pai_mul_dev", "pai_matmul", "pai_matmul_dev", "pai_add_plain", "pai_add_plain_dev",
             "pai_segment_add", "pai_segment_add_dev")
@@ -58,6 +59,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.pai_ctx_get_option.argtypes = [P, I, P]
         lib.pai_ctx_stage_times.argtypes = [P, P, I, P]
         lib.pai_ctx_fixed_base_info.argtypes = [P, P, P, P, P]
+        lib.pai_ctx_fixed_base_prepare.argtypes = [P]
+        lib.pai_ctx_fixed_base_setup.argtypes = [P, P, P, P]
         lib.pai_encrypt.argtypes = [P, I, P, S, I, ctypes.c_int32, I, P, S, S, P, U64, P, P, P]
         lib.pai_add.argtypes = [P, P, P, I, S, P, P]
         lib.pai_decrypt.argtypes = [P, P, P, S, P, P, P, P]
@@ -181,11 +184,27 @@ class Context:
 
     @property
     def fb_window(self) -> int:
+        """Window of the resident fixed-base tables (else the requested one)."""
         return self._get_option(PAI_OPT_FB_WINDOW)
 
     def set_fb_window(self, bits: int):
-        """Digit window of the fixed-base tables (8, 12, 16 or 20); rebuilds them."""
+        """Digit window of the fixed-base tables (8, 12, 16 or 20); the tables are rebuilt lazily."""
         _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_FB_WINDOW, int(bits)))
+
+    @property
+    def fb_ready(self) -> bool:
+        """True when the fixed-base tables are resident on the device."""
+        return bool(self._get_option(PAI_OPT_FB_READY))
+
+    def prepare_fixed_base(self):
+        """Build the fixed-base tables now (NativeError with the reason when unavailable)."""
+        _check(self.lib.pai_ctx_fixed_base_prepare(self._h))
+
+    def fixed_base_setup(self):
+        """(host_ms, device_ms, table_bytes) of the last table build."""
+        hm, dm, tb = ctypes.c_float(), ctypes.c_float(), ctypes.c_uint64()
+        _check(self.lib.pai_ctx_fixed_base_setup(self._h, ctypes.byref(hm), ctypes.byref(dm), ctypes.byref(tb)))
+        return float(hm.value), float(dm.value), int(tb.value)
 
     def close(self):
         if getattr(self, "_h", None):

@@ -88,7 +88,11 @@ typedef struct pai_ctx pai_ctx;
                                     r^n for uniform r, see pai_ctx_fixed_base_info); 0: r from the
                                     ChaCha20 stream and r^n by exponentiation. Read back: 1 when used */
 #define PAI_OPT_FB_WINDOW 6      /* digit window of the fixed-base tables: 8, 12, 16 or 20 bits (default 16, or
-                                    $FLEXPAI_FB_WINDOW); setting it rebuilds the tables (K 2^W rows per half) */
+                                    $FLEXPAI_FB_WINDOW); setting it drops the tables (rebuilt lazily). Read
+                                    back: the window of the resident tables, which is the largest one <= the
+                                    requested window whose 2 K 2^W rows fit $FLEXPAI_FB_MAX_BYTES (default:
+                                    free device memory less 4 GiB)                                        */
+#define PAI_OPT_FB_READY 7       /* read-only: 1 when the fixed-base tables are resident                    */
 
 int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** out);
 int pai_ctx_set_private(pai_ctx* ctx, const uint8_t* p_le, const uint8_t* q_le, size_t half_bytes);
@@ -104,10 +108,20 @@ int pai_ctx_stage_times(pai_ctx* ctx, float* ms_out, int max_out, int* count);
 int pai_ctx_info(const pai_ctx* ctx, int* key_bits, int* ct_words, int* pt_words);
 const char* pai_last_error(void);
 /* Fixed-base obfuscation parameters (PAI_OPT_FIXED_BASE): the bases g_p, g_q (generators of Z_p*,
- * Z_q*, p < q) with G_h = g_h^n mod h^2, the digit count K and the window W: element i's exponent a_h
- * is the little-endian integer of the first K*W bits of the ChaCha20 stream (rng_key, counter 0..,
- * nonce = (index lo, index hi, 0x66786230 + h)); r^n mod h^2 is G_h^a_h.                         */
-int pai_ctx_fixed_base_info(const pai_ctx* ctx, uint32_t* g_p, uint32_t* g_q, int* digits, int* window);
+ * Z_q*, p < q) with G_h = g_h^n mod h^2, the digit count K and the window W. Element i's exponent is
+ * a_h = raw_h mod (h - 1), raw_h = the little-endian integer of the first max(bits(p-1), bits(q-1)) + 64
+ * bits of the ChaCha20 stream (rng_key, counter 0.., nonce = (index lo, index hi, 0x66786230 + h));
+ * r^n mod h^2 is G_h^a_h, i.e. the ciphertext is the reference's encryption under the obfuscator
+ * r = CRT(g_p^a_p mod p, g_q^a_q mod q). Builds the tables if they are not resident (like
+ * pai_ctx_fixed_base_prepare); PAI_ERR_KEY with the reason when the path is unavailable.          */
+int pai_ctx_fixed_base_info(pai_ctx* ctx, uint32_t* g_p, uint32_t* g_q, int* digits, int* window);
+/* Build the fixed-base tables now (otherwise on the first PAI_OBF_RNG encryption with the private key).
+ * 0 when they are resident; PAI_ERR_KEY / PAI_ERR_NOPRIV with the reason otherwise (encryption then
+ * uses the generic CRT path; decryption is never affected).                                       */
+int pai_ctx_fixed_base_prepare(pai_ctx* ctx);
+/* Cost of the last table build: host ms (bases, B_k, constants, hipMalloc), device ms (table kernels),
+ * resident table bytes.                                                                            */
+int pai_ctx_fixed_base_setup(const pai_ctx* ctx, float* host_ms, float* device_ms, uint64_t* table_bytes);
 
 /* Encrypt N plaintexts. dtype PAI_F32/F64/I64. obf_mode PAI_OBF_*.
  *   r_le:      PAI_OBF_GIVEN only: r values as little-endian byte strings of r_bytes each, element i

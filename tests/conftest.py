@@ -20,3 +20,10 @@ def golden():
     import json
     with open(os.path.join(ROOT, "tests", "golden", "paillier_golden.json")) as f:
         return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def golden_fb():
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "paillier_golden_fb.json")) as f:
+        return json.load(f)

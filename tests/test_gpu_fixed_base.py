@@ -1,8 +1,14 @@
 """GPU parity of the fixed-base obfuscation sampler (kernels_fb.hpp), the default device-RNG
-encryption for key holders: bit-exact against its CPU restatement (oracle/paillier_oracle.py
-fb_rn: r^n mod h^2 = (g_h^n)^a_h, a_h from the ChaCha20 stream), decryptable, independent of the
-launch geometry (index base, ragged sizes), and with the reference's randomizer statistics on the
-publicly visible part (Jacobi symbol of c mod n, uniform +-1 like r^n for uniform r)."""
+encryption for key holders:
+
+* bit-exact against THE REFERENCE's own ciphertexts (tests/golden/paillier_golden_fb.json: the
+  reference's pe.encrypt(x, random_value=r) for r = CRT(g_p^a_p mod p, g_q^a_q mod q), made by
+  tests/golden/make_golden_fb.py) at the windows W = 16 and W = 20;
+* bit-exact against its CPU restatement (oracle/paillier_oracle.py fb_rn) at other sizes, index
+  bases and windows; decryptable; with the reference's randomizer statistics on the publicly
+  visible part (Jacobi symbol of c mod n, uniform +-1 like r^n for uniform r);
+* never in the way of decryption: with the table memory capped below one table the context still
+  encrypts (generic CRT, bit-identical to the explicit-r reference path) and decrypts exactly."""
 import numpy as np
 import pytest
 
@@ -52,8 +58,11 @@ def test_fixed_base_params_match_oracle(ctxs, nb):
     assert ctx.fixed_base
     gp, gq, K, W = ctx.fixed_base_info()
     assert (gp, gq) == (O.fb_base(key.p), O.fb_base(key.q))
-    assert W == ctx.fb_window and W in (8, 12, 16)
-    assert K == O.fb_digits(key.p.bit_length(), key.q.bit_length(), W)
+    assert W == ctx.fb_window and W in (8, 12, 16, 20)
+    assert K == O.fb_digits(key.p, key.q, W)
+    assert ctx.fb_ready
+    host_ms, dev_ms, nbytes = ctx.fixed_base_setup()
+    assert nbytes == 2 * K * (1 << W) * (2 * nb // 64) * 4 and host_ms > 0 and dev_ms > 0
 
 
 def test_fixed_base_needs_private_key(golden):
@@ -119,8 +128,8 @@ def test_fixed_base_jacobi_statistics(ctxs):
 
 @pytest.mark.parametrize("nb", [1024, 2048])
 def test_fixed_base_windows(ctxs, nb):
-    """Windows 8, 12, 16, 20 rebuild the tables; each is bit-exact against the oracle, and 8 and 16
-    (same 1088-bit exponent for 2048-bit keys, 576-bit for 1024-bit) give identical ciphertexts."""
+    """Windows 8, 12, 16, 20 rebuild the tables; each is bit-exact against the oracle, and all give
+    identical ciphertexts (the exponent a_h is reduced mod p_h - 1 before it is cut into digits)."""
     N = _native()
     ctx, key = ctxs[nb]
     w0 = ctx.fb_window
@@ -137,8 +146,60 @@ def test_fixed_base_windows(ctxs, nb):
             for i in (0, 150, 299):
                 assert (got[i], int(ex[i])) == O.fb_encrypt_value(x[i], key, rk, 99 + i, params), (w, i)
             outs[w] = ct
-        assert np.array_equal(outs[8], outs[16])
+        for w in (12, 16, 20):
+            assert np.array_equal(outs[8], outs[w])
     finally:
         ctx.set_fb_window(w0)
     with pytest.raises(RuntimeError):
         ctx.set_fb_window(10)
+
+
+@pytest.mark.parametrize("nb", [1024, 2048])
+@pytest.mark.parametrize("window", [16, 20])
+def test_fixed_base_matches_reference_goldens(ctxs, golden_fb, nb, window):
+    """k_fb + k_fb_fin against the reference's own encryption under the sampler's obfuscator r."""
+    N = _native()
+    ctx, key = ctxs[nb]
+    g = golden_fb["keys"][str(nb)]
+    assert (hex(key.n), hex(key.p), hex(key.q)) == (g["n"], g["p"], g["q"])
+    w0 = ctx.fb_window
+    recs = golden_fb["encrypt"][str(nb)]
+    x = np.array([r["bits"] for r in recs], dtype=np.uint32).view(np.float32)
+    try:
+        ctx.set_fb_window(window)
+        gp, gq, K, W = ctx.fixed_base_info()
+        assert (gp, gq, W) == (g["g_p"], g["g_q"], window)
+        ct, ex, st = ctx.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=bytes.fromhex(golden_fb["rng_key"]),
+                                 index_base=golden_fb["index_base"])
+    finally:
+        ctx.set_fb_window(w0)
+    got = N.words_to_ints(ct)
+    for i, r in enumerate(recs):
+        assert (hex(got[i]), int(ex[i])) == (r["c"], r["e"]), f"element {i}"
+    val, _, _, _ = ctx.decrypt(ct, ex)
+    assert [float(v).hex() for v in val] == [r["dec"] for r in recs]
+
+
+def test_fixed_base_memory_cap_falls_back(golden, monkeypatch):
+    """A table budget below one table: the fixed-base path reports itself unavailable, device-RNG
+    encryption runs on the generic CRT kernels (r = the ChaCha20 stream, bit-identical to the
+    explicit-r path) and decryption is unaffected."""
+    N = _native()
+    key = _key(golden, 2048)
+    monkeypatch.setenv("FLEXPAI_FB_MAX_BYTES", "1000000")
+    monkeypatch.setenv("FLEXPAI_QUIET", "1")
+    ctx = N.Context(key.n, 0, key.p, key.q)
+    assert ctx.fixed_base and not ctx.fb_ready            # not tried yet: set_private built no tables
+    x = np.random.default_rng(5).standard_normal(64).astype(np.float32)
+    rk = b"\x07" * 32
+    ct, ex, _ = ctx.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=11)
+    assert not ctx.fixed_base and not ctx.fb_ready
+    with pytest.raises(RuntimeError):
+        ctx.prepare_fixed_base()
+    got = N.words_to_ints(ct)
+    rbytes = ((2048 + 64 + 31) // 32) * 4
+    for i in (0, 31, 63):
+        r = O.device_r(rk, 11 + i, rbytes) % key.n
+        assert got[i] == O.encrypt_value(x[i], key, r)[0]
+    val, _, _, _ = ctx.decrypt(ct, ex)
+    assert np.array_equal(val, x.astype(np.float64))

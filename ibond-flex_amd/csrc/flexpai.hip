@@ -296,6 +296,17 @@ static int blocks_per_cu(K kernel, int threads, size_t lds) {
 // C-linkage comes from the declarations in flexpai.h.
 const char* pai_last_error(void) { return g_last_error.c_str(); }
 
+int pai_device_count(int* count) {
+  if (!count) return fail(PAI_ERR_ARG, "null argument");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    n = 0;
+  }
+  *count = n;
+  return 0;
+}
+
 int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** out) {
   if (!n_le || !out || n_bytes == 0) return fail(PAI_ERR_ARG, "pai_ctx_create: null argument");
   HBig n = HBig::from_le_bytes(n_le, n_bytes);

@@ -7,14 +7,18 @@
  * pow (~9x slower at 2048 bits). Whole-array operations never come here: they go to the
  * GPU through libflexpai.so.
  *
- * Conversions copy CPython's 30-bit long digits straight into / out of mpz limbs (mpz_import /
- * mpz_export with 2 nail bits), as gmpy2 does. Built by __graft_entry__.build() against GMP 6.2.1
+ * Conversions repack CPython's 30-bit long digits straight into / out of 64-bit mpz limbs, as gmpy2
+ * does (mpz_import with nails is a slow generic loop). Built by __graft_entry__.build() against GMP 6.2.1
  * (/opt/conda, the library gmpy2 2.0.8 wraps).
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 #include <longintrepr.h>
 #include <gmp.h>
+
+/* Work registers, allocated once and reused (every call holds the GIL, so they are never shared
+ * concurrently); results go to a register distinct from the inputs, so GMP needs no temporaries. */
+static mpz_t A, B, C, T;
 
 static int to_mpz(PyObject* o, mpz_t z) {
   if (!PyLong_Check(o)) {
@@ -27,22 +31,53 @@ static int to_mpz(PyObject* o, mpz_t z) {
     mpz_set_ui(z, 0);
     return 0;
   }
-  mpz_import(z, (size_t)n, -1, sizeof(digit), 0, sizeof(digit) * 8 - PyLong_SHIFT, l->ob_digit);
-  if (size < 0) mpz_neg(z, z);
+  /* pack the 30-bit digits into 64-bit limbs directly (mpz_import with nails is a slow generic loop) */
+  const size_t nl = ((size_t)n * PyLong_SHIFT + GMP_NUMB_BITS - 1) / GMP_NUMB_BITS;
+  mp_limb_t* w = mpz_limbs_write(z, (mp_size_t)nl);
+  mp_limb_t acc = 0;
+  int have = 0;
+  size_t k = 0;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    const mp_limb_t d = l->ob_digit[i];
+    acc |= d << have;
+    have += PyLong_SHIFT;
+    if (have >= GMP_NUMB_BITS) {
+      w[k++] = acc;
+      have -= GMP_NUMB_BITS;
+      acc = have ? d >> (PyLong_SHIFT - have) : 0;
+    }
+  }
+  if (have) w[k++] = acc;
+  while (k > 0 && w[k - 1] == 0) --k;
+  mpz_limbs_finish(z, size < 0 ? -(mp_size_t)k : (mp_size_t)k);
   return 0;
 }
 
 static PyObject* from_mpz(const mpz_t z) {
   const int sgn = mpz_sgn(z);
   if (sgn == 0) return PyLong_FromLong(0);
+  const size_t nl = mpz_size(z);
+  const mp_limb_t* w = mpz_limbs_read(z);
   const size_t bits = mpz_sizeinbase(z, 2);
   const size_t n = (bits + PyLong_SHIFT - 1) / PyLong_SHIFT;
   PyLongObject* l = _PyLong_New((Py_ssize_t)n);
   if (!l) return NULL;
-  size_t count = 0;
-  mpz_export(l->ob_digit, &count, -1, sizeof(digit), 0, sizeof(digit) * 8 - PyLong_SHIFT, z);
-  for (size_t i = count; i < n; ++i) l->ob_digit[i] = 0;
-  Py_SET_SIZE(l, sgn < 0 ? -(Py_ssize_t)count : (Py_ssize_t)count);
+  const digit mask = ((digit)1 << PyLong_SHIFT) - 1;
+  size_t k = 0;
+  int have = 0;          /* unread bits left in w[k] past position `pos` */
+  int pos = 0;
+  for (size_t i = 0; i < n; ++i) {
+    mp_limb_t v = k < nl ? w[k] >> pos : 0;
+    have = GMP_NUMB_BITS - pos;
+    if (have < PyLong_SHIFT && k + 1 < nl) v |= w[k + 1] << have;
+    l->ob_digit[i] = (digit)(v & mask);
+    pos += PyLong_SHIFT;
+    if (pos >= GMP_NUMB_BITS) {
+      pos -= GMP_NUMB_BITS;
+      ++k;
+    }
+  }
+  Py_SET_SIZE(l, sgn < 0 ? -(Py_ssize_t)n : (Py_ssize_t)n);
   return (PyObject*)l;
 }
 
@@ -53,20 +88,14 @@ static PyObject* g_mulmod(PyObject* self, PyObject* const* args, Py_ssize_t narg
     PyErr_SetString(PyExc_TypeError, "mulmod(a, b, c)");
     return NULL;
   }
-  mpz_t a, b, c;
-  mpz_inits(a, b, c, NULL);
-  PyObject* r = NULL;
-  if (to_mpz(args[0], a) || to_mpz(args[1], b) || to_mpz(args[2], c)) goto done;
-  if (mpz_sgn(c) == 0) {
+  if (to_mpz(args[0], A) || to_mpz(args[1], B) || to_mpz(args[2], C)) return NULL;
+  if (mpz_sgn(C) == 0) {
     PyErr_SetString(PyExc_ZeroDivisionError, "mulmod by zero");
-    goto done;
+    return NULL;
   }
-  mpz_mul(a, a, b);
-  mpz_fdiv_r(a, a, c);
-  r = from_mpz(a);
-done:
-  mpz_clears(a, b, c, NULL);
-  return r;
+  mpz_mul(T, A, B);
+  mpz_fdiv_r(A, T, C);
+  return from_mpz(A);
 }
 
 /* powmod(a, b, c) (gmpy_math.py:51-63): 1 for a == 1; b < 0 means powers of the inverse */
@@ -76,30 +105,22 @@ static PyObject* g_powmod(PyObject* self, PyObject* const* args, Py_ssize_t narg
     PyErr_SetString(PyExc_TypeError, "powmod(a, b, c)");
     return NULL;
   }
-  mpz_t a, b, c;
-  mpz_inits(a, b, c, NULL);
-  PyObject* r = NULL;
-  if (to_mpz(args[0], a) || to_mpz(args[1], b) || to_mpz(args[2], c)) goto done;
-  if (mpz_cmp_ui(a, 1) == 0) {
-    r = PyLong_FromLong(1);
-    goto done;
-  }
-  if (mpz_sgn(c) == 0) {
+  if (to_mpz(args[0], A) || to_mpz(args[1], B) || to_mpz(args[2], C)) return NULL;
+  if (mpz_cmp_ui(A, 1) == 0) return PyLong_FromLong(1);
+  if (mpz_sgn(C) == 0) {
     PyErr_SetString(PyExc_ZeroDivisionError, "powmod by zero");
-    goto done;
+    return NULL;
   }
-  if (mpz_sgn(b) < 0) {
-    if (!mpz_invert(a, a, c)) {
+  if (mpz_sgn(B) < 0) {
+    if (!mpz_invert(T, A, C)) {
       PyErr_SetString(PyExc_ZeroDivisionError, "powmod: base not invertible");
-      goto done;
+      return NULL;
     }
-    mpz_neg(b, b);
+    mpz_swap(T, A);
+    mpz_neg(B, B);
   }
-  mpz_powm(a, a, b, c);
-  r = from_mpz(a);
-done:
-  mpz_clears(a, b, c, NULL);
-  return r;
+  mpz_powm(T, A, B, C);
+  return from_mpz(T);
 }
 
 /* invert(a, b) (gmpy_math.py:66-74): ZeroDivisionError when no inverse exists */
@@ -109,18 +130,12 @@ static PyObject* g_invert(PyObject* self, PyObject* const* args, Py_ssize_t narg
     PyErr_SetString(PyExc_TypeError, "invert(a, b)");
     return NULL;
   }
-  mpz_t a, b;
-  mpz_inits(a, b, NULL);
-  PyObject* r = NULL;
-  if (to_mpz(args[0], a) || to_mpz(args[1], b)) goto done;
-  if (mpz_sgn(b) == 0 || !mpz_invert(a, a, b) || mpz_sgn(a) == 0) {
+  if (to_mpz(args[0], A) || to_mpz(args[1], B)) return NULL;
+  if (mpz_sgn(B) == 0 || !mpz_invert(T, A, B) || mpz_sgn(T) == 0) {
     PyErr_SetString(PyExc_ZeroDivisionError, "invert(a, b) no inverse exists");
-    goto done;
+    return NULL;
   }
-  r = from_mpz(a);
-done:
-  mpz_clears(a, b, NULL);
-  return r;
+  return from_mpz(T);
 }
 
 /* mul(a, b) (gmpy_math.py:27-28) */
@@ -130,15 +145,9 @@ static PyObject* g_mul(PyObject* self, PyObject* const* args, Py_ssize_t nargs) 
     PyErr_SetString(PyExc_TypeError, "mul(a, b)");
     return NULL;
   }
-  mpz_t a, b;
-  mpz_inits(a, b, NULL);
-  PyObject* r = NULL;
-  if (to_mpz(args[0], a) || to_mpz(args[1], b)) goto done;
-  mpz_mul(a, a, b);
-  r = from_mpz(a);
-done:
-  mpz_clears(a, b, NULL);
-  return r;
+  if (to_mpz(args[0], A) || to_mpz(args[1], B)) return NULL;
+  mpz_mul(T, A, B);
+  return from_mpz(T);
 }
 
 static PyMethodDef methods[] = {
@@ -152,6 +161,10 @@ static struct PyModuleDef moddef = {PyModuleDef_HEAD_INIT, "_gmp", "GMP binding 
                                     NULL, NULL, NULL, NULL};
 
 PyMODINIT_FUNC PyInit__gmp(void) {
+  mpz_init2(A, 8192);
+  mpz_init2(B, 8192);
+  mpz_init2(C, 8192);
+  mpz_init2(T, 16384);
   PyObject* m = PyModule_Create(&moddef);
   if (m) PyModule_AddStringConstant(m, "gmp_version", gmp_version);
   return m;

@@ -34,6 +34,9 @@ struct EncParams {
   int ct_words;
 };
 
+constexpr int ADD_KMAX = 64;     // operands per k_add launch (the R^s constants go up to s = ADD_KMAX + 1)
+constexpr int ADD_TMAX = 1024;   // step-count buckets of the k_add schedule sort
+
 struct AddParams {
   const uint32_t* cts;    // k x n x ct_words
   const int32_t* exps;    // k x n
@@ -42,14 +45,13 @@ struct AddParams {
   int32_t* out_exp;
   long long n;
   const uint32_t* N;
-  const uint32_t* R2;
-  const uint32_t* oneR;   // R mod n^2
+  const uint32_t* RS;     // [ADD_KMAX + 2][S]: R^s mod n^2, s = 0 .. ADD_KMAX + 1 (group layout)
   uint32_t mprime;
   int ct_words;
-  uint32_t* scratch;
   // nullable: operand j of instance i is element gidx[i k + j] of the flat cts/exps arrays (-1: padding);
   // segmented sums (pai_segment_add) gather their members this way
   const long long* gidx;
+  const int* perm;        // nullable: instance slot t processes instance perm[t] (schedule sort)
 };
 
 // Per-half (p: h=0, q: h=1) constants for CRT decryption; all LB-bit limb arrays of S limbs.
@@ -285,9 +287,92 @@ __global__ __launch_bounds__(BLOCK, 2) void k_encrypt(EncParams p) {
 }
 
 // ================================================================= k-way homomorphic add
-// prod_j c_j^(16^(E - e_j)) mod n^2 (encrypted_number.py:115-137, 166-185).
-// The running product lives in tile 0; groups that need fewer alignment squarings than their
-// wave-mates multiply by R mod n^2 (the Montgomery one) instead, which leaves them unchanged.
+// prod_j c_j^(16^(E - e_j)) mod n^2 (encrypted_number.py:115-137, 166-185), evaluated
+// by Horner over the exponent levels instead of operand by operand:
+//   acc = prod_{e_j = l0} c_j ;  for each next level l: acc = acc^(16^(l - l_prev)) * prod_{e_j = l} c_j
+// so the 4 (E - e_j) alignment squarings of every operand become 4 (E - e_min) squarings of the running
+// product (the value is the same integer mod n^2; the reference's sum is order independent). Operands
+// enter in plain form; the Montgomery factor is tracked (rho: acc = value R^rho, rho = 1 - m after m plain
+// operands of a level) and restored with ONE product by R^s mod n^2 per level change (s = 1 + m) and at
+// the end (s = m), instead of one to-Montgomery product per operand.
+//
+// Every step is one Montgomery product acc * B with a per-group B (acc itself, an operand, or R^s), so
+// the groups of a wave run in lock step; a group that is done multiplies by R (leaves acc unchanged).
+// k_add_plan / k_add_scan / k_add_scatter sort the elements by their step count, so the 16 groups of a
+// wave do (almost) the same number of steps.
+__device__ __forceinline__ long long add_src(const AddParams& p, long long e, int j) {
+  return p.gidx ? p.gidx[e * p.k + j] : (long long)j * p.n + e;
+}
+__device__ __forceinline__ int add_exp(const AddParams& p, long long src) { return src < 0 ? PAD_EXP : p.exps[src]; }
+
+// Products the Horner schedule of instance e needs (0 for an all-padding instance).
+__device__ __forceinline__ int add_steps(const AddParams& p, long long e, int& E) {
+  int emin = INT32_MAX, keff = 0;
+  E = PAD_EXP;
+  for (int j = 0; j < p.k; ++j) {
+    const int ej = add_exp(p, add_src(p, e, j));
+    if (ej == PAD_EXP) continue;
+    ++keff;
+    E = max(E, ej);
+    emin = min(emin, ej);
+  }
+  if (!keff) return 0;
+  int levels = 0, cur = emin, last = 0;
+  for (;;) {
+    int cnt = 0, nl = INT32_MAX;
+    for (int j = 0; j < p.k; ++j) {
+      const int ej = add_exp(p, add_src(p, e, j));
+      if (ej == PAD_EXP) continue;
+      cnt += ej == cur;
+      if (ej > cur && ej < nl) nl = ej;
+    }
+    ++levels;
+    last = cnt;
+    if (nl == INT32_MAX) break;
+    cur = nl;
+  }
+  const long long t = (long long)(keff - 1) + 4ll * ((long long)E - emin) + (levels - 1) + (last >= 2 ? 1 : 0);
+  return (int)min(t, (long long)INT32_MAX);
+}
+
+template <int DUMMY = 0>
+__global__ __launch_bounds__(256) void k_add_plan(AddParams p, uint16_t* bucket, unsigned* hist) {
+  __shared__ unsigned h[ADD_TMAX];
+  for (int t = threadIdx.x; t < ADD_TMAX; t += blockDim.x) h[t] = 0u;
+  __syncthreads();
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < p.n; e += (long long)gridDim.x * blockDim.x) {
+    int E;
+    const int b = min(add_steps(p, e, E), ADD_TMAX - 1);
+    bucket[e] = (uint16_t)b;
+    atomicAdd(&h[b], 1u);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < ADD_TMAX; t += blockDim.x)
+    if (h[t]) atomicAdd(&hist[t], h[t]);
+}
+
+// exclusive prefix sum of the ADD_TMAX bucket counts (one block of ADD_TMAX threads)
+template <int DUMMY = 0>
+__global__ __launch_bounds__(ADD_TMAX) void k_add_scan(unsigned* hist) {
+  __shared__ unsigned v[ADD_TMAX];
+  const int t = threadIdx.x;
+  v[t] = hist[t];
+  __syncthreads();
+  for (int o = 1; o < ADD_TMAX; o <<= 1) {
+    const unsigned x = t >= o ? v[t - o] : 0u;
+    __syncthreads();
+    v[t] += x;
+    __syncthreads();
+  }
+  hist[t] = v[t] - hist[t];
+}
+
+template <int DUMMY = 0>
+__global__ __launch_bounds__(256) void k_add_scatter(long long n, const uint16_t* bucket, unsigned* offs, int* perm) {
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x)
+    perm[atomicAdd(&offs[bucket[e]], 1u)] = (int)e;
+}
+
 template <int TPI>
 __global__ __launch_bounds__(BLOCK, 2) void k_add(AddParams p) {
   constexpr int S = TPI * L;
@@ -299,51 +384,86 @@ __global__ __launch_bounds__(BLOCK, 2) void k_add(AddParams p) {
   uint32_t* slot = smem + gib * S;
   uint32_t m[L];
   load_limbs_g<TPI>(p.N, m, tig);
-  uint32_t* tw = lane_tiles(p.scratch);
 
   for (long long base = (long long)blockIdx.x * GPB; base < p.n; base += (long long)gridDim.x * GPB) {
     const long long inst = base + gib;
     const bool valid = inst < p.n;
     const long long ii = valid ? inst : p.n - 1;
-    // padding operands (exponent PAD_EXP, used by the chunked reductions of pai_matmul) count as 1
-    int E = PAD_EXP;
+    const long long el = p.perm ? (long long)p.perm[ii] : ii;
+    // levels: E = max, cur = min exponent over the non-padding operands (padding counts as 1)
+    int E = PAD_EXP, cur = INT32_MAX;
     for (int j = 0; j < p.k; ++j) {
-      const long long src = p.gidx ? p.gidx[ii * p.k + j] : (long long)j * p.n + ii;
-      const int ej = src < 0 ? PAD_EXP : p.exps[src];
-      if (ej != PAD_EXP) E = max(E, ej);
+      const int ej = add_exp(p, add_src(p, el, j));
+      if (ej == PAD_EXP) continue;
+      E = max(E, ej);
+      cur = min(cur, ej);
     }
+    const bool empty = E == PAD_EXP;
     uint32_t a[L];
-    for (int j = 0; j < p.k; ++j) {
-      const long long src = p.gidx ? p.gidx[ii * p.k + j] : (long long)j * p.n + ii;
-      const int ej = src < 0 ? PAD_EXP : p.exps[src];
-      const bool pad = ej == PAD_EXP;
-      words_to_limbs(p.cts + (src < 0 ? 0 : src) * p.ct_words, pad ? 0 : p.ct_words, a, tig);
-      if (pad && tig == 0) a[0] = 1u;
-      copy_g_to_lds<TPI>(slot, p.R2, tig);
-      montmul<TPI>(a, a, slot, TPI, m, p.mprime, lane, tig);           // Montgomery form
-      const int nsq = pad ? 0 : 4 * (E - ej);
-      for (int t = 0;; ++t) {                                            // wave-uniform trip count
-        const bool need = t < nsq;
-        if (ballot(need) == 0ull) break;
-        if (need) {
-          write_limbs_lds<TPI>(slot, a, tig);
-        } else {
-          copy_g_to_lds<TPI>(slot, p.oneR, tig);
-        }
-        montmul<TPI>(a, a, slot, TPI, m, p.mprime, lane, tig);
-      }
-      if (j > 0) {
-        write_limbs_lds<TPI>(slot, a, tig);
-        tile_load(tw, 0, a, lane);
-        montmul<TPI>(a, a, slot, TPI, m, p.mprime, lane, tig);
-      }
-      tile_store(tw, 0, a, lane);
+    int jc = 0, sq = 0, mcount = 0;
+    bool done = empty;
+    if (!empty) {
+      while (add_exp(p, add_src(p, el, jc)) != cur) ++jc;
+      words_to_limbs(p.cts + add_src(p, el, jc) * p.ct_words, p.ct_words, a, tig);   // rho = 0
+      ++jc;
+      mcount = 1;
+    } else {
+#pragma unroll
+      for (int i = 0; i < L; ++i) a[i] = (tig == 0 && i == 0) ? 1u : 0u;
     }
-    write_one_lds<TPI>(slot, tig);
-    montmul<TPI>(a, a, slot, TPI, m, p.mprime, lane, tig);               // leave the Montgomery domain
+    for (;;) {
+      // this group's next step: 0 square, 1 times operand `osrc`, 2 times R^s, 3 nothing (times R)
+      int op = 3, s = 1;
+      long long osrc = 0;
+      if (!done) {
+        if (sq > 0) {
+          op = 0;
+          --sq;
+        } else {
+          while (jc < p.k && add_exp(p, add_src(p, el, jc)) != cur) ++jc;
+          if (jc < p.k) {
+            op = 1;
+            osrc = add_src(p, el, jc);
+            ++jc;
+            ++mcount;                                // rho = 1 - mcount
+          } else {
+            int nl = INT32_MAX;
+            for (int j = 0; j < p.k; ++j) {
+              const int ej = add_exp(p, add_src(p, el, j));
+              if (ej != PAD_EXP && ej > cur && ej < nl) nl = ej;
+            }
+            if (nl != INT32_MAX) {
+              op = 2;
+              s = 1 + mcount;                        // back to rho = 1 for the squarings
+              sq = 4 * (nl - cur);
+              cur = nl;
+              jc = 0;
+              mcount = 0;
+            } else {
+              done = true;
+              if (mcount >= 2) {                     // rho = 1 - mcount -> 0
+                op = 2;
+                s = mcount;
+              }
+            }
+          }
+        }
+      }
+      if (ballot(op != 3) == 0ull) break;
+      if (op == 0) {
+        write_limbs_lds<TPI>(slot, a, tig);
+      } else if (op == 1) {
+        uint32_t t[L];
+        words_to_limbs(p.cts + osrc * p.ct_words, p.ct_words, t, tig);
+        write_limbs_lds<TPI>(slot, t, tig);
+      } else {
+        copy_g_to_lds<TPI>(slot, p.RS + (size_t)s * S, tig);
+      }
+      montmul<TPI>(a, a, slot, TPI, m, p.mprime, lane, tig);
+    }
     cond_sub<TPI>(a, m, lane, tig);
-    emit_words<TPI>(slot, a, p.out + ii * p.ct_words, p.ct_words, valid, tig);
-    if (valid && tig == 0) p.out_exp[ii] = E;
+    emit_words<TPI>(slot, a, p.out + el * p.ct_words, p.ct_words, valid, tig);
+    if (valid && tig == 0) p.out_exp[el] = E;
   }
 }
 

@@ -5,6 +5,7 @@ and is REQUIRED: there is no CPU fallback. Loading fails loudly if it is missing
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import os
 import threading
@@ -23,7 +24,7 @@ EL_OK, EL_INT, EL_INT_BIG, EL_OVERFLOW, EL_FLOAT_OVF, EL_ENC_RANGE = 0, 1, 2, 3,
 PAI_OPT_CRT_ENCRYPT, PAI_OPT_CRT_AVAILABLE, PAI_OPT_STAGE_TIMING, PAI_OPT_LANE_DECRYPT = 1, 2, 3, 4
 PAI_OPT_FIXED_BASE, PAI_OPT_FB_WINDOW, PAI_OPT_FB_READY = 5, 6, 7
 
-EXPORTED = ("pai_ctx_create", "pai_ctx_set_private", "pai_ctx_destroy", "pai_ctx_info", "pai_last_error",
+EXPORTED = ("pai_device_count", "pai_ctx_create", "pai_ctx_set_private", "pai_ctx_destroy", "pai_ctx_info", "pai_last_error",
             "pai_ctx_set_option", "pai_ctx_get_option", "pai_ctx_stage_times", "pai_ctx_fixed_base_info",
             "pai_ctx_fixed_base_prepare", "pai_ctx_fixed_base_setup",
             "pai_encrypt", "pai_add", "pai_decrypt", "pai_encrypt_dev", "pai_add_dev", "pai_decrypt_dev",
@@ -49,6 +50,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                               f"(hipcc --offload-arch=gfx950). There is no CPU fallback.")
         lib = ctypes.CDLL(path)
         P, S, I, U64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+        lib.pai_device_count.argtypes = [P]
         lib.pai_ctx_create.argtypes = [P, S, I, ctypes.POINTER(ctypes.c_void_p)]
         lib.pai_ctx_set_private.argtypes = [P, P, P, S]
         lib.pai_ctx_destroy.argtypes = [P]
@@ -80,6 +82,13 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                 getattr(lib, name).restype = ctypes.c_int
         _lib = lib
         return lib
+
+
+def device_count() -> int:
+    """GPUs visible to the engine (0 without one). Raises when libflexpai.so is missing."""
+    n = ctypes.c_int()
+    _check(load_library().pai_device_count(ctypes.byref(n)))
+    return n.value
 
 
 def _check(rc: int):
@@ -115,6 +124,7 @@ class Context:
         _check(self.lib.pai_ctx_info(h, ctypes.byref(kb), ctypes.byref(cw), ctypes.byref(pw)))
         self.key_bits, self.ct_words, self.pt_words = kb.value, cw.value, pw.value
         self.has_private = False
+        self.calls = collections.Counter()     # C-ABI entry points this context has run (tests, stats)
         if p is not None:
             self.set_private(p, q)
 
@@ -217,6 +227,12 @@ class Context:
         except Exception:
             pass
 
+    def _check_words(self, ct: np.ndarray, exp: np.ndarray, N: int):
+        """Host buffers must be exactly [N, ct_words] words and N exponents: the C ABI reads N * ct_words."""
+        if ct.dtype != np.uint32 or ct.shape != (N, self.ct_words) or exp.shape != (N,):
+            raise ValueError(f"ciphertext buffer shape {ct.shape} / exponents {exp.shape} do not match "
+                             f"({N}, {self.ct_words})")
+
     # ----------------------------------------------------------------- host-buffer ops
     def encrypt(self, x: np.ndarray, exp_mode: int = PAI_EXP_AUTO, fixed_exp: int = 0,
                 obf_mode: int = PAI_OBF_RNG, r: Optional[Sequence[int]] = None, r_scalar: Optional[int] = None,
@@ -244,6 +260,7 @@ class Context:
                 r_buf = np.frombuffer(b"".join(int_to_le(v, r_bytes) for v in r), dtype=np.uint8).copy()
                 r_stride = r_bytes
         key = rng_key if rng_key is not None else os.urandom(32)
+        self.calls["pai_encrypt"] += 1
         _check(self.lib.pai_encrypt(self._h, dt, _ptr(x), N, exp_mode, fixed_exp, obf_mode,
                                     _ptr(r_buf) if r_buf is not None else None, r_stride, r_bytes,
                                     key, index_base, _ptr(ct), _ptr(ex), _ptr(st)))
@@ -254,6 +271,9 @@ class Context:
         cts = [np.ascontiguousarray(c, dtype=np.uint32) for c in cts]
         exps = [np.ascontiguousarray(e, dtype=np.int32) for e in exps]
         N = exps[0].size
+        for c, e in zip(cts, exps):
+            self._check_words(c, e, N)
+        self.calls["pai_add"] += 1
         ct_ptrs = (ctypes.c_void_p * k)(*[_ptr(c) for c in cts])
         ex_ptrs = (ctypes.c_void_p * k)(*[_ptr(e) for e in exps])
         out = np.empty((N, self.ct_words), dtype=np.uint32)
@@ -268,8 +288,10 @@ class Context:
         exp = np.ascontiguousarray(exp, dtype=np.int32)
         x = np.ascontiguousarray(x)
         N = exp.size
+        self._check_words(ct, exp, N)
         if x.size not in (1, N):
             raise ValueError("scalar operand must have 1 or N elements")
+        self.calls["pai_mul"] += 1
         out = np.empty((N, self.ct_words), dtype=np.uint32)
         oe = np.empty(N, dtype=np.int32)
         st = np.empty(N, dtype=np.int32)
@@ -284,8 +306,10 @@ class Context:
         exp = np.ascontiguousarray(exp, dtype=np.int32)
         x = np.ascontiguousarray(x)
         N = exp.size
+        self._check_words(ct, exp, N)
         if x.size not in (1, N):
             raise ValueError("plain operand must have 1 or N elements")
+        self.calls["pai_add_plain"] += 1
         out = np.empty((N, self.ct_words), dtype=np.uint32)
         oe = np.empty(N, dtype=np.int32)
         st = np.empty(N, dtype=np.int32)
@@ -301,6 +325,8 @@ class Context:
         index = np.ascontiguousarray(index, dtype=np.int64)
         seg_off = np.ascontiguousarray(seg_off, dtype=np.int64)
         nseg = seg_off.size - 1
+        self._check_words(ct, exp, exp.size)
+        self.calls["pai_segment_add"] += 1
         out = np.empty((max(nseg, 0), self.ct_words), dtype=np.uint32)
         oe = np.empty(max(nseg, 0), dtype=np.int32)
         if nseg <= 0:
@@ -316,6 +342,8 @@ class Context:
         x = np.ascontiguousarray(x)
         if exp.size != m * K or x.size != K * d:
             raise ValueError("matmul: shape mismatch")
+        self._check_words(ct, exp, m * K)
+        self.calls["pai_matmul"] += 1
         out = np.empty((m * d, self.ct_words), dtype=np.uint32)
         oe = np.empty(m * d, dtype=np.int32)
         _check(self.lib.pai_matmul(self._h, _ptr(ct), _ptr(exp), m, K, scalar_dtype(x), _ptr(x), d, _ptr(out), _ptr(oe)))
@@ -325,6 +353,8 @@ class Context:
         ct = np.ascontiguousarray(ct, dtype=np.uint32)
         exp = np.ascontiguousarray(exp, dtype=np.int32)
         N = exp.size
+        self._check_words(ct, exp, N)
+        self.calls["pai_decrypt"] += 1
         val = np.empty(N, dtype=np.float64)
         mant = np.empty(N, dtype=np.int64)
         st = np.empty(N, dtype=np.int32)

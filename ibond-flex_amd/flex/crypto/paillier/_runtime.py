@@ -9,20 +9,44 @@ Private keys known to this process (a PaillierDecryptor was built, or the factor
 generate_paillier_encryptor_decryptor made the pair) are registered here so that the context
 of that key can encrypt through the CRT kernels (same ciphertext bits, ~4x fewer multiplies);
 the registry is process-local and never pickled. $FLEXPAI_CRT=0 disables CRT encryption.
+
+Contexts live in a bounded LRU ($FLEXPAI_MAX_CONTEXTS, default 4): a process that cycles through
+keys (a new keypair per round, or several simulated parties) drops the least recently used context,
+whose device memory (constants, fixed-base tables) is released when the last reference goes.
 """
 from __future__ import annotations
 
+import collections
 import os
 import threading
-from typing import Dict, Tuple
+from typing import Dict, Optional, Tuple
 
 import numpy as np
 
 from . import _native
 
 _lock = threading.Lock()
-_ctxs: Dict[Tuple[int, int, int], "_native.Context"] = {}
+_ctxs: "collections.OrderedDict[Tuple[int, int, int], _native.Context]" = collections.OrderedDict()
 _private: Dict[int, object] = {}
+_gpus: Optional[Tuple[int, int]] = None     # (pid, device count)
+
+
+def max_contexts() -> int:
+    try:
+        return max(1, int(os.environ.get("FLEXPAI_MAX_CONTEXTS", "4")))
+    except ValueError:
+        return 4
+
+
+def gpu_available() -> bool:
+    """True when this process sees a GPU (raises when libflexpai.so is missing: no silent fallback).
+    Without one, operators on existing ciphertext arrays use the reference's per-element computation
+    (cipher_array.py); encryption and decryption raise."""
+    global _gpus
+    pid = os.getpid()
+    if _gpus is None or _gpus[0] != pid:
+        _gpus = (pid, _native.device_count())
+    return _gpus[1] > 0
 
 
 def register_private(public_key, private_key) -> None:
@@ -51,9 +75,19 @@ def context(public_key, private_key=None) -> "_native.Context":
         if ctx is None:
             ctx = _native.Context(public_key.n, dev)
             _ctxs[k] = ctx
+            while len(_ctxs) > max_contexts():
+                _ctxs.popitem(last=False)        # freed once no caller holds it any more
+        else:
+            _ctxs.move_to_end(k)
         if private_key is not None and not ctx.has_private:
             ctx.set_private(private_key.p, private_key.q)
     return ctx
+
+
+def cached_contexts():
+    """The contexts currently cached (most recently used last)."""
+    with _lock:
+        return list(_ctxs.values())
 
 
 def ints_to_words(vals, nwords: int) -> np.ndarray:

@@ -17,11 +17,22 @@ indexes, reshapes or pickles the result keep working unchanged. Two additions:
   GPU launch (negative scalars: one batch inversion for the whole array), and ``a.dot(x)`` /
   ``a @ x`` with a plain matrix (he_otp_lr_ft1/train.py:160) as one launch plus a reduction tree.
 
-Pickling produces a plain object ndarray (``__reduce__``), so unmodified FLEX peers can load it.
+Pickling (ionic_bond ships pickles, ion.py:150-178) writes the bulk wire format below and unpickles
+into a PaillierArray again, with its packed words cached: an array received from a flexpai peer goes
+straight back to the GPU for the receiver's ``+``, ``sum``, ``.dot`` and ``*`` (HE_SA_FT coordinator
+he_sa_ft/train.py:66-69, HE_OTP_LR he_otp_lr_ft1/train.py:158-160, HE_LINEAR he_linear_ft/train.py:64-65).
+With ``FLEXPAI_PICKLE_PLAIN=1`` it pickles as a plain object ndarray instead, for deployments that mix in
+unmodified FLEX peers (they cannot import this module). Plain object ndarrays received from such peers
+run the reference's per-element operators on the package's GMP binding (_bigint.py).
+
+On a host without a GPU (e.g. a CPU-only protocol coordinator) the operators on existing ciphertext
+arrays fall back to numpy's per-element loop over PaillierEncryptedNumber, i.e. exactly the reference's
+computation on GMP; encryption and decryption still require the GPU and raise without one.
 """
 from __future__ import annotations
 
 import operator
+import os
 from typing import Optional, Tuple
 
 import numpy as np
@@ -48,7 +59,13 @@ class PaillierArray(np.ndarray):
         self._packed = None
 
     def __reduce__(self):
-        return np.asarray(self).view(np.ndarray).__reduce__()
+        plain = np.asarray(self).view(np.ndarray).__reduce__
+        if os.environ.get("FLEXPAI_PICKLE_PLAIN", "0").strip() not in ("", "0"):
+            return plain()
+        try:
+            return (_from_pickle, (to_wire(self),))
+        except (TypeError, ValueError):      # empty, mixed keys or non-ciphertext elements
+            return plain()
 
     def __setitem__(self, key, value):
         self._packed = None
@@ -161,12 +178,16 @@ def pack(arr: np.ndarray, public_key) -> Tuple[np.ndarray, np.ndarray, list]:
     return words, exps.astype(np.int32), ints
 
 
-def materialize(public_key, words: np.ndarray, exps: np.ndarray, shape, obfuscated: bool) -> PaillierArray:
-    """Device output -> PaillierArray of PaillierEncryptedNumber (+ packed cache)."""
+def materialize(public_key, words: np.ndarray, exps: np.ndarray, shape, obfuscated) -> PaillierArray:
+    """Device output -> PaillierArray of PaillierEncryptedNumber (+ packed cache). `obfuscated` is one
+    flag for all elements or a per-element flag array."""
     from . import _runtime
     ints = _runtime.words_to_ints(words)
     make = PaillierEncryptedNumber._make
-    el = [make(public_key, c, int(e), obfuscated) for c, e in zip(ints, exps.tolist())]
+    if isinstance(obfuscated, np.ndarray):
+        el = [make(public_key, c, int(e), bool(o)) for c, e, o in zip(ints, exps.tolist(), obfuscated.tolist())]
+    else:
+        el = [make(public_key, c, int(e), obfuscated) for c, e in zip(ints, exps.tolist())]
     objs = np.empty(len(el), dtype=object)
     objs[:] = el
     return PaillierArray(objs.reshape(shape), _Packed(public_key.n, words, exps.astype(np.int64), ints))
@@ -174,8 +195,10 @@ def materialize(public_key, words: np.ndarray, exps: np.ndarray, shape, obfuscat
 
 def add_encrypted(a, b):
     """Batched GPU add of two encrypted arrays (broadcasting like numpy). Returns NotImplemented
-    when either side is not entirely PaillierEncryptedNumber."""
+    when either side is not entirely PaillierEncryptedNumber (or there is no GPU)."""
     from . import _runtime
+    if not _runtime.gpu_available():
+        return NotImplemented
     A = np.asarray(a, dtype=object) if not isinstance(a, PaillierEncryptedNumber) else None
     if A is None or A.size == 0:
         return NotImplemented
@@ -259,6 +282,8 @@ def mul_plain(a, y):
     from . import _runtime
     if isinstance(y, PaillierEncryptedNumber):
         raise ValueError("PaillierEncryptedNumber * PaillierEncryptedNumber is not allowed.")
+    if not _runtime.gpu_available():
+        return NotImplemented
     A, pk = _encrypted_operand(a)
     if A is None:
         return NotImplemented
@@ -294,7 +319,7 @@ def dot_plain(a, b):
     the GPU: every output is sum_k a[.., k] * b[k, ..] with the reference's exponent alignment
     (bit-identical to numpy's object loop over __mul__ and __add__). NotImplemented otherwise."""
     from . import _runtime
-    if not isinstance(b, np.ndarray) or b.dtype == object or b.ndim not in (1, 2):
+    if not isinstance(b, np.ndarray) or b.dtype == object or b.ndim not in (1, 2) or not _runtime.gpu_available():
         return NotImplemented
     A, pk = _encrypted_operand(a)
     if A is None or A.ndim not in (1, 2):
@@ -335,7 +360,7 @@ def add_plain(a, y):
     redone by the per-element operator, which raises the reference's exception where it does.
     NotImplemented when an operand is not of a device type."""
     from . import _runtime
-    if isinstance(y, PaillierEncryptedNumber) or not _plain_operand(y):
+    if isinstance(y, PaillierEncryptedNumber) or not _plain_operand(y) or not _runtime.gpu_available():
         return NotImplemented
     A, pk = _encrypted_operand(a)
     if A is None:
@@ -399,30 +424,39 @@ def from_wire(buf, public_key=None) -> PaillierArray:
     """Inverse of to_wire. `public_key` (optional) must match the key in the buffer (ValueError
     otherwise, like encrypted_number.py:169-170); without it a PaillierPublicKey is rebuilt from n."""
     from .keypair import PaillierPublicKey
-    mv = memoryview(buf)
-    if bytes(mv[:6]) != _WIRE_MAGIC:
+    mv = memoryview(buf).cast("B")
+    bad = ValueError("corrupted ciphertext array")
+    if len(mv) < 14 or bytes(mv[:6]) != _WIRE_MAGIC:
         raise ValueError("not a flexpai ciphertext array")
     o = 6
     ndim = int(np.frombuffer(mv, "<u4", 1, o)[0]); o += 4
+    if ndim > 32 or len(mv) < o + 8 * ndim + 4:
+        raise bad
     shape = tuple(int(v) for v in np.frombuffer(mv, "<i8", ndim, o)); o += 8 * ndim
     nb = int(np.frombuffer(mv, "<u4", 1, o)[0]); o += 4
+    if any(v < 0 for v in shape) or nb == 0 or len(mv) < o + nb + 4:
+        raise bad
     n = int.from_bytes(mv[o:o + nb], "little"); o += nb
     W = int(np.frombuffer(mv, "<u4", 1, o)[0]); o += 4
+    if n < 3 or W != (2 * n.bit_length() + 31) // 32:     # the key's ciphertext width, not the sender's word
+        raise bad
     N = int(np.prod(shape)) if shape else 1
+    if len(mv) != o + N * (4 * W + 5):
+        raise ValueError("corrupted ciphertext array (length mismatch)")
     exps = np.frombuffer(mv, "<i4", N, o).astype(np.int32); o += 4 * N
     obf = np.frombuffer(mv, np.uint8, N, o); o += N
     words = np.frombuffer(mv, "<u4", N * W, o).reshape(N, W).copy(); o += 4 * N * W
-    if o != len(mv):
-        raise ValueError("corrupted ciphertext array (length mismatch)")
     if public_key is None:
         public_key = PaillierPublicKey(n)
     elif public_key.n != n:
         raise ValueError("ciphertext array was encrypted under a different public key")
-    res = materialize(public_key, words, exps, shape, obfuscated=False)
-    flat = np.asarray(res).reshape(-1)
-    for i in np.flatnonzero(obf).tolist():
-        e = flat[i]
-        flat[i] = PaillierEncryptedNumber._make(public_key, e.ciphertext(False), e.exponent, True)
-    if obf.any():
-        res._packed = None
+    res = materialize(public_key, words, exps, shape, obfuscated=obf != 0)
+    nsq = public_key.nsquare
+    if any(c >= nsq for c in res._packed.ints):
+        raise ValueError("corrupted ciphertext array (ciphertext >= n^2)")
     return res
+
+
+def _from_pickle(buf) -> PaillierArray:
+    """Unpickling hook of PaillierArray (see the module docstring)."""
+    return from_wire(buf)

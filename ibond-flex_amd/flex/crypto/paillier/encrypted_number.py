@@ -87,6 +87,11 @@ class PaillierEncryptedNumber(object):
         if new_exponent < self.exponent:
             raise ValueError("New exponent %i should be great than old exponent %i" % (new_exponent, self.exponent))
         factor = pow(FixedPointNumber.BASE, new_exponent - self.exponent)
+        if factor <= self.public_key.max_int:
+            # __mul__(factor) for an int factor in range: encode gives (factor, exponent 0), so it is
+            # c^factor mod n^2 (encrypted_number.py:107-109); out-of-range factors take __mul__ and raise
+            c = gmpy_math.powmod(self.ciphertext(False), factor, self.public_key.nsquare)
+            return PaillierEncryptedNumber(self.public_key, c, new_exponent)
         new_encryptednumber = self.__mul__(factor)
         new_encryptednumber.exponent = new_exponent
         return new_encryptednumber

@@ -94,6 +94,8 @@ typedef struct pai_ctx pai_ctx;
                                     free device memory less 4 GiB)                                        */
 #define PAI_OPT_FB_READY 7       /* read-only: 1 when the fixed-base tables are resident                    */
 
+/* Number of visible GPUs (0 when there is none or the runtime cannot start). */
+int pai_device_count(int* count);
 int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** out);
 int pai_ctx_set_private(pai_ctx* ctx, const uint8_t* p_le, const uint8_t* q_le, size_t half_bytes);
 void pai_ctx_destroy(pai_ctx* ctx);

@@ -1,0 +1,60 @@
+"""GPU parity at BASELINE.json's full sizes (configs[1], configs[2]: 1 048 576 elements, nb = 2048),
+through the C ABI, checked by size-independent properties plus a bit-exact oracle sample:
+
+* decrypt(encrypt(x)) == x exactly for every element (fixed-base key-holder path, the bench's timed
+  path), with every status OK; a sample of ciphertexts equals the oracle's restatement;
+* one 8-way add of 8 encrypted 1M arrays: the decrypted sums equal the exact sums (checked against the
+  float64 sums within one ulp, and bit-exactly against the oracle on a sample of ciphertexts)."""
+import numpy as np
+import pytest
+
+from oracle import paillier_oracle as O
+
+pytestmark = pytest.mark.gpu
+N = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def ctx2048(golden):
+    from flex.crypto.paillier import _native
+    k = golden["keys"]["2048"]
+    key = O.Key(int(k["n"], 16), int(k["p"], 16), int(k["q"], 16))
+    return _native.Context(key.n, 0, key.p, key.q), key
+
+
+def test_full_size_roundtrip(ctx2048):
+    from flex.crypto.paillier import _native as Nn
+    ctx, key = ctx2048
+    x = np.random.default_rng(0).standard_normal(N, dtype=np.float32)
+    rk = bytes(range(200, 232))
+    ct, ex, st = ctx.encrypt(x, obf_mode=Nn.PAI_OBF_RNG, rng_key=rk, index_base=0)
+    assert np.all(st == 0)
+    val, _, dst, _ = ctx.decrypt(ct, ex)
+    assert np.all(dst == 0) and np.array_equal(val, x.astype(np.float64))
+    params = ctx.fixed_base_info()
+    idx = [0, 1, N // 3, N - 1]
+    got = Nn.words_to_ints(ct[idx])
+    for j, i in enumerate(idx):
+        assert (got[j], int(ex[i])) == O.fb_encrypt_value(x[i], key, rk, i, params)
+
+
+def test_full_size_add8(ctx2048):
+    from flex.crypto.paillier import _native as Nn
+    ctx, key = ctx2048
+    xs = [np.random.default_rng(k).standard_normal(N, dtype=np.float32) for k in range(8)]
+    rk = bytes(range(32))
+    cts, exs = [], []
+    for k, x in enumerate(xs):
+        ct, ex, _ = ctx.encrypt(x, obf_mode=Nn.PAI_OBF_RNG, rng_key=rk, index_base=(k + 1) * N)
+        cts.append(ct)
+        exs.append(ex)
+    s, es = ctx.add(cts, exs)
+    val, _, st, _ = ctx.decrypt(s, es)
+    assert np.all(st == 0)
+    ref = np.sum([x.astype(np.float64) for x in xs], axis=0)
+    assert np.all(np.abs(val - ref) <= np.spacing(np.abs(ref)))
+    idx = [0, 12345, N - 1]
+    got = Nn.words_to_ints(s[idx])
+    for j, i in enumerate(idx):
+        C, E = O.add_k([Nn.words_to_ints(c[i:i + 1])[0] for c in cts], [int(e[i]) for e in exs], key)
+        assert (got[j], int(es[i])) == (C, E)

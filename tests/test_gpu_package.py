@@ -157,3 +157,68 @@ def test_decrypt_errors(pe_pd, golden):
     pe2, _ = generate_paillier_encryptor_decryptor(1024, seed=99)
     with pytest.raises(ValueError):
         pd.decrypt(pe2.encrypt(np.array([1.0], dtype=np.float32)))
+
+
+def test_received_arrays_run_on_the_gpu(pe_pd):
+    """Arrays that arrive over the wire (pickled by the sender, ion.py:150-178) unpickle as PaillierArray
+    and the receiver's unchanged operators reach the device: the HE_SA_FT coordinator's `+`
+    (he_sa_ft/train.py:66-69) -> pai_add, HE_LINEAR's `sum(...)` (he_linear_ft/train.py:64-65) ->
+    pai_add_plain + pai_add, HE_OTP_LR's `(-1/bs) * enc.dot(features)` (he_otp_lr_ft1/train.py:158-160)
+    -> pai_matmul + pai_mul. Bit-exact against the oracle's restatement of encrypted_number.py."""
+    from flex.crypto.paillier import _runtime
+    from flex.crypto.paillier.cipher_array import PaillierArray
+    pe, pd = pe_pd
+    key = O.Key(pe.pub_key.n, pd.priv_key.p, pd.priv_key.q)
+    rng = np.random.default_rng(11)
+    xs = [(rng.standard_normal(300) * (10.0 ** (k - 3))).astype(np.float32) for k in range(8)]
+    recv = [pickle.loads(pickle.dumps(pe.encrypt(x))) for x in xs]
+    assert all(type(r) is PaillierArray and r._valid_packed() is not None for r in recv)
+    ctx = _runtime.context(pe.pub_key)
+    c0 = dict(ctx.calls)
+    s = recv[0]
+    for r in recv[1:]:
+        s = s + r
+    assert ctx.calls["pai_add"] - c0.get("pai_add", 0) == 7
+    for i in (0, 17, 299):
+        C, E = O.add_k([r[i].ciphertext(False) for r in recv], [r[i].exponent for r in recv], key)
+        assert (s[i].ciphertext(False), s[i].exponent) == (C, E)
+    assert np.allclose(pd.decrypt(s), np.sum([x.astype(np.float64) for x in xs], axis=0), rtol=1e-12, atol=0)
+    c1 = dict(ctx.calls)
+    t = sum(recv)
+    assert ctx.calls["pai_add_plain"] - c1.get("pai_add_plain", 0) == 1
+    assert ctx.calls["pai_add"] - c1.get("pai_add", 0) == 7
+    assert [(a.ciphertext(False), a.exponent) for a in t] == [(a.ciphertext(False), a.exponent) for a in s]
+    v = pickle.loads(pickle.dumps(pe.encrypt(xs[3][:32])))
+    feats = rng.standard_normal((32, 6))
+    c2 = dict(ctx.calls)
+    g = (-1 / 32) * v.dot(feats)
+    assert ctx.calls["pai_matmul"] - c2.get("pai_matmul", 0) == 1
+    assert ctx.calls["pai_mul"] - c2.get("pai_mul", 0) == 1
+    for j in (0, 5):
+        terms = [O.mul_scalar(v[i].ciphertext(False), v[i].exponent, float(feats[i, j]), key) for i in range(32)]
+        C, E = O.add_k([a for a, _ in terms], [b for _, b in terms], key)
+        C, E = O.mul_scalar(C, E, -1 / 32, key)
+        assert (g[j].ciphertext(False), g[j].exponent) == (C, E)
+
+
+def test_context_cache_is_bounded(monkeypatch):
+    """contexts are held in a bounded LRU; a process cycling through keys does not keep
+    every key's fixed-base tables resident."""
+    import torch
+    from flex.crypto.paillier import _runtime
+    from flex.crypto.paillier.keypair import generate_paillier_keypair
+    monkeypatch.setenv("FLEXPAI_MAX_CONTEXTS", "2")
+    monkeypatch.setenv("FLEXPAI_FB_WINDOW", "16")
+    import gc
+    gc.collect()
+    free0, _ = torch.cuda.mem_get_info()
+    for seed in range(21, 27):
+        pk, sk = generate_paillier_keypair(1024, seed=seed)
+        ctx = _runtime.context(pk, sk)
+        ctx.prepare_fixed_base()                # ~0.5 GB of tables per 1024-bit key at W = 16
+        assert ctx.fb_ready
+        del ctx
+        gc.collect()
+    assert len(_runtime.cached_contexts()) <= 2
+    free1, _ = torch.cuda.mem_get_info()
+    assert free0 - free1 < 3 * 600 * 2 ** 20, (free0 - free1) / 2 ** 20

@@ -9,6 +9,8 @@ import re
 import numpy as np
 import pytest
 
+from oracle import paillier_oracle as O
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -78,17 +80,116 @@ def test_encrypted_number_pickle_layout():
     assert e2.ciphertext(False) == 12345 and e2.exponent == 13 and e2.public_key == pk
 
 
-def test_cipher_array_pickles_as_plain_ndarray():
+def _small_array(pk, vals, obf=(False, True, False)):
     from flex.crypto.paillier.cipher_array import PaillierArray
     from flex.crypto.paillier.encrypted_number import PaillierEncryptedNumber
+    objs = np.empty(len(vals), dtype=object)
+    objs[:] = [PaillierEncryptedNumber._make(pk, c, e, o) for (c, e), o in zip(vals, obf)]
+    return PaillierArray(objs)
+
+
+def test_cipher_array_pickles_through_wire_format(monkeypatch):
+    """A PaillierArray unpickles as a PaillierArray (ciphertexts, exponents, obfuscation flags kept, packed
+    words cached for the GPU ops); FLEXPAI_PICKLE_PLAIN=1 pickles a plain object ndarray instead."""
+    from flex.crypto.paillier.cipher_array import PaillierArray
     from flex.crypto.paillier.keypair import PaillierPublicKey
     pk = PaillierPublicKey(1000003 * 1000033)
-    objs = np.empty(3, dtype=object)
-    objs[:] = [PaillierEncryptedNumber(pk, i + 5, 1) for i in range(3)]
-    a = PaillierArray(objs)
+    a = _small_array(pk, [(5, 1), (6, -3), (7, 12)])
     assert isinstance(a, np.ndarray)
     b = pickle.loads(pickle.dumps(a))
-    assert type(b) is np.ndarray and b.dtype == object and b[2].ciphertext(False) == 7
+    assert type(b) is PaillierArray and b._valid_packed() is not None
+    assert [e.ciphertext(False) for e in b] == [5, 6, 7] and [e.exponent for e in b] == [1, -3, 12]
+    assert [e._is_obfuscated() for e in b] == [False, True, False]
+    assert b[0].public_key == pk
+    monkeypatch.setenv("FLEXPAI_PICKLE_PLAIN", "1")
+    c = pickle.loads(pickle.dumps(a))
+    assert type(c) is np.ndarray and c.dtype == object and c[2].ciphertext(False) == 7
+    # the plain pickle is the reference's own object layout (slots state), loadable by unmodified peers
+    assert c[1]._is_obfuscated() and c[1].exponent == -3
+
+
+def test_from_wire_rejects_tampered_buffers():
+    """the word count W, the shape and every ciphertext (< n^2) are validated before any
+    buffer reaches the C ABI."""
+    from flex.crypto.paillier import cipher_array as ca
+    from flex.crypto.paillier.keypair import PaillierPublicKey
+    n = 1000003 * 1000033
+    pk = PaillierPublicKey(n)
+    buf = bytearray(ca.to_wire(_small_array(pk, [(5, 1), (6, 2), (7, 3)])))
+    assert [e.ciphertext(False) for e in ca.from_wire(bytes(buf))] == [5, 6, 7]
+    nb = (n.bit_length() + 7) // 8
+    w_off = 6 + 4 + 8 + 4 + nb
+    for W in (2, 4):                               # fewer / more words than the key's ciphertext width (3)
+        t = bytearray(buf)
+        t[w_off:w_off + 4] = np.uint32(W).tobytes()
+        with pytest.raises(ValueError):
+            ca.from_wire(bytes(t))
+    t = bytearray(buf)
+    t[10:18] = np.int64(-3).tobytes()              # negative shape entry
+    with pytest.raises(ValueError):
+        ca.from_wire(bytes(t))
+    t = bytearray(buf)
+    t[-4:] = b"\xff\xff\xff\xff"                  # last ciphertext >= n^2
+    with pytest.raises(ValueError):
+        ca.from_wire(bytes(t))
+    with pytest.raises(ValueError):
+        ca.from_wire(bytes(buf[:-1]))
+    with pytest.raises(ValueError):
+        ca.from_wire(bytes(buf), PaillierPublicKey(1000003 * 1000037))
+
+
+def test_host_gmp_binding_matches_python_ints():
+    import random
+    from flex.crypto.paillier import _bigint
+    assert _bigint._gmp is not None, "the package's GMP binding (_gmp.so) is built by __graft_entry__.build()"
+    rnd = random.Random(7)
+    for _ in range(300):
+        c = rnd.getrandbits(rnd.randint(65, 4096)) | 1
+        a, b = rnd.getrandbits(rnd.randint(0, 4100)), rnd.getrandbits(rnd.randint(0, 80))
+        assert _bigint.mulmod(a, b, c) == a * b % c
+        assert _bigint.powmod(a, b, c) == (1 if a == 1 else pow(a, b, c))
+        try:
+            inv = pow(a, -1, c)
+        except ValueError:
+            with pytest.raises(ZeroDivisionError):
+                _bigint.invert(a, c)
+        else:
+            assert _bigint.invert(a, c) == inv
+
+
+def test_operators_without_gpu_follow_the_reference(golden):
+    """On a host without a GPU (this container) the operators on unpickled ciphertext arrays run the
+    reference's per-element computation (numpy's object loop over PaillierEncryptedNumber on GMP):
+    bit-identical to the oracle's restatement of encrypted_number.py:65-185."""
+    from flex.crypto.paillier import _runtime
+    from flex.crypto.paillier.encrypted_number import PaillierEncryptedNumber
+    from flex.crypto.paillier.keypair import PaillierPublicKey
+    if _runtime.gpu_available():
+        pytest.skip("a GPU is present: the device path runs instead (tests/test_gpu_package.py)")
+    k = golden["keys"]["1024"]
+    key = O.Key(int(k["n"], 16), int(k["p"], 16), int(k["q"], 16))
+    pk = PaillierPublicKey(key.n)
+    rng = np.random.default_rng(3)
+    xs = [rng.standard_normal(6).astype(np.float32) * np.float32(10.0 ** k) for k in range(3)]
+    arrs = []
+    for s, x in enumerate(xs):
+        recs = [O.encrypt_value(v, key, O.golden_r(key.n, 900 + s, i)) for i, v in enumerate(x)]
+        arrs.append(pickle.loads(pickle.dumps(_small_array(pk, recs, [True] * len(recs)))))
+    tot = arrs[0]
+    for a in arrs[1:]:
+        tot = tot + a                              # HE_SA_FT coordinator (iterative_add)
+    for i in range(6):
+        want = O.add_k([a[i].ciphertext(False) for a in arrs], [a[i].exponent for a in arrs], key)
+        assert (tot[i].ciphertext(False), tot[i].exponent) == want
+    s2 = sum(arrs)                                 # HE_LINEAR sum(ciphertexts)
+    assert [(e.ciphertext(False), e.exponent) for e in s2] == [(e.ciphertext(False), e.exponent) for e in tot]
+    feats = rng.standard_normal((6, 2))
+    d = arrs[0].dot(feats)                         # HE_OTP_LR enc_diff_y.dot(features)
+    for j in range(2):
+        terms = [O.mul_scalar(arrs[0][i].ciphertext(False), arrs[0][i].exponent, float(feats[i, j]), key)
+                 for i in range(6)]
+        want = O.add_k([t[0] for t in terms], [t[1] for t in terms], key)
+        assert isinstance(d[j], PaillierEncryptedNumber) and (d[j].ciphertext(False), d[j].exponent) == want
 
 
 def test_encryptor_pickles_without_device_state():

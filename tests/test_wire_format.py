@@ -1,6 +1,7 @@
 """Bulk ciphertext-array wire format (cipher_array.to_wire / from_wire): round trip of
-ciphertexts, exponents, obfuscation flags and shape; key checks; and that pickling a PaillierArray still
-produces the plain object ndarray unmodified FLEX peers load. CPU only (no kernel calls)."""
+ciphertexts, exponents, obfuscation flags and shape; key checks; pickling a PaillierArray goes through the
+wire format (a PaillierArray comes back), and with FLEXPAI_PICKLE_PLAIN=1 it produces the plain object
+ndarray unmodified FLEX peers load. CPU only (no kernel calls)."""
 import pickle
 
 import numpy as np
@@ -41,7 +42,7 @@ def test_wire_round_trip(golden, shape):
     assert from_wire(buf).reshape(-1)[0].public_key.n == pk.n
 
 
-def test_wire_errors_and_pickle(golden):
+def test_wire_errors_and_pickle(golden, monkeypatch):
     from flex.crypto.paillier.cipher_array import from_wire, to_wire
     from flex.crypto.paillier.keypair import PaillierPublicKey
     arr, pk = _array(golden, (4,))
@@ -54,5 +55,10 @@ def test_wire_errors_and_pickle(golden):
         from_wire(b"nonsense" + buf)
     with pytest.raises(TypeError):
         to_wire(np.array([1.0, 2.0]))
+    back = pickle.loads(pickle.dumps(arr))
+    assert type(back) is type(arr) and back._valid_packed() is not None
+    assert [(a.ciphertext(False), a.exponent, a._is_obfuscated()) for a in arr] == \
+        [(b.ciphertext(False), b.exponent, b._is_obfuscated()) for b in back]
+    monkeypatch.setenv("FLEXPAI_PICKLE_PLAIN", "1")
     plain = pickle.loads(pickle.dumps(arr))
     assert type(plain) is np.ndarray and plain.dtype == object

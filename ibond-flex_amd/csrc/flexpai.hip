@@ -43,6 +43,9 @@ struct pai_ctx {
   uint32_t* d_prog = nullptr;   // Montgomery program for x^n (run_program, kernels.hpp)
   int nprog = 0;
   uint32_t* d_oneR = nullptr;   // R mod n^2
+  uint32_t* d_RS = nullptr;     // [ADD_KMAX + 2][ct_words]: R^s mod n^2 (k_add's Montgomery corrections)
+  void* d_addplan = nullptr;    // k_add schedule sort: buckets, permutation, histogram
+  size_t addplan_bytes = 0;
   // private key material
   bool has_priv = false;
   DecHalf* d_halves = nullptr;
@@ -83,6 +86,8 @@ struct pai_ctx {
   std::vector<void*> fb_mem;    // tables and their constants (rebuilt when the window changes)
   HBig fb_p, fb_q;              // p < q
   float fb_host_ms = 0.f, fb_dev_ms = 0.f;
+  uint32_t* fb_last_w = nullptr;  // debugging: k_fb output of the last chunk ([2][SB][fb_last_n])
+  long long fb_last_n = 0;
   uint64_t fb_table_bytes = 0;
   std::vector<void*> allocs;
   std::vector<void*> priv_allocs;   // private-key constants: all freed together if set_private fails
@@ -119,6 +124,7 @@ struct pai_ctx {
     if (d_inv) (void)hipFree(d_inv);
     if (d_plain) (void)hipFree(d_plain);
     if (d_seg) (void)hipFree(d_seg);
+    if (d_addplan) (void)hipFree(d_addplan);
   }
 };
 
@@ -259,6 +265,8 @@ static int ensure_scratch(pai_ctx* c, size_t bytes) {
   return 0;
 }
 
+static size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
+
 static int ensure_buf(void** buf, size_t* have, size_t bytes) {
   if (bytes <= *have) return 0;
   if (*buf) HIPCHK(hipFree(*buf));
@@ -295,6 +303,15 @@ static int blocks_per_cu(K kernel, int threads, size_t lds) {
 
 // C-linkage comes from the declarations in flexpai.h.
 const char* pai_last_error(void) { return g_last_error.c_str(); }
+
+int pai_device_mem_info(int device, uint64_t* free_bytes, uint64_t* total_bytes) {
+  HIPCHK(hipSetDevice(device));
+  size_t fr = 0, tot = 0;
+  HIPCHK(hipMemGetInfo(&fr, &tot));
+  if (free_bytes) *free_bytes = fr;
+  if (total_bytes) *total_bytes = tot;
+  return 0;
+}
 
 int pai_device_count(int* count) {
   if (!count) return fail(PAI_ERR_ARG, "null argument");
@@ -346,8 +363,19 @@ int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** ou
   }
   c->nprog = (int)prog.size();
   HBig oneR = mul_pow2_mod(HBig(1), Rbits, c->N);
+  std::vector<uint32_t> rs;
+  {
+    HMont M(c->N);
+    HBig x(1);
+    for (int s = 0; s <= ADD_KMAX + 1; ++s) {
+      const std::vector<uint32_t> v = x.words(c->ct_words);
+      rs.insert(rs.end(), v.begin(), v.end());
+      x = M.mul(M.mul(x, oneR), M.r2);   // x R mod N
+    }
+  }
   int rc;
-  if ((rc = upload(c, c->N.limbs(c->S_e, LB), &c->d_N)) || (rc = upload(c, R2.limbs(c->S_e, LB), &c->d_R2)) ||
+  if ((rc = upload(c, rs, &c->d_RS)) || (rc = upload(c, c->N.limbs(c->S_e, LB), &c->d_N)) ||
+      (rc = upload(c, R2.limbs(c->S_e, LB), &c->d_R2)) ||
       (rc = upload(c, n.limbs(c->S_e, LB), &c->d_nl)) || (rc = upload(c, prog, &c->d_prog)) ||
       (rc = upload(c, oneR.limbs(c->S_e, LB), &c->d_oneR))) {
     delete c;
@@ -912,6 +940,8 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     pf.status = e.status ? e.status + off : nullptr;
     HIPCHK(fb_launch(SB, pf, (int)std::min<long long>(gxF, (n + LANE_BLOCK - 1) / LANE_BLOCK), st));
     stage_mark(c, 2, st);
+    c->fb_last_w = w;
+    c->fb_last_n = n;
     FbFinParams pg{};
     pg.w = w;
     pg.n = n;
@@ -1063,13 +1093,58 @@ static int launch_add(pai_ctx* c, AddParams& p, hipStream_t st) {
   constexpr int GPB = BLOCK / TPI;
   const size_t lds = (size_t)GPB * S * 4;
   const int grid = grid_for(c, k_add<TPI>, lds, p.n, GPB);
-  int rc = ensure_scratch(c, (size_t)grid * BLOCK * TILE_WORDS_PER_LANE * 4);
-  if (rc) return rc;
-  p.scratch = (uint32_t*)c->d_scratch;
   hipLaunchKernelGGL(k_add<TPI>, dim3(grid), dim3(BLOCK), lds, st, p);
   HIPCHK(hipGetLastError());
   return 0;
 }
+
+// k-way add of p.k <= ADD_KMAX operands per instance: schedule sort (k_add_plan, k_add_scan,
+// k_add_scatter) then the Horner product k_add (kernels.hpp).
+static int run_add(pai_ctx* c, AddParams p, hipStream_t st) {
+  if (p.n <= 0) return 0;
+  const size_t nb_bucket = align16((size_t)p.n * 2), nb_perm = align16((size_t)p.n * 4);
+  int rc = ensure_buf(&c->d_addplan, &c->addplan_bytes, nb_bucket + nb_perm + ADD_TMAX * 4);
+  if (rc) return rc;
+  uint16_t* bucket = (uint16_t*)c->d_addplan;
+  int* perm = (int*)((char*)c->d_addplan + nb_bucket);
+  unsigned* hist = (unsigned*)((char*)c->d_addplan + nb_bucket + nb_perm);
+  p.N = c->d_N;
+  p.RS = c->d_RS;
+  p.mprime = c->mprime_N;
+  p.ct_words = c->ct_words;
+  p.perm = nullptr;
+  const int g = (int)std::max<long long>(1, std::min<long long>((p.n + 255) / 256, 8ll * c->cus));
+  HIPCHK(hipMemsetAsync(hist, 0, ADD_TMAX * 4, st));
+  hipLaunchKernelGGL(k_add_plan<0>, dim3(g), dim3(256), 0, st, p, bucket, hist);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_add_scan<0>, dim3(1), dim3(ADD_TMAX), 0, st, hist);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_add_scatter<0>, dim3(g), dim3(256), 0, st, (long long)p.n, (const uint16_t*)bucket, hist, perm);
+  HIPCHK(hipGetLastError());
+  p.perm = perm;
+  switch (c->tpi_e) {
+    case 2: return launch_add<2>(c, p, st);
+    case 4: return launch_add<4>(c, p, st);
+    case 8: return launch_add<8>(c, p, st);
+  }
+  return fail(PAI_ERR_KEY, "unsupported group size");
+}
+
+static AddParams add_params(const uint32_t* cts, const int32_t* exps, int k, long long N, uint32_t* out, int32_t* out_exp,
+                            const long long* gidx = nullptr) {
+  AddParams p{};
+  p.cts = cts;
+  p.exps = exps;
+  p.k = k;
+  p.out = out;
+  p.out_exp = out_exp;
+  p.n = N;
+  p.gidx = gidx;
+  return p;
+}
+
+static int add_dev(pai_ctx* c, const uint32_t* cts, const int32_t* exps, int k, long long N, uint32_t* out,
+                   int32_t* out_exp, hipStream_t st);
 
 int pai_add_dev(pai_ctx* c, const uint32_t* d_cts, const int32_t* d_exps, int k, size_t N, uint32_t* d_out,
                 int32_t* d_exp_out, void* stream) {
@@ -1077,15 +1152,7 @@ int pai_add_dev(pai_ctx* c, const uint32_t* d_cts, const int32_t* d_exps, int k,
   if (N == 0) return 0;
   if (k < 1 || !d_cts || !d_exps || !d_out || !d_exp_out) return fail(PAI_ERR_ARG, "pai_add_dev: bad arguments");
   HIPCHK(hipSetDevice(c->device));
-  AddParams p{d_cts, d_exps, k, d_out, d_exp_out, (long long)N, c->d_N, c->d_R2, c->d_oneR, c->mprime_N,
-              c->ct_words, nullptr};
-  hipStream_t st = (hipStream_t)stream;
-  switch (c->tpi_e) {
-    case 2: return launch_add<2>(c, p, st);
-    case 4: return launch_add<4>(c, p, st);
-    case 8: return launch_add<8>(c, p, st);
-  }
-  return fail(PAI_ERR_KEY, "unsupported group size");
+  return add_dev(c, d_cts, d_exps, k, (long long)N, d_out, d_exp_out, (hipStream_t)stream);
 }
 
 template <int TPI>
@@ -1202,7 +1269,6 @@ struct DevScope {
 };
 
 // ------------------------------------------------------------------ ciphertext x plaintext
-static size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
 
 static int inv_grid(pai_ctx* c, long long nseg) {
   int occ = 1;
@@ -1280,15 +1346,27 @@ static int launch_mul(pai_ctx* c, MulParams& p, hipStream_t st) {
   return 0;
 }
 
+// k consecutive [N][W] operand arrays; more than ADD_KMAX operands are summed in chunks of ADD_KMAX
+// (the partial sums are exact ciphertexts, so the result is the same integer)
 static int add_dev(pai_ctx* c, const uint32_t* cts, const int32_t* exps, int k, long long N, uint32_t* out,
                    int32_t* out_exp, hipStream_t st) {
-  AddParams p{cts, exps, k, out, out_exp, N, c->d_N, c->d_R2, c->d_oneR, c->mprime_N, c->ct_words, nullptr};
-  switch (c->tpi_e) {
-    case 2: return launch_add<2>(c, p, st);
-    case 4: return launch_add<4>(c, p, st);
-    case 8: return launch_add<8>(c, p, st);
+  if (k <= ADD_KMAX) return run_add(c, add_params(cts, exps, k, N, out, out_exp), st);
+  const int parts = (k + ADD_KMAX - 1) / ADD_KMAX;
+  const size_t W = c->ct_words;
+  uint32_t* pc = nullptr;
+  int32_t* pe = nullptr;
+  HIPCHK(hipMallocAsync((void**)&pc, (size_t)parts * N * W * 4, st));
+  HIPCHK(hipMallocAsync((void**)&pe, (size_t)parts * N * 4, st));
+  int rc = 0;
+  for (int q = 0; q < parts && !rc; ++q) {
+    const int kq = std::min(ADD_KMAX, k - q * ADD_KMAX);
+    rc = run_add(c, add_params(cts + (size_t)q * ADD_KMAX * N * W, exps + (size_t)q * ADD_KMAX * N, kq, N,
+                               pc + (size_t)q * N * W, pe + (size_t)q * N), st);
   }
-  return fail(PAI_ERR_KEY, "unsupported group size");
+  if (!rc) rc = add_dev(c, pc, pe, parts, N, out, out_exp, st);
+  (void)hipFreeAsync(pc, st);
+  (void)hipFreeAsync(pe, st);
+  return rc;
 }
 
 int pai_mul_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t N, int dtype, const void* d_x,
@@ -1417,14 +1495,7 @@ int pai_segment_add_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, 
     HIPCHK(hipMemcpyAsync(d_g, g.data(), g.size() * 8, hipMemcpyHostToDevice, st));
     uint32_t* o = last ? d_out : part[side];
     int32_t* oe = last ? d_exp_out : pexp[side];
-    AddParams p{in, in_e, C, o, oe, outs, c->d_N, c->d_R2, c->d_oneR, c->mprime_N, c->ct_words, nullptr, d_g};
-    switch (c->tpi_e) {
-      case 2: rc = launch_add<2>(c, p, st); break;
-      case 4: rc = launch_add<4>(c, p, st); break;
-      case 8: rc = launch_add<8>(c, p, st); break;
-      default: rc = fail(PAI_ERR_KEY, "unsupported group size");
-    }
-    if (rc) return rc;
+    if ((rc = run_add(c, add_params(in, in_e, C, outs, o, oe, d_g), st))) return rc;
     HIPCHK(hipStreamSynchronize(st));   // the gather rows (host vector) are reused by the next level
     if (last) return 0;
     in = o;
@@ -1695,6 +1766,20 @@ int pai_decrypt(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, do
   return 0;
 }
 
+
+// ------------------------------------------------------------------ debugging hook (tests / tools only)
+// Copies the per-half k_fb outputs (c0 G_h^a_h mod h^2, limbs [2][SB][n]) of the last fixed-base chunk.
+extern "C" int pai_debug_fb_w(pai_ctx* c, uint32_t* out, size_t max_words, long long* n, int* sb) {
+  if (!c || !c->fb_last_w) return fail(PAI_ERR_ARG, "no fixed-base output");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipDeviceSynchronize());
+  const size_t words = (size_t)2 * c->crt_sb * c->fb_last_n;
+  if (words > max_words) return fail(PAI_ERR_ARG, "buffer too small");
+  HIPCHK(hipMemcpy(out, c->fb_last_w, words * 4, hipMemcpyDeviceToHost));
+  *n = c->fb_last_n;
+  *sb = c->crt_sb;
+  return 0;
+}
 
 // ------------------------------------------------------------------ engine unit-test hook
 template <int TPI>

@@ -45,7 +45,7 @@ struct AddParams {
   int32_t* out_exp;
   long long n;
   const uint32_t* N;
-  const uint32_t* RS;     // [ADD_KMAX + 2][S]: R^s mod n^2, s = 0 .. ADD_KMAX + 1 (group layout)
+  const uint32_t* RS;     // [ADD_KMAX + 2][ct_words]: R^s mod n^2, s = 0 .. ADD_KMAX + 1 (32-bit words)
   uint32_t mprime;
   int ct_words;
   // nullable: operand j of instance i is element gidx[i k + j] of the flat cts/exps arrays (-1: padding);
@@ -411,6 +411,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_add(AddParams p) {
 #pragma unroll
       for (int i = 0; i < L; ++i) a[i] = (tig == 0 && i == 0) ? 1u : 0u;
     }
+#pragma clang loop unroll(disable)
     for (;;) {
       // this group's next step: 0 square, 1 times operand `osrc`, 2 times R^s, 3 nothing (times R)
       int op = 3, s = 1;
@@ -450,14 +451,15 @@ __global__ __launch_bounds__(BLOCK, 2) void k_add(AddParams p) {
         }
       }
       if (ballot(op != 3) == 0ull) break;
-      if (op == 0) {
-        write_limbs_lds<TPI>(slot, a, tig);
-      } else if (op == 1) {
+      // branch-free B fill, so the kernel has ONE montmul site (a branch per kind of B makes the
+      // compiler duplicate the 11k-instruction product per path)
+      {
+        const uint32_t* src = op == 1 ? p.cts + osrc * p.ct_words : p.RS + (size_t)s * p.ct_words;
         uint32_t t[L];
-        words_to_limbs(p.cts + osrc * p.ct_words, p.ct_words, t, tig);
+        words_to_limbs(src, p.ct_words, t, tig);
+#pragma unroll
+        for (int i = 0; i < L; ++i) t[i] = op == 0 ? a[i] : t[i];
         write_limbs_lds<TPI>(slot, t, tig);
-      } else {
-        copy_g_to_lds<TPI>(slot, p.RS + (size_t)s * S, tig);
       }
       montmul<TPI>(a, a, slot, TPI, m, p.mprime, lane, tig);
     }

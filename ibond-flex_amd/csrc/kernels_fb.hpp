@@ -463,6 +463,13 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_fb_fin(FbFinParams p) {
       wp[j] = p.w[(size_t)j * p.n + ii];
       wq[j] = p.w[((size_t)SB + j) * p.n + ii];
     }
+    // w_q canonical mod q^2 FIRST: h must be formed from the same representative that c adds
+    {
+      uint32_t q2[SB];
+#pragma unroll
+      for (int j = 0; j < SB; ++j) q2[j] = q2s[j];
+      lane::cond_sub<SB>(wq, q2);                // w_q < q^2
+    }
     // t = w_p + 8 p^2 - w_q in (0, 10 p^2): a valid CIOS input (< 2^(28 SB - 20))
     {
       int64_t c = 0;
@@ -480,12 +487,6 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_fb_fin(FbFinParams p) {
       lane::mont_mul<SB>(wp, cr, m, p.mprime);   // h < 2 p^2
     }
     lane::cond_sub<SB>(wp, m);                   // h < p^2
-    {
-      uint32_t q2[SB];
-#pragma unroll
-      for (int j = 0; j < SB; ++j) q2[j] = q2s[j];
-      lane::cond_sub<SB>(wq, q2);                // w_q < q^2
-    }
     fb_out_all<SB, CW>(wp, wq, q2s, reinterpret_cast<uint4*>(p.ct + ii * p.ct_words), valid,
                        std::make_integer_sequence<int, 2 * SB>{});
   }

@@ -24,7 +24,7 @@ EL_OK, EL_INT, EL_INT_BIG, EL_OVERFLOW, EL_FLOAT_OVF, EL_ENC_RANGE = 0, 1, 2, 3,
 PAI_OPT_CRT_ENCRYPT, PAI_OPT_CRT_AVAILABLE, PAI_OPT_STAGE_TIMING, PAI_OPT_LANE_DECRYPT = 1, 2, 3, 4
 PAI_OPT_FIXED_BASE, PAI_OPT_FB_WINDOW, PAI_OPT_FB_READY = 5, 6, 7
 
-EXPORTED = ("pai_device_count", "pai_ctx_create", "pai_ctx_set_private", "pai_ctx_destroy", "pai_ctx_info", "pai_last_error",
+EXPORTED = ("pai_device_count", "pai_device_mem_info", "pai_ctx_create", "pai_ctx_set_private", "pai_ctx_destroy", "pai_ctx_info", "pai_last_error",
             "pai_ctx_set_option", "pai_ctx_get_option", "pai_ctx_stage_times", "pai_ctx_fixed_base_info",
             "pai_ctx_fixed_base_prepare", "pai_ctx_fixed_base_setup",
             "pai_encrypt", "pai_add", "pai_decrypt", "pai_encrypt_dev", "pai_add_dev", "pai_decrypt_dev",
@@ -51,6 +51,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         lib = ctypes.CDLL(path)
         P, S, I, U64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
         lib.pai_device_count.argtypes = [P]
+        lib.pai_device_mem_info.argtypes = [I, P, P]
         lib.pai_ctx_create.argtypes = [P, S, I, ctypes.POINTER(ctypes.c_void_p)]
         lib.pai_ctx_set_private.argtypes = [P, P, P, S]
         lib.pai_ctx_destroy.argtypes = [P]
@@ -89,6 +90,13 @@ def device_count() -> int:
     n = ctypes.c_int()
     _check(load_library().pai_device_count(ctypes.byref(n)))
     return n.value
+
+
+def device_mem_info(device: int = 0):
+    """(free, total) device memory in bytes, through the engine's own HIP runtime."""
+    fr, tot = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(load_library().pai_device_mem_info(device, ctypes.byref(fr), ctypes.byref(tot)))
+    return fr.value, tot.value
 
 
 def _check(rc: int):

@@ -96,6 +96,8 @@ typedef struct pai_ctx pai_ctx;
 
 /* Number of visible GPUs (0 when there is none or the runtime cannot start). */
 int pai_device_count(int* count);
+/* Free and total device memory of `device` (bytes). */
+int pai_device_mem_info(int device, uint64_t* free_bytes, uint64_t* total_bytes);
 int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** out);
 int pai_ctx_set_private(pai_ctx* ctx, const uint8_t* p_le, const uint8_t* q_le, size_t half_bytes);
 void pai_ctx_destroy(pai_ctx* ctx);

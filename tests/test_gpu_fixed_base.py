@@ -203,3 +203,25 @@ def test_fixed_base_memory_cap_falls_back(golden, monkeypatch):
         assert got[i] == O.encrypt_value(x[i], key, r)[0]
     val, _, _, _ = ctx.decrypt(ct, ex)
     assert np.array_equal(val, x.astype(np.float64))
+
+
+def test_fixed_base_garner_unreduced_half_regression(ctxs):
+    """Regression: k_fb's per-half outputs are < 2 h^2, and Garner must reduce w_q mod q^2 BEFORE it forms
+    h = (w_p - w_q) (q^2)^-1 mod p^2. With the 1024-bit key (R / p^2 = 2^12) w_q lands in [q^2, 2 q^2) for
+    about 1 element in 10^4: elements 1762 and 1798 of this input did, and round-tripped to garbage."""
+    N = _native()
+    ctx, key = ctxs[1024]
+    w0 = ctx.fb_window
+    x = np.random.default_rng(0).standard_normal(20000).astype(np.float32)
+    rk = bytes(range(32))
+    try:
+        ctx.set_fb_window(16)
+        ct, ex, _ = ctx.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk)
+        params = ctx.fixed_base_info()
+    finally:
+        ctx.set_fb_window(w0)
+    val, _, st, _ = ctx.decrypt(ct, ex)
+    assert np.array_equal(val, x.astype(np.float64))
+    got = N.words_to_ints(ct[[1762, 1798]])
+    for j, i in enumerate((1762, 1798)):
+        assert (got[j], int(ex[i])) == O.fb_encrypt_value(x[i], key, rk, i, params)

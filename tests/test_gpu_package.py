@@ -204,14 +204,13 @@ def test_received_arrays_run_on_the_gpu(pe_pd):
 def test_context_cache_is_bounded(monkeypatch):
     """contexts are held in a bounded LRU; a process cycling through keys does not keep
     every key's fixed-base tables resident."""
-    import torch
-    from flex.crypto.paillier import _runtime
+    from flex.crypto.paillier import _native, _runtime
     from flex.crypto.paillier.keypair import generate_paillier_keypair
     monkeypatch.setenv("FLEXPAI_MAX_CONTEXTS", "2")
     monkeypatch.setenv("FLEXPAI_FB_WINDOW", "16")
     import gc
     gc.collect()
-    free0, _ = torch.cuda.mem_get_info()
+    free0, _ = _native.device_mem_info(0)
     for seed in range(21, 27):
         pk, sk = generate_paillier_keypair(1024, seed=seed)
         ctx = _runtime.context(pk, sk)
@@ -220,5 +219,5 @@ def test_context_cache_is_bounded(monkeypatch):
         del ctx
         gc.collect()
     assert len(_runtime.cached_contexts()) <= 2
-    free1, _ = torch.cuda.mem_get_info()
+    free1, _ = _native.device_mem_info(0)
     assert free0 - free1 < 3 * 600 * 2 ** 20, (free0 - free1) / 2 ** 20

@@ -1,35 +1,35 @@
 #!/usr/bin/env python3
-"""bench.py — Paillier-2048 array encryption on MI355X (BASELINE.json metric).
+"""bench.py — Paillier array encryption on MI355X (BASELINE.json metric and configs).
 
-A step = one device-resident encryption of the rank's 1M-element float32 vector: fixed-point
-encode -> c0 = 1 + n*m -> c0 * r^n mod n^2 with a device ChaCha20 obfuscator r per element
-(flex/crypto/paillier/encryptor.py:71-114 semantics), then, for N > 1 GPUs, one RCCL all-gather of
-the ciphertext shards so every rank holds the whole encrypted vector (weak scaling).
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config {0,1,2,3,4}] ...
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL over xGMI)
 
-The workload (BASELINE.json configs[1]: "encrypt+decrypt on 1 MI355X") holds the private key, so
-the default path is the key holder's: r^n sampled through fixed-base tables per CRT half
-(kernels_fb.hpp, `--obf fixedbase`, digit window `--fb-window`, default 20) and recombined with c0
-(k_crt_fin). The generic CRT path (`--obf generic`: r from the ChaCha20 stream, r^n by half-size
-exponentiations, bit-identical to the public-key kernel and GMP), the public-key-only kernel,
-device decryption, the configs[2] leg (8 arrays, 8-way add, decrypt) and the host-boundary rates
-are measured on the same input in the same run, outside the timed region, under `extra`.
-For N > 1 the ciphertext and exponent shards are double-buffered and step i's all-gather overlaps
-step i+1's encryption.
+Workloads (BASELINE.json configs; synthetic float32 N(0,1) vectors, seeded keys):
+  --config 1 (default at N = 1): nb = 2048, 1 048 576 elements per GPU, device-resident encryption
+             (the headline metric "Paillier-2048 encrypts/sec (device-resident), 1M-elem float32 array");
+  --config 3 (default at N > 1): nb = 2048, 16 777 216 elements in total, sharded over the N ranks
+             (strong scaling: 2M per GPU at N = 8), ciphertext shards reassembled on every rank by an
+             RCCL all-gather inside the timed step (double-buffered: step i's gather overlaps step i+1);
+  --config 4: nb = 4096, 4 194 304 elements in total, sharded like config 3;
+  --config 2: nb = 2048, 1M elements: a step = encrypt 8 arrays + one 8-way homomorphic add + decrypt;
+  --config 0: nb = 1024, 1000 elements (the reference's plumbing case; its CPU leg is timed in full).
+A step = one pass of the hot path over the rank's shard, obfuscators from the device ChaCha20 stream
+keyed by the GLOBAL element index (ciphertexts do not depend on N). A key holder encrypts through the
+fixed-base sampler (kernels_fb.hpp; its tables are built, and timed under `setup`, before the timed
+region). `value` = elements of the whole job per second over the K timed steps (barrier + synchronize
+on both sides, max over ranks).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--path crt|public] [--obf fixedbase|generic]
-    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU)
-
-Rank 0 prints ONE JSON line. `value` = encrypts/s over all ranks (max-over-ranks wall clock of the
-K timed steps). `roofline` is for the dominant kernel of the timed path, timed live with HIP events
-recorded on the launch stream between the kernels of every timed encrypt call; its work figure is
-the SURVEY.md §8d canonical 32x32->64 MAC count. `cpu_baseline` is the
-GMP restatement of the reference CPU path (oracle/gmp_oracle.c) on this host's cores, on a bounded
-sample of the same workload, which doubles as a bit-exact check of the GPU output.
+Rank 0 prints ONE JSON line. `roofline` is for the dominant kernel of the timed path, its duration
+timed live with HIP events recorded on the launch stream between the kernels of every timed call; its
+work figure is that kernel's own MAC count (the fixed-base count for k_fb, NOT SURVEY.md §8d's public-
+key W_enc, which is reported beside it as `w_enc_equivalent`). `cpu_baseline` (N = 1 only) is the GMP
+restatement of the reference CPU path (oracle/gmp_oracle.c, threads = os.cpu_count() like the
+reference's Pool(cpu_count())) on a bounded sample of the same workload, which doubles as a bit-exact
+check of the GPU output; `extra.config0_cpu` times configs[0] (nb = 1024, 1k elements) in full.
 """
 import argparse
 import hashlib
 import json
-import math
 import os
 import sys
 import time
@@ -48,6 +48,19 @@ import torch  # noqa: E402
 INT_MAC_PEAK = float(os.environ.get("FLEXPAI_INT_MAC_PEAK", "35.13e12"))
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 
+CONFIGS = {
+    0: {"nb": 1024, "total": 1000, "shard": "strong",
+        "desc": "configs[0]: Paillier n=1024, 1k-element float32 vector (the reference's CPU plumbing case)"},
+    1: {"nb": 2048, "total": 1 << 20, "shard": "weak",
+        "desc": "configs[1]: Paillier n=2048, 1M-element float32 vector per GPU, device-resident encrypt (+decrypt)"},
+    2: {"nb": 2048, "total": 1 << 20, "shard": "weak",
+        "desc": "configs[2]: Paillier n=2048, encrypt 8 x 1M float32 arrays + one 8-way homomorphic add + decrypt"},
+    3: {"nb": 2048, "total": 16 << 20, "shard": "strong",
+        "desc": "configs[3]: Paillier n=2048, 16M-element float32 vector sharded over the GPUs, RCCL all-gather"},
+    4: {"nb": 4096, "total": 4 << 20, "shard": "strong",
+        "desc": "configs[4]: Paillier n=4096, 4M-element float32 vector sharded over the GPUs, RCCL all-gather"},
+}
+
 
 # ------------------------------------------------------------- canonical work
 def _M(s: int) -> int:
@@ -61,20 +74,16 @@ def _P(b: int) -> int:
 
 
 def work_enc_public(nb: int) -> float:
+    """SURVEY.md §8d W_enc: the public-key encryption's canonical MACs per element."""
     return float((_P(nb) + 1) * _M(nb // 16))
 
 
 def work_crt(nb: int) -> dict:
-    """Per-element canonical MACs of the CRT encryption stages."""
+    """Per-element canonical MACs of the generic CRT encryption stages."""
     h = nb // 2
     return {"k_crt_a": float(2 * (_P(h) + 1) * _M(nb // 64)),      # (r mod p_h)^(e_h) mod p_h, both halves
             "k_crt_b": float(2 * (_P(h) + 2) * _M(nb // 32)),      # y^(p_h) * coef mod p_h^2, both halves
             "k_crt_fin": float(3 * _M(nb // 16))}                  # (u_p q^2 + u_q p^2) * c0 mod n^2
-
-
-def fb_digit_count(nb: int, window: int) -> int:
-    """Exponent digits K of the fixed-base sampler: window-bit digits of a_h mod (p_h - 1) (nb/2 bits)."""
-    return -(-(nb // 2) // window)
 
 
 def work_fb(nb: int, digits: int) -> dict:
@@ -83,13 +92,20 @@ def work_fb(nb: int, digits: int) -> dict:
     takes c0), no squarings; k_fb_fin (Garner) = one product mod p^2 + one plain (nb/32)^2 product; the
     ChaCha digit kernel does no MACs. This is NOT the public-key W_enc of §8d (a different algorithm)."""
     s = nb // 32
-    return {"k_fb_digits": 0.0,
-            "k_fb": float(2 * digits * _M(s)),
-            "k_fb_fin": float(_M(s) + s * s)}
+    return {"k_fb_digits": 0.0, "k_fb": float(2 * digits * _M(s)), "k_fb_fin": float(_M(s) + s * s)}
 
 
 def work_dec(nb: int) -> float:
     return float(2 * (_P(nb // 2) + 2) * _M(nb // 32))
+
+
+def work_add(exps: "torch.Tensor", nb: int) -> float:
+    """Canonical k-way add work over [k][N] exponents: per element (k - 1) products plus
+    4 d squarings per operand aligned by d (the reference's per-operand alignment)."""
+    k, n = exps.shape
+    E = exps.max(0).values
+    sq = int((4 * (E.unsqueeze(0) - exps)).sum().item())
+    return float((n * (k - 1) + sq) * _M(nb // 16))
 
 
 def load_traffic(kernel: str, n: int, nb: int):
@@ -104,20 +120,36 @@ def load_traffic(kernel: str, n: int, nb: int):
     return None
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=1 << 20, help="elements per GPU")
-    ap.add_argument("--nb", type=int, default=2048, help="Paillier key bits")
+    ap.add_argument("--config", type=int, choices=sorted(CONFIGS), default=None,
+                    help="BASELINE.json config (default: 1 on one GPU, 3 on several)")
+    ap.add_argument("--n", type=int, default=None, help="override: total elements (per GPU for weak configs)")
+    ap.add_argument("--nb", type=int, default=None, help="override: Paillier key bits")
     ap.add_argument("--path", choices=("crt", "public"), default="crt")
     ap.add_argument("--obf", choices=("fixedbase", "generic"), default="fixedbase",
                     help="device-RNG sampler of r^n on the CRT path (kernels_fb.hpp vs r from ChaCha20)")
     ap.add_argument("--fb-window", type=int, default=20, choices=(8, 12, 16, 20),
-                    help="digit window of the fixed-base tables (20: 55 products per half, 17.5 GB table per half)")
+                    help="digit window of the fixed-base tables (20: 52 products per half, 13.4 GB per half)")
     ap.add_argument("--cpu-sample", type=int, default=16384)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=os.cpu_count() or 1,
+                    help="threads of the GMP CPU baseline (default os.cpu_count(), like the reference's Pool)")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="fixed obfuscator key (sha256 constant) instead of os.urandom on rank 0; reproducible runs only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-decrypt", action="store_true")
     ap.add_argument("--no-public", action="store_true", help="skip timing the public-key path beside CRT")
@@ -130,6 +162,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    cfg_id = args.config if args.config is not None else (1 if world == 1 else 3)
+    cfg = CONFIGS[cfg_id]
+    nb = args.nb or cfg["nb"]
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     dist = None
@@ -141,58 +176,136 @@ def main():
     from flex.crypto.paillier.keypair import generate_paillier_keypair
     from flex.crypto.paillier.sharding import gather_shards_async, shard_bounds
 
-    pk, sk = generate_paillier_keypair(args.nb, seed=1)
-    ctx = _native.Context(pk.n, local_rank, sk.p, sk.q)
+    # workload geometry: weak = N per GPU; strong = the total split into contiguous shards of
+    # ceil(total / world) (the last shard is padded; its tail is computed and discarded)
+    if cfg["shard"] == "weak":
+        N = args.n or cfg["total"]
+        total = world * N
+        index_base, n_real = rank * N, N
+    else:
+        total = args.n or cfg["total"]
+        lo, hi = shard_bounds(total, world, rank)
+        N = -(-total // world)
+        index_base, n_real = lo, hi - lo
+
+    setup = {}
+    t0 = time.perf_counter()
+    pk, sk = generate_paillier_keypair(nb, seed=1)
+    setup["keygen_s"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    ctx = _native.Context(pk.n, local_rank)
+    ctx.set_private(sk.p, sk.q)
+    setup["context_and_private_key_ms"] = (time.perf_counter() - t0) * 1e3
     use_crt = args.path == "crt" and ctx.crt_available
     ctx.set_crt(use_crt)
     use_fb = use_crt and args.obf == "fixedbase"
     ctx.set_fixed_base(use_fb)
-    use_fb = use_fb and ctx.fixed_base
+    fb_info = None
     if use_fb:
-        ctx.set_fb_window(args.fb_window)     # a dedicated encrypt GPU: 2 x 17.5 GB of tables at W = 20
-    fb_info = ctx.fixed_base_info() if use_fb else None
+        ctx.set_fb_window(args.fb_window)     # a dedicated encrypt GPU: 2 x 13.4 GB of tables at W = 20
+        t0 = time.perf_counter()
+        try:
+            ctx.prepare_fixed_base()
+        except _native.NativeError as exc:
+            setup["fixed_base_unavailable"] = str(exc)
+        setup["fixed_base_build_wall_ms"] = (time.perf_counter() - t0) * 1e3
+        use_fb = ctx.fb_ready
+        if use_fb:
+            fb_info = ctx.fixed_base_info()
+            h_ms, d_ms, tbytes = ctx.fixed_base_setup()
+            setup.update({"fixed_base_host_ms": h_ms, "fixed_base_device_ms": d_ms, "fixed_base_table_bytes": tbytes,
+                          "fixed_base_note": "once per key: bases + B_k on the host, hipMalloc, k_fb_lohi + k_fb_fill; "
+                                             "outside the timed region (the tables stay resident)"})
     ctx.set_stage_timing(True)
     lib = _native.load_library()
-    N, W = args.n, ctx.ct_words
-    x_host = np.random.default_rng(rank).standard_normal(N, dtype=np.float32)
-    x = torch.from_numpy(x_host).to(dev)
-    ct = torch.empty((N, W), dtype=torch.int32, device=dev)
-    ex = torch.empty(N, dtype=torch.int32, device=dev)
-    st = torch.empty(N, dtype=torch.int32, device=dev)
-    rng_key = hashlib.sha256(b"flexpai-bench-key").digest()
-    total = world * N                 # weak scaling: N elements per GPU
-    index_base, _ = shard_bounds(total, world, rank)   # obfuscators keyed by the GLOBAL element index
+    W = ctx.ct_words
     stream = torch.cuda.current_stream(dev)
 
-    def encrypt(out, exo=ex):
-        rc = lib.pai_encrypt_dev(ctx.handle, _native.PAI_F32, x.data_ptr(), N, 0, 0, _native.PAI_OBF_RNG,
-                                 None, 0, 0, rng_key, index_base, out.data_ptr(), exo.data_ptr(), st.data_ptr(),
+    # obfuscator key: fresh per run, shared by the ranks (a secret in production: INTEGRATION.md)
+    if args.deterministic:
+        rng_key = hashlib.sha256(b"flexpai-bench-key").digest()
+    else:
+        kt = torch.tensor(list(os.urandom(32)), dtype=torch.uint8, device=dev)
+        if world > 1:
+            dist.broadcast(kt, src=0)
+        rng_key = bytes(kt.cpu().tolist())
+
+    x_host = np.random.default_rng(rank).standard_normal(N, dtype=np.float32)
+    x = torch.from_numpy(x_host).to(dev)
+    st = torch.empty(N, dtype=torch.int32, device=dev)
+
+    def encrypt(xd, out, exo, base, n=N):
+        rc = lib.pai_encrypt_dev(ctx.handle, _native.PAI_F32, xd.data_ptr(), n, 0, 0, _native.PAI_OBF_RNG,
+                                 None, 0, 0, rng_key, base, out.data_ptr(), exo.data_ptr(), st.data_ptr(),
                                  stream.cuda_stream)
         if rc != 0:
             raise RuntimeError(lib.pai_last_error().decode())
 
-    # N > 1: double-buffered shards; step i's RCCL all-gather (ciphertexts + exponents) runs on the process
-    # group's stream while step i+1 encrypts on the compute stream
-    bufs = [(ct, ex)] + ([(torch.empty_like(ct), torch.empty_like(ex))] if world > 1 else [])
-    works = [[] for _ in bufs]
+    def decrypt(ct, ex, val, stt, n=N):
+        rc = lib.pai_decrypt_dev(ctx.handle, ct.data_ptr(), ex.data_ptr(), n, val.data_ptr(), None,
+                                 stt.data_ptr(), None, stream.cuda_stream)
+        if rc != 0:
+            raise RuntimeError(lib.pai_last_error().decode())
 
-    def step(i):
-        b = i % len(bufs)
-        for w in works[b]:
-            w.wait()                   # the gather that last read this buffer is done
-        works[b] = []
-        encrypt(*bufs[b])
-        if world > 1:
-            for t in bufs[b]:
-                _, w = gather_shards_async(t, total, world)
-                if w is not None:
-                    works[b].append(w)
+    def add_k(cts, exs, k, out, oe):
+        rc = lib.pai_add_dev(ctx.handle, cts.data_ptr(), exs.data_ptr(), k, N, out.data_ptr(), oe.data_ptr(),
+                             stream.cuda_stream)
+        if rc != 0:
+            raise RuntimeError(lib.pai_last_error().decode())
 
-    def drain():
-        for b in range(len(bufs)):
+    extra = {}
+    K8 = 8
+    add_events = []
+    if cfg_id == 2:
+        # ---- a step = the configs[2] pipeline: encrypt 8 arrays, one 8-way add, decrypt the sum
+        xs8 = torch.stack([torch.from_numpy(np.random.default_rng(k).standard_normal(N, dtype=np.float32))
+                           for k in range(K8)]).to(dev)
+        cts8 = torch.empty((K8, N, W), dtype=torch.int32, device=dev)
+        exs8 = torch.empty((K8, N), dtype=torch.int32, device=dev)
+        sum_ct = torch.empty((N, W), dtype=torch.int32, device=dev)
+        sum_ex = torch.empty(N, dtype=torch.int32, device=dev)
+        val8 = torch.empty(N, dtype=torch.float64, device=dev)
+        st8 = torch.empty(N, dtype=torch.int32, device=dev)
+
+        def step(i):
+            for k in range(K8):
+                encrypt(xs8[k], cts8[k], exs8[k], index_base + (k + 1) * total)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            add_k(cts8, exs8, K8, sum_ct, sum_ex)
+            e1.record(stream)
+            add_events.append((e0, e1))
+            decrypt(sum_ct, sum_ex, val8, st8)
+
+        def drain():
+            pass
+    else:
+        ct = torch.empty((N, W), dtype=torch.int32, device=dev)
+        ex = torch.empty(N, dtype=torch.int32, device=dev)
+        # N > 1: double-buffered shards and gathered outputs; step i's RCCL all-gather (ciphertexts +
+        # exponents) runs on the process group's stream while step i+1 encrypts
+        bufs = [(ct, ex)] + ([(torch.empty_like(ct), torch.empty_like(ex))] if world > 1 else [])
+        gath = [(torch.empty((world * N, W), dtype=torch.int32, device=dev),
+                 torch.empty(world * N, dtype=torch.int32, device=dev)) for _ in bufs] if world > 1 else []
+        works = [[] for _ in bufs]
+
+        def step(i):
+            b = i % len(bufs)
             for w in works[b]:
-                w.wait()
+                w.wait()                   # the gather that last read this buffer is done
             works[b] = []
+            encrypt(x, bufs[b][0], bufs[b][1], index_base)
+            if world > 1:
+                for t, o in zip(bufs[b], gath[b]):
+                    _, w = gather_shards_async(t, world * N, world, out=o)
+                    if w is not None:
+                        works[b].append(w)
+
+        def drain():
+            for b in range(len(bufs)):
+                for w in works[b]:
+                    w.wait()
+                works[b] = []
 
     for i in range(args.warmup):
         step(i)
@@ -201,11 +314,13 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    add_events.clear()
     stage_ms = []
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
-        stage_ms.append(ctx.stage_times())     # HIP events recorded between this call's kernels
+        if cfg_id != 2:
+            stage_ms.append(ctx.stage_times())   # HIP events recorded between this encrypt call's kernels
     drain()
     torch.cuda.synchronize()
     if world > 1:
@@ -216,86 +331,105 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    ct, ex = bufs[(args.steps - 1) % len(bufs)]   # the last timed step's output (checked below)
-    stage_avg = [float(np.mean([s[i] for s in stage_ms])) for i in range(len(stage_ms[0]))]
-    S_chk = min(N, args.cpu_sample)
-    ct_timed_check = ct[:S_chk].cpu().numpy().view(np.uint32).copy()
-    ex_timed_check = ex[:S_chk].cpu().numpy().copy()
+    units = (total if cfg["shard"] == "strong" else world * N) * args.steps
+    value = units / elapsed
 
-    extra = {}
-    # Fixed-base sampling (kernels_fb.hpp) draws r^n directly, so its ciphertexts are not the ones of
-    # the ChaCha r stream; the generic CRT path on the same input (untimed) is the bit-reproducible
-    # reference the public-key kernel and the GMP CPU baseline are compared with.
-    ct_ref = ct
-    if use_fb:
-        ct_ref = torch.empty_like(ct)
-        ctx.set_fixed_base(False)
-        encrypt(ct_ref)
-        encrypt(ct_ref)
-        gen_ms = ctx.stage_times()
-        ctx.set_fixed_base(True)
-        torch.cuda.synchronize()
-        wc = work_crt(args.nb)
-        extra["generic_crt_path"] = {
-            "value": N / (sum(gen_ms) * 1e-3), "unit": "encrypts/s per GPU",
-            "note": "r from the ChaCha20 stream and r^n by CRT exponentiation (kernels_crt.hpp); "
-                    "bit-identical to the public-key kernel and the GMP baseline",
-            "stages_ms": dict(zip(["k_crt_a", "k_crt_b", "k_crt_fin"], gen_ms)),
-            "k_crt_b_int_mac_frac": N * wc["k_crt_b"] / (gen_ms[1] * 1e-3) / INT_MAC_PEAK if len(gen_ms) > 1 else None}
-    ct_host_check = ct_ref[:S_chk].cpu().numpy().view(np.uint32).copy()
-    ex_host_check = ex[:S_chk].cpu().numpy().copy()
+    if cfg_id == 2:
+        ref = xs8.double().sum(0)
+        err = float((val8 - ref).abs().max().item())
+        ok8 = bool(torch.all((val8 - ref).abs() <= torch.finfo(torch.float64).eps * ref.abs()).item()) and \
+            int((st8 > 1).sum().item()) == 0
+        extra["config2_check"] = {"max_abs_err_vs_float64_sum": err, "within_1ulp": ok8}
+        if not ok8:
+            raise SystemExit("configs[2]: decrypted sums differ from the float64 sums")
+        ct, ex = cts8[0], exs8[0]
+        x_host = xs8[0].cpu().numpy()
+        x = xs8[0]
+        index_base_chk = index_base + total
+    else:
+        index_base_chk = index_base
+        ct, ex = bufs[(args.steps - 1) % len(bufs)]   # the last timed step's output (checked below)
+        if world > 1:
+            # the gathered array holds every rank's shard; this rank's block equals its own output
+            go, ge = gath[(args.steps - 1) % len(gath)]
+            same = bool(torch.equal(go[rank * N:(rank + 1) * N], ct)) and bool(torch.equal(ge[rank * N:(rank + 1) * N], ex))
+            extra["allgather_own_shard_identical"] = same
+            if not same:
+                raise SystemExit("all-gathered shard differs from the local one")
+    stage_avg = [float(np.mean([s[i] for s in stage_ms])) for i in range(len(stage_ms[0]))] if stage_ms else []
 
-    # the public-key path on the same input (untimed region), for the record and as a parity check
-    if use_crt and not args.no_public:
-        ct2 = torch.empty_like(ct)
-        ctx.set_crt(False)
-        encrypt(ct2)
-        pub_ms = ctx.stage_times()[0]
-        ctx.set_crt(True)
-        torch.cuda.synchronize()
-        same = bool(torch.equal(ct2, ct_ref))
-        extra["public_key_path"] = {"value": N / (pub_ms * 1e-3), "unit": "encrypts/s per GPU",
-                                    "kernel": "k_encrypt", "kernel_ms": pub_ms,
-                                    "int_mac_frac": N * work_enc_public(args.nb) / (pub_ms * 1e-3) / INT_MAC_PEAK,
-                                    "bit_identical_to_crt": same}
-        del ct2
-        if not same:
-            raise SystemExit("CRT and public-key ciphertexts differ")
-
-    # correctness of the timed output: decrypt on the device and compare with the input exactly
-    if not args.no_decrypt:
+    # ---- correctness of the timed output: decrypt on the device, compare with the input exactly
+    if not args.no_decrypt and cfg_id != 2:
         val = torch.empty(N, dtype=torch.float64, device=dev)
         stt = torch.empty(N, dtype=torch.int32, device=dev)
         d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         d0.record(stream)
-        rc = lib.pai_decrypt_dev(ctx.handle, ct.data_ptr(), ex.data_ptr(), N, val.data_ptr(), None,
-                                 stt.data_ptr(), None, stream.cuda_stream)
+        decrypt(ct, ex, val, stt)
         d1.record(stream)
-        if rc != 0:
-            raise RuntimeError(lib.pai_last_error().decode())
         torch.cuda.synchronize()
         dec_ms = d0.elapsed_time(d1)
         dst = ctx.stage_times()
         if ctx.lane_decrypt and len(dst) == 3:
-            wd = work_dec(args.nb)
+            wd = work_dec(nb)
             extra["decrypt_stages"] = {
                 "k_dec_pre": {"kernel_ms": dst[0]},
                 "k_dec_pow": {"kernel_ms": dst[1], "work_mac_per_elem": wd,
                               "achieved_tmac_s": N * wd / (dst[1] * 1e-3) / 1e12},
                 "k_dec_fin": {"kernel_ms": dst[2]}}
         extra["decrypt_path"] = "lane" if ctx.lane_decrypt else "group"
-        ok = bool(torch.equal(val, x.double())) and int((stt > 1).sum().item()) == 0
+        ok = bool(torch.equal(val[:n_real], x[:n_real].double())) and int((stt[:n_real] > 1).sum().item()) == 0
         extra["decrypt_per_s_per_gpu"] = N / (dec_ms * 1e-3)
         extra["decrypt_kernel_ms"] = dec_ms
-        extra["decrypt_int_mac_frac"] = N * work_dec(args.nb) / (dec_ms * 1e-3) / INT_MAC_PEAK
+        extra["decrypt_int_mac_frac"] = N * work_dec(nb) / (dec_ms * 1e-3) / INT_MAC_PEAK
         extra["roundtrip_exact"] = ok
         if not ok:
             raise SystemExit("decrypt(encrypt(x)) != x on the device")
 
-    # configs[2]: encrypt 8 arrays (default_rng(k), k = 0..7), one 8-way homomorphic add (k_add), decrypt the
-    # sum; device-resident, HIP events on the launch stream; the decrypted sum is checked against float64
-    if not args.no_add8 and not args.no_decrypt:
-        K8 = 8
+    solo = world == 1 and rank == 0        # single-GPU legs beside the timed path
+    # ---- the generic CRT path on the same input (untimed): bit-reproducible against GMP
+    ct_ref = ct
+    if use_fb and solo:
+        ct_ref = torch.empty_like(ct)
+        ex_ref = torch.empty_like(ex)
+        ctx.set_fixed_base(False)
+        encrypt(x, ct_ref, ex_ref, index_base_chk)
+        encrypt(x, ct_ref, ex_ref, index_base_chk)
+        gen_ms = ctx.stage_times()
+        ctx.set_fixed_base(True)
+        torch.cuda.synchronize()
+        wc = work_crt(nb)
+        extra["generic_crt_path"] = {
+            "value": N / (sum(gen_ms) * 1e-3), "unit": "encrypts/s per GPU",
+            "note": "r from the ChaCha20 stream and r^n by CRT exponentiation (kernels_crt.hpp); "
+                    "bit-identical to the public-key kernel and the GMP baseline",
+            "stages_ms": dict(zip(["k_crt_a", "k_crt_b", "k_crt_fin"], gen_ms)),
+            "k_crt_b_int_mac_frac": N * wc["k_crt_b"] / (gen_ms[1] * 1e-3) / INT_MAC_PEAK if len(gen_ms) > 1 else None}
+    S_chk = min(N, args.cpu_sample)
+    ct_host_check = ct_ref[:S_chk].cpu().numpy().view(np.uint32).copy()
+    ex_host_check = ex[:S_chk].cpu().numpy().copy()
+    ct_timed_check = ct[:S_chk].cpu().numpy().view(np.uint32).copy()
+
+    # ---- the public-key path on the same input (untimed region), for the record and as a parity check
+    if use_crt and not args.no_public and solo:
+        ct2 = torch.empty_like(ct)
+        ex2 = torch.empty_like(ex)
+        npub = min(N, 1 << 16) if nb > 2048 else N
+        ctx.set_crt(False)
+        encrypt(x, ct2, ex2, index_base_chk, npub)
+        pub_ms = ctx.stage_times()[0]
+        ctx.set_crt(True)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(ct2[:npub], ct_ref[:npub]))
+        extra["public_key_path"] = {"value": npub / (pub_ms * 1e-3), "unit": "encrypts/s per GPU", "elements": npub,
+                                    "kernel": "k_encrypt", "kernel_ms": pub_ms,
+                                    "int_mac_frac": npub * work_enc_public(nb) / (pub_ms * 1e-3) / INT_MAC_PEAK,
+                                    "bit_identical_to_crt": same}
+        del ct2, ex2
+        if not same:
+            raise SystemExit("CRT and public-key ciphertexts differ")
+
+    # ---- configs[2] beside configs[1]: encrypt 8 arrays, one 8-way add (k_add), decrypt the sum
+    if cfg_id == 1 and solo and not args.no_add8 and not args.no_decrypt:
         xs8 = torch.stack([torch.from_numpy(np.random.default_rng(k).standard_normal(N, dtype=np.float32))
                            for k in range(K8)]).to(dev)
         cts8 = torch.empty((K8, N, W), dtype=torch.int32, device=dev)
@@ -309,51 +443,42 @@ def main():
         t8 = time.perf_counter()
         ev[0].record(stream)
         for k in range(K8):
-            rc = lib.pai_encrypt_dev(ctx.handle, _native.PAI_F32, xs8[k].data_ptr(), N, 0, 0, _native.PAI_OBF_RNG,
-                                     None, 0, 0, rng_key, index_base + (k + 1) * total, cts8[k].data_ptr(),
-                                     exs8[k].data_ptr(), st.data_ptr(), stream.cuda_stream)
-            if rc != 0:
-                raise RuntimeError(lib.pai_last_error().decode())
+            encrypt(xs8[k], cts8[k], exs8[k], index_base + (k + 1) * total)
         ev[1].record(stream)
-        rc = lib.pai_add_dev(ctx.handle, cts8.data_ptr(), exs8.data_ptr(), K8, N, sum_ct.data_ptr(),
-                             sum_ex.data_ptr(), stream.cuda_stream)
-        if rc != 0:
-            raise RuntimeError(lib.pai_last_error().decode())
+        add_k(cts8, exs8, K8, sum_ct, sum_ex)
         ev[2].record(stream)
-        rc = lib.pai_decrypt_dev(ctx.handle, sum_ct.data_ptr(), sum_ex.data_ptr(), N, val8.data_ptr(), None,
-                                 st8.data_ptr(), None, stream.cuda_stream)
-        if rc != 0:
-            raise RuntimeError(lib.pai_last_error().decode())
+        decrypt(sum_ct, sum_ex, val8, st8)
         ev[3].record(stream)
         torch.cuda.synchronize()
         wall8 = time.perf_counter() - t8
         ref = xs8.double().sum(0)
         err = float((val8 - ref).abs().max().item())
         add_ms = ev[1].elapsed_time(ev[2])
-        # canonical add work: (k-1) products + 4 d squarings per operand aligned by d
-        E = exs8.max(0).values
-        sq = int((4 * (E.unsqueeze(0) - exs8)).sum().item())
-        add_work = (N * (K8 - 1) + sq) * _M(args.nb // 16)
-        extra["config3_add8"] = {
+        E, emin = exs8.max(0).values, exs8.min(0).values
+        extra["config2_add8"] = {
             "workload": "configs[2]: encrypt 8 x 1M float32 arrays, one 8-way add, decrypt the sum (device-resident)",
             "elements_per_s": N / wall8, "wall_s": wall8,
             "encrypt8_ms": ev[0].elapsed_time(ev[1]), "k_add_ms": add_ms, "decrypt_ms": ev[2].elapsed_time(ev[3]),
-            "k_add_int_mac_frac": add_work / (add_ms * 1e-3) / INT_MAC_PEAK,
-            "k_add_alignment_squarings_per_elem": sq / N,
+            "k_add_int_mac_frac": work_add(exs8, nb) / (add_ms * 1e-3) / INT_MAC_PEAK,
+            "k_add_note": "canonical W_add of SURVEY.md §8d (per-operand alignment squarings); k_add evaluates the "
+                          "same product by Horner over exponent levels (squarings of the running product); "
+                          "k_add_ms includes the schedule sort (k_add_plan/scan/scatter)",
+            "canonical_alignment_squarings_per_elem": int((4 * (E.unsqueeze(0) - exs8)).sum().item()) / N,
+            "horner_squarings_per_elem": int((4 * (E - emin)).sum().item()) / N,
             "max_abs_err_vs_float64_sum": err, "statuses_ok": int((st8 > 1).sum().item()) == 0}
         del xs8, cts8, exs8, sum_ct, sum_ex, val8, st8
         torch.cuda.empty_cache()
 
-    # host boundary (DESIGN.md §Host boundary): plaintexts start in host numpy and ciphertexts leave as
-    # host buffers / PaillierEncryptedNumber objects; never part of `value`
-    if not args.no_host and rank == 0:
+    # ---- host boundary: plaintexts start in host numpy, ciphertexts leave as host buffers /
+    # PaillierEncryptedNumber objects; never part of `value`
+    if not args.no_host and solo and cfg_id in (1, 3):
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         hct, hex_, _ = ctx.encrypt(x_host, obf_mode=_native.PAI_OBF_RNG, rng_key=rng_key, index_base=index_base)
         t_host = time.perf_counter() - t1
         hb = {"host_buffers_encrypts_per_s": N / t_host,
               "host_buffers_note": "pai_encrypt: H2D float32 x, kernels, D2H ciphertext words "
-                                   f"({N * W * 4 / 2**20:.0f} MiB), pageable host memory",
+                                   f"({N * W * 4 / 2**20:.0f} MiB) into caller (pageable) memory",
               "host_buffers_bit_identical": bool(np.array_equal(hct[: len(ct_timed_check)], ct_timed_check))}
         from flex.crypto.paillier import _runtime
         from flex.crypto.paillier.encryptor import PaillierEncryptor
@@ -374,49 +499,58 @@ def main():
             dist.destroy_process_group()
         return
 
-    value = world * N * args.steps / elapsed
-    if use_crt:
-        if use_fb:
-            names = ["k_fb_digits", "k_fb", "k_fb_fin"]
-            works = work_fb(args.nb, fb_info[2])
+    # ---- roofline of the dominant kernel of the timed path
+    alg_bytes = 4 + W * 4 + 4     # x in, ciphertext out, exponent out (r generated on the device)
+    if cfg_id == 2:
+        add_ms = float(np.mean([a.elapsed_time(b) for a, b in add_events]))
+        dom, dom_ms, dom_work = "k_add", add_ms, work_add(exs8, nb) / N
+        achieved = N * dom_work / (dom_ms * 1e-3)
+        extra["k_add_ms"] = add_ms
+    else:
+        if use_crt and use_fb:
+            names, works = ["k_fb_digits", "k_fb", "k_fb_fin"], work_fb(nb, fb_info[2])
+        elif use_crt:
+            names, works = ["k_crt_a", "k_crt_b", "k_crt_fin"], work_crt(nb)
         else:
-            names = ["k_crt_a", "k_crt_b", "k_crt_fin"]
-            works = work_crt(args.nb)
+            names, works = ["k_encrypt"], {"k_encrypt": work_enc_public(nb)}
         stages = {nm: {"kernel_ms": ms, "work_mac_per_elem": works[nm],
                        "achieved_tmac_s": N * works[nm] / (ms * 1e-3) / 1e12}
                   for nm, ms in zip(names, stage_avg)}
-        dom = max(names, key=lambda nm: stages[nm]["kernel_ms"])
+        dom = max(stages, key=lambda nm: stages[nm]["kernel_ms"])
         dom_ms, dom_work = stages[dom]["kernel_ms"], works[dom]
         extra["stages"] = stages
-        total_work = sum(works.values())
-    else:
-        dom, dom_ms, dom_work = "k_encrypt", stage_avg[0], work_enc_public(args.nb)
-        total_work = dom_work
-    achieved = N * dom_work / (dom_ms * 1e-3)
-    alg_bytes = 4 + W * 4 + 4     # x in, ciphertext out, exponent out (r generated on the device)
-    extra["path"] = ("crt-fixedbase" if use_fb else "crt") if use_crt else "public"
-    if use_fb:
-        extra["fixed_base"] = {"g_p": fb_info[0], "g_q": fb_info[1], "digits": fb_info[2],
-                               "window_bits": fb_info[3] if len(fb_info) > 3 else 8}
-    extra["encrypt_call_ms"] = float(sum(stage_avg))
-    extra["path_int_mac_frac"] = N * total_work / (sum(stage_avg) * 1e-3) / INT_MAC_PEAK
-    extra["hbm_algorithmic_gbs"] = N * alg_bytes / (sum(stage_avg) * 1e-3) / 1e9
+        achieved = N * dom_work / (dom_ms * 1e-3)
+        enc_ms = float(sum(stage_avg))
+        extra["path"] = ("crt-fixedbase" if use_fb else "crt") if use_crt else "public"
+        if use_fb:
+            extra["fixed_base"] = {"g_p": fb_info[0], "g_q": fb_info[1], "digits": fb_info[2], "window_bits": fb_info[3]}
+        extra["encrypt_call_ms"] = enc_ms
+        extra["path_int_mac_frac"] = N * sum(works.values()) / (enc_ms * 1e-3) / INT_MAC_PEAK
+        extra["hbm_algorithmic_gbs"] = N * alg_bytes / (enc_ms * 1e-3) / 1e9
+        # SURVEY.md §8d prices every encryption at the public-key work W_enc; the fraction it implies
+        extra["w_enc_equivalent"] = {
+            "frac_of_peak": (N / (enc_ms * 1e-3)) * work_enc_public(nb) / INT_MAC_PEAK,
+            "note": "encrypt rate x SURVEY.md §8d W_enc / peak: > 1 means the path does less work than the "
+                    "canonical public-key exponentiation, not a faster multiplier"}
 
     cpu = None
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:
         from oracle import gmp_oracle
         if gmp_oracle.available():
+            th = max(1, args.cpu_threads)
+            cores = {"os_cpu_count": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+                     "cpu_model": cpu_model()}
             S = min(args.cpu_sample, N)
-            th = max(1, min(args.cpu_threads, os.cpu_count() or 1))
             t1 = time.perf_counter()
-            cct, cex = gmp_oracle.encrypt_f32_chacha(pk.n, x_host[:S], rng_key, index_base, th)
+            cct, cex = gmp_oracle.encrypt_f32_chacha(pk.n, x_host[:S], rng_key, index_base_chk, th)
             cdt = time.perf_counter() - t1
             same = bool(np.array_equal(ct_host_check[:S], cct) and np.array_equal(ex_host_check[:S], cex))
             cpu = {"value": S / cdt, "unit": "encrypts/s", "cores": th, "kind": "port",
                    "sample": f"first {S} elements of the rank-0 vector with the same ChaCha20 obfuscators; "
                              f"GMP 6.2.1 mpz_powm(r, n, n^2) per element (the library gmpy2 2.0.8 wraps, "
                              f"obfuscator.py:36), {th} worker threads like the reference's Pool(cpu_count())",
-                   "gpu_bit_exact_on_sample": same}
+                   "extrapolated_full_job_s": N / (S / cdt),
+                   "gpu_bit_exact_on_sample": same, **cores}
             if not same:
                 raise SystemExit("GPU ciphertexts differ from the GMP oracle on the CPU sample")
             if use_fb:
@@ -425,40 +559,59 @@ def main():
                 okey = O.Key(pk.n, sk.p, sk.q)
                 idx = sorted({0, 1, S_chk // 2, S_chk - 1})
                 got = _native.words_to_ints(ct_timed_check[idx])
-                fb_ok = all(O.fb_encrypt_value(x_host[i], okey, rng_key, index_base + i, fb_info)
-                            == (got[j], int(ex_timed_check[i])) for j, i in enumerate(idx))
+                fb_ok = all(O.fb_encrypt_value(x_host[i], okey, rng_key, index_base_chk + i, fb_info)
+                            == (got[j], int(ex_host_check[i])) for j, i in enumerate(idx))
                 cpu["fixed_base_bit_exact_vs_oracle"] = {"elements": idx, "ok": fb_ok}
                 if not fb_ok:
                     raise SystemExit("fixed-base ciphertexts differ from the oracle restatement")
+            # configs[0] timed in full: nb = 1024, 1000 elements, encrypt + decrypt, threads = os.cpu_count()
+            pk0, sk0 = generate_paillier_keypair(1024, seed=1)
+            x0 = np.random.default_rng(0).standard_normal(1000, dtype=np.float32)
+            t1 = time.perf_counter()
+            c0, _ = gmp_oracle.encrypt_f32_chacha(pk0.n, x0, rng_key, 0, th)
+            t_e0 = time.perf_counter() - t1
+            t1 = time.perf_counter()
+            gmp_oracle.decrypt_raw(sk0.p, sk0.q, c0, th)
+            t_d0 = time.perf_counter() - t1
+            extra["config0_cpu"] = {"workload": CONFIGS[0]["desc"], "encrypt_per_s": 1000 / t_e0,
+                                    "decrypt_per_s": 1000 / t_d0, "encrypt_s": t_e0, "decrypt_s": t_d0,
+                                    "threads": th, **cores, "kind": "port (oracle/gmp_oracle.c)"}
 
+    metric = {1: "Paillier-2048 encrypts/sec (device-resident), 1M-elem float32 array",
+              2: "Paillier-2048 encrypt + 8-way add + decrypt, elements/sec (device-resident), 1M-elem arrays"}
     out = {
-        "metric": "Paillier-2048 encrypts/sec (device-resident), 1M-elem float32 array" if args.nb == 2048
-        else f"Paillier-{args.nb} encrypts/sec (device-resident)",
+        "metric": metric.get(cfg_id, f"Paillier-{nb} encrypts/sec (device-resident)") if nb == cfg["nb"]
+        else f"Paillier-{nb} encrypts/sec (device-resident)",
         "value": value,
-        "unit": "encrypts/s",
+        "unit": "encrypts/s" if cfg_id != 2 else "elements/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": cfg["shard"],
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic: numpy default_rng(rank).standard_normal float32; seeded key "
                 "generate_paillier_keypair(nb, seed=1); device ChaCha20 obfuscators keyed by global index",
-        "config": {"workload": f"Paillier n={args.nb} encrypt of a {N}-element float32 vector per GPU, "
-                               f"device-resident, key holder ({('CRT, fixed-base r^n sampler' if use_fb else 'CRT') if use_crt else 'public-key'} path)"
-                               + (", RCCL all-gather of ciphertext shards" if world > 1 else ""),
-                   "key_bits": args.nb, "elements_per_gpu": N, "parallelism": f"dp{world}"},
+        "config": {"workload": cfg["desc"] + " (" + ((("key holder: CRT, fixed-base r^n sampler" if use_fb else
+                                                      "key holder: CRT") if use_crt else "public-key") + " path"
+                                                    + (", RCCL all-gather of ciphertext shards in the step" if world > 1 else "") + ")"),
+                   "baseline_config": cfg_id, "key_bits": nb,
+                   "elements_total": total if cfg["shard"] == "strong" else world * N,
+                   "elements_per_gpu": N, "parallelism": f"dp{world}"},
         "roofline": {"bound": "valu-int-mac", "achieved": achieved / 1e12, "peak": INT_MAC_PEAK / 1e12,
                      "unit": "TMAC/s", "frac": achieved / INT_MAC_PEAK,
-                     "traffic": load_traffic(dom, N, args.nb),
+                     "traffic": load_traffic(dom, N, nb),
                      "kernel": dom, "kernel_ms": dom_ms,
-                     "work_per_unit": f"{dom_work:.4g} canonical 32x32->64 MAC per element (SURVEY.md §8d)"},
-        "roofline_hbm": {"bound": "hbm", "achieved": extra["hbm_algorithmic_gbs"], "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": extra["hbm_algorithmic_gbs"] / HBM_PEAK_GBS,
+                     "work_per_unit": (f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} table "
+                                       f"products per half, 32-bit limbs, kernels_fb.hpp), not SURVEY.md §8d's W_enc"
+                                       if dom == "k_fb" else f"{dom_work:.4g} canonical 32x32->64 MAC per element (SURVEY.md §8d)")},
+        "roofline_hbm": {"bound": "hbm", "achieved": extra.get("hbm_algorithmic_gbs"), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": (extra["hbm_algorithmic_gbs"] / HBM_PEAK_GBS) if "hbm_algorithmic_gbs" in extra else None,
                          "algorithmic_bytes_per_unit": alg_bytes},
         "cpu_baseline": cpu,
+        "setup": setup,
         "extra": extra,
     }
     print(json.dumps(out))

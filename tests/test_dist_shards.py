@@ -49,6 +49,14 @@ def _worker(rank, world, port, keyt, x, q):
         if work is not None:
             work.wait()
         assert torch.equal(full, full2)
+        # preallocated receive buffer reused across steps (bench.py double-buffers these)
+        per = -(-TOTAL // world)
+        buf = torch.zeros((world * per,) + tuple(local.shape[1:]), dtype=local.dtype)
+        for _ in range(2):
+            full3, work = gather_shards_async(local, TOTAL, world, out=buf)
+            if work is not None:
+                work.wait()
+            assert torch.equal(full, full3) and full3.data_ptr() == buf.data_ptr()
         if rank == 0:
             q.put(full.numpy().view(np.uint32).copy())
     finally:

@@ -15,6 +15,7 @@
 #include "engine_dec.hpp"
 #include "engine_lane.hpp"
 #include "engine_fb.hpp"
+#include "engine_grp.hpp"
 #include "engine_mul.hpp"
 
 using namespace fpai;
@@ -54,6 +55,7 @@ struct pai_ctx {
   int nwin = 0, n_limbs = 0;
   // CRT encryption (kernels_crt.hpp): available when the private key is set and the halves fit
   bool crt_ok = false;
+  bool fbg_ok = false;        // 4096-bit keys: fixed-base sampler on the group engine (engine_grp), no lane CRT
   bool crt_enabled = true;
   int crt_sa = 0, crt_sb = 0;
   CrtHalf* d_crt_a = nullptr;   // [2] stage A halves
@@ -444,7 +446,10 @@ static int fb_default_window() {
   return (w == 8 || w == 12 || w == 16 || w == 20) ? w : 16;
 }
 
-static int fb_row_words(int sb) { return sb == 37 ? FbGeom<37>::TW : sb == 74 ? FbGeom<74>::TW : 0; }
+// 32-bit words of one table row: packed words for the lane kernels, S canonical limbs for the group kernel
+static int fb_row_words(int sb) {
+  return sb == 37 ? FbGeom<37>::TW : sb == 74 ? FbGeom<74>::TW : sb == GRP_TPI * L ? GRP_TPI * L : 0;
+}
 
 static int fb_digit_count(const pai_ctx* c, int W) {
   const size_t kb = std::max(sub(c->fb_p, HBig(1)).bits(), sub(c->fb_q, HBig(1)).bits());
@@ -491,11 +496,12 @@ static int fb_unavailable(pai_ctx* c, const std::string& why) {
 static int ensure_fb(pai_ctx* c) {
   if (c->fb_state == pai_ctx::FB_READY) return 1;
   if (c->fb_state == pai_ctx::FB_UNAVAILABLE) return 0;
-  if (!c->crt_ok) return fb_unavailable(c, "needs the private key and the CRT kernels");
+  if (!c->crt_ok && !c->fbg_ok) return fb_unavailable(c, "needs the private key and the CRT kernels");
   const int sb = c->crt_sb, TW = fb_row_words(sb);
   if (!TW) return fb_unavailable(c, "key size not supported by the fixed-base kernels");
+  const bool grp = sb == GRP_TPI * L;   // group-engine rows (limbs), recombined by k_crt_fin
   const HBig sq[2] = {mul(c->fb_p, c->fb_p), mul(c->fb_q, c->fb_q)};
-  if (sq[0].bits() > (size_t)32 * TW || sq[1].bits() > (size_t)32 * TW || c->ct_words != 2 * TW)
+  if (!grp && (sq[0].bits() > (size_t)32 * TW || sq[1].bits() > (size_t)32 * TW || c->ct_words != 2 * TW))
     return fb_unavailable(c, "unbalanced primes: p^2 or q^2 exceeds the table row");
   if (!c->fb_W) c->fb_W = fb_default_window();
   const uint64_t budget = fb_budget(c);
@@ -530,14 +536,22 @@ static int ensure_fb(pai_ctx* c) {
       std::copy(v.begin(), v.end(), bl.begin() + (size_t)k * sb);
       for (int q = 0; q < W; ++q) x = M2.mul(x, x);
     }
-    // c0 folding: n 2^(CB c) mod p_h^2 (c < NC) and 2^PB p_h^2
-    const int CB = sb == 37 ? FbGeom<37>::CB : FbGeom<74>::CB, NC = sb == 37 ? FbGeom<37>::NC : FbGeom<74>::NC;
-    const int PB = sb == 37 ? FbGeom<37>::PB : FbGeom<74>::PB;
+    // c0 folding: n 2^(CB c) mod p_h^2 (c < NC) and 2^PB p_h^2; the group kernel instead finishes with
+    // the CRT coefficient (other^2)^-1 mod p_h^2 and leaves c0 to k_crt_fin
     std::vector<uint32_t> nm;
-    const HBig nmod = mod(c->n, m2);
-    for (int k = 0; k < NC; ++k) {
-      const std::vector<uint32_t> v = mul_pow2_mod(nmod, (size_t)CB * k, m2).limbs(sb, LB);
-      nm.insert(nm.end(), v.begin(), v.end());
+    int PB = 0;
+    if (grp) {
+      const HBig coef = inv_mod(sq[1 - h], m2);
+      if (coef.is_zero()) return fb_unavailable(c, "p^2, q^2 not coprime");
+      nm = coef.limbs(sb, LB);
+    } else {
+      const int CB = sb == 37 ? FbGeom<37>::CB : FbGeom<74>::CB, NC = sb == 37 ? FbGeom<37>::NC : FbGeom<74>::NC;
+      PB = sb == 37 ? FbGeom<37>::PB : FbGeom<74>::PB;
+      const HBig nmod = mod(c->n, m2);
+      for (int k = 0; k < NC; ++k) {
+        const std::vector<uint32_t> v = mul_pow2_mod(nmod, (size_t)CB * k, m2).limbs(sb, LB);
+        nm.insert(nm.end(), v.begin(), v.end());
+      }
     }
     uint32_t *dm, *dR2, *done, *dbases, *dlohi, *dnm, *dpbig;
     if ((rc = upload_fb(c, m2.limbs(sb, LB), &dm)) ||
@@ -574,8 +588,9 @@ static int ensure_fb(pai_ctx* c) {
       (rc = upload_fb(c, sq[1].limbs(sb, LB), &c->d_fb_q2)))
     return fb_unavailable(c, pai_last_error());
   const auto t1 = std::chrono::steady_clock::now();
-  if (fb_build_tables(sb, c->d_fb_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr) != hipSuccess ||
-      hipDeviceSynchronize() != hipSuccess)
+  const hipError_t be = grp ? grp_build_tables(c->d_fb_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
+                            : fb_build_tables(sb, c->d_fb_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
+  if (be != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return fb_unavailable(c, "table construction failed");
   const auto t2 = std::chrono::steady_clock::now();
   c->fb_host_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
@@ -588,9 +603,29 @@ static int ensure_fb(pai_ctx* c) {
   return 1;
 }
 
+// 4096-bit keys (p^2 of 148 limbs): no lane CRT; the fixed-base sampler runs on the group engine
+// (kernels_grp.hpp) and k_crt_fin<8> recombines, so only its constants are set up here. Without resident
+// tables, encryption takes the public-key path.
+static int setup_fbg(pai_ctx* c, const HBig& p, const HBig& q) {
+  constexpr int SBG = GRP_TPI * L;
+  const size_t pb = std::max(p.bits(), q.bits());
+  if ((size_t)LB * SBG < 2 * pb + 4 || c->tpi_e != 8) return 0;
+  const size_t RE = (size_t)LB * c->S_e;
+  int rc;
+  if ((rc = upload(c, mul_pow2_mod(mul(q, q), 2 * RE, c->N).limbs(c->S_e, LB), &c->d_kq)) ||
+      (rc = upload(c, mul_pow2_mod(mul(p, p), 2 * RE, c->N).limbs(c->S_e, LB), &c->d_kp)))
+    return rc;
+  c->crt_sa = 0;
+  c->crt_sb = SBG;
+  c->fb_p = p;
+  c->fb_q = q;
+  c->fbg_ok = true;
+  return 0;
+}
+
 // CRT encryption constants (kernels_crt.hpp). p < q here (sorted like keypair.py:57-62).
 static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
-  c->crt_ok = false;
+  c->crt_ok = c->fbg_ok = false;
   const size_t pb = std::max(p.bits(), q.bits());
   int sa = 0, sb = 0;
   for (auto cand : {std::pair<int, int>{19, 37}, std::pair<int, int>{37, 74}}) {
@@ -600,7 +635,7 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
       break;
     }
   }
-  if (!sa) return 0;   // key too large for the lane engine: public-key path only
+  if (!sa) return setup_fbg(c, p, q);   // too large for the lane engine: fixed-base on the group engine
   const size_t RA = (size_t)LB * sa, RB = (size_t)LB * sb, RE = (size_t)LB * c->S_e;
   const HBig primes[2] = {p, q};
   const HBig sq[2] = {mul(p, p), mul(q, q)};
@@ -714,7 +749,7 @@ int pai_ctx_set_private(pai_ctx* c, const uint8_t* p_le, const uint8_t* q_le, si
     for (void* a : c->priv_allocs) (void)hipFree(a);
     c->priv_allocs.clear();
     (void)hipGetLastError();
-    c->has_priv = c->crt_ok = c->dec_lane_ok = false;
+    c->has_priv = c->crt_ok = c->fbg_ok = c->dec_lane_ok = false;
     c->fb_state = pai_ctx::FB_UNTRIED;
     g_last_error = msg;
   }
@@ -804,7 +839,7 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
     case PAI_OPT_LANE_DECRYPT: *value = (c->dec_lane_ok && c->dec_lane_enabled) ? 1 : 0; return 0;
     // 1 when device-RNG encryption will use the fixed bases (tables resident, or not yet tried)
     case PAI_OPT_FIXED_BASE:
-      *value = (c->crt_ok && c->fb_enabled && c->fb_state != pai_ctx::FB_UNAVAILABLE) ? 1 : 0;
+      *value = ((c->crt_ok || c->fbg_ok) && c->fb_enabled && c->fb_state != pai_ctx::FB_UNAVAILABLE) ? 1 : 0;
       return 0;
     case PAI_OPT_FB_WINDOW: *value = c->fb_W_used ? c->fb_W_used : c->fb_W ? c->fb_W : fb_default_window(); return 0;
     case PAI_OPT_FB_READY: *value = c->fb_state == pai_ctx::FB_READY ? 1 : 0; return 0;
@@ -826,7 +861,8 @@ int pai_ctx_stage_times(pai_ctx* c, float* ms_out, int max_out, int* count) {
 
 int pai_ctx_fixed_base_info(pai_ctx* c, uint32_t* g_p, uint32_t* g_q, int* digits, int* window) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
-  if (!c->crt_ok) return fail(PAI_ERR_NOPRIV, "fixed-base obfuscation not available (needs the private key)");
+  if (!c->crt_ok && !c->fbg_ok)
+    return fail(PAI_ERR_NOPRIV, "fixed-base obfuscation not available (needs the private key)");
   HIPCHK(hipSetDevice(c->device));
   if (!ensure_fb((pai_ctx*)c)) return fail(PAI_ERR_KEY, "fixed-base obfuscation not available: " + c->fb_reason);
   if (g_p) *g_p = c->fb_g[0];
@@ -838,7 +874,8 @@ int pai_ctx_fixed_base_info(pai_ctx* c, uint32_t* g_p, uint32_t* g_q, int* digit
 
 int pai_ctx_fixed_base_prepare(pai_ctx* c) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
-  if (!c->crt_ok) return fail(PAI_ERR_NOPRIV, "fixed-base obfuscation not available (needs the private key)");
+  if (!c->crt_ok && !c->fbg_ok)
+    return fail(PAI_ERR_NOPRIV, "fixed-base obfuscation not available (needs the private key)");
   HIPCHK(hipSetDevice(c->device));
   if (!ensure_fb(c)) return fail(PAI_ERR_KEY, "fixed-base obfuscation not available: " + c->fb_reason);
   return 0;
@@ -897,11 +934,15 @@ static int launch_crt_fin(pai_ctx* c, CrtFinParams& f, hipStream_t st) {
 // table products with c0 folded in, Garner recombination into the ciphertext words.
 static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
   const int SB = c->crt_sb;
+  const bool grp = SB == GRP_TPI * L;
   const long long N = e.n;
   const long long chunk = std::min(N, CRT_CHUNK);
   int occF = 1, occG = 1;
-  if (fb_occupancy(SB, &occF, &occG)) return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
-  const long long lane_blocks = (chunk + LANE_BLOCK - 1) / LANE_BLOCK;
+  if (grp) grp_occupancy(&occF);
+  else if (fb_occupancy(SB, &occF, &occG)) return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
+  // elements per block: one per lane, or one per lane group (grp)
+  const int EPB = grp ? BLOCK / GRP_TPI : LANE_BLOCK;
+  const long long lane_blocks = (chunk + EPB - 1) / EPB;
   const int gxF = (int)std::max<long long>(1, std::min<long long>(lane_blocks, (long long)occF * c->cus / 2));
   const int gxG = (int)std::max<long long>(1, std::min<long long>(lane_blocks, (long long)occG * c->cus));
   const size_t dbytes = (size_t)2 * c->fb_K * 4, wbytes = (size_t)2 * SB * 4;   // per element
@@ -938,10 +979,33 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     pf.fexp = e.fexp;
     pf.exp = e.exp + off;
     pf.status = e.status ? e.status + off : nullptr;
-    HIPCHK(fb_launch(SB, pf, (int)std::min<long long>(gxF, (n + LANE_BLOCK - 1) / LANE_BLOCK), st));
+    const int gF = (int)std::min<long long>(gxF, (n + EPB - 1) / EPB);
+    HIPCHK(grp ? grp_launch_fb(pf, gF, st) : fb_launch(SB, pf, gF, st));
     stage_mark(c, 2, st);
     c->fb_last_w = w;
     c->fb_last_n = n;
+    if (grp) {   // u_h = G_h^(a_h) coef_h mod p_h^2 -> c = (u_p q^2 + u_q p^2) c0 mod n^2 (kernels_crt.hpp)
+      CrtFinParams f{};
+      f.x = pf.x;
+      f.dtype = e.dtype;
+      f.exp_mode = e.exp_mode;
+      f.fexp = e.fexp;
+      f.u = w;
+      f.sb = SB;
+      f.n = n;
+      f.N = c->d_N;
+      f.nl = c->d_nl;
+      f.kq = c->d_kq;
+      f.kp = c->d_kp;
+      f.mprime = c->mprime_N;
+      f.ct = e.ct + (size_t)off * c->ct_words;
+      f.exp = pf.exp;
+      f.status = pf.status;
+      f.ct_words = c->ct_words;
+      if ((rc = launch_crt_fin<8>(c, f, st))) return rc;
+      stage_mark(c, 3, st);
+      continue;
+    }
     FbFinParams pg{};
     pg.w = w;
     pg.n = n;
@@ -1075,6 +1139,8 @@ int pai_encrypt_dev(pai_ctx* c, int dtype, const void* d_x, size_t N, int exp_mo
   p.nprog = c->nprog;
   p.ct_words = c->ct_words;
   hipStream_t st = (hipStream_t)stream;
+  if (obf_mode == PAI_OBF_RNG && c->fbg_ok && c->crt_enabled && c->fb_enabled && ensure_fb(c))
+    return launch_fb(c, p, st);
   if (obf_mode != PAI_OBF_NONE && c->crt_ok && c->crt_enabled) {
     if (c->crt_sa == 19) return launch_crt<19, 37>(c, p, st);
     if (c->crt_sa == 37) return launch_crt<37, 74>(c, p, st);

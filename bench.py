@@ -95,6 +95,14 @@ def work_fb(nb: int, digits: int) -> dict:
     return {"k_fb_digits": 0.0, "k_fb": float(2 * digits * _M(s)), "k_fb_fin": float(_M(s) + s * s)}
 
 
+def work_fbg(nb: int, digits: int) -> dict:
+    """Per-element MACs of the 4096-bit key holder's fixed-base path (kernels_grp.hpp), counted like work_fb:
+    k_fbg = K table products mod p_h^2 per half plus the coefficient product; k_crt_fin<8> = three products
+    mod n^2 (u_p q^2, u_q p^2, times c0)."""
+    s = nb // 32
+    return {"k_fb_digits": 0.0, "k_fbg": float(2 * (digits + 1) * _M(s)), "k_crt_fin": float(3 * _M(nb // 16))}
+
+
 def work_dec(nb: int) -> float:
     return float(2 * (_P(nb // 2) + 2) * _M(nb // 32))
 
@@ -196,10 +204,14 @@ def main():
     ctx = _native.Context(pk.n, local_rank)
     ctx.set_private(sk.p, sk.q)
     setup["context_and_private_key_ms"] = (time.perf_counter() - t0) * 1e3
-    use_crt = args.path == "crt" and ctx.crt_available
-    ctx.set_crt(use_crt)
-    use_fb = use_crt and args.obf == "fixedbase"
+    # key holder ("crt"): lane CRT kernels for nb <= 2048; at nb = 4096 only the fixed-base sampler exists
+    # (group engine, kernels_grp.hpp) and anything else runs the public-key kernel
+    holder = args.path == "crt"
+    use_crt = holder and ctx.crt_available
+    ctx.set_crt(holder)
+    use_fb = holder and args.obf == "fixedbase" and ctx.fixed_base
     ctx.set_fixed_base(use_fb)
+    grp_fb = use_fb and not use_crt          # 4096-bit keys: k_fb_digits, k_fbg, k_crt_fin<8>
     fb_info = None
     if use_fb:
         ctx.set_fb_window(args.fb_window)     # a dedicated encrypt GPU: 2 x 13.4 GB of tables at W = 20
@@ -386,40 +398,51 @@ def main():
             raise SystemExit("decrypt(encrypt(x)) != x on the device")
 
     solo = world == 1 and rank == 0        # single-GPU legs beside the timed path
+    cpu_sample = args.cpu_sample if nb <= 2048 else min(args.cpu_sample, 4096)   # bounded CPU work at nb = 4096
+    S_chk = min(N, cpu_sample)
     # ---- the generic CRT path on the same input (untimed): bit-reproducible against GMP
     ct_ref = ct
     if use_fb and solo:
         ct_ref = torch.empty_like(ct)
         ex_ref = torch.empty_like(ex)
         ctx.set_fixed_base(False)
-        encrypt(x, ct_ref, ex_ref, index_base_chk)
-        encrypt(x, ct_ref, ex_ref, index_base_chk)
+        n_gen = N if use_crt else S_chk        # 4096: the public-key kernel, on the CPU-checked prefix only
+        encrypt(x, ct_ref, ex_ref, index_base_chk, n_gen)
+        encrypt(x, ct_ref, ex_ref, index_base_chk, n_gen)
         gen_ms = ctx.stage_times()
         ctx.set_fixed_base(True)
         torch.cuda.synchronize()
-        wc = work_crt(nb)
-        extra["generic_crt_path"] = {
-            "value": N / (sum(gen_ms) * 1e-3), "unit": "encrypts/s per GPU",
-            "note": "r from the ChaCha20 stream and r^n by CRT exponentiation (kernels_crt.hpp); "
-                    "bit-identical to the public-key kernel and the GMP baseline",
-            "stages_ms": dict(zip(["k_crt_a", "k_crt_b", "k_crt_fin"], gen_ms)),
-            "k_crt_b_int_mac_frac": N * wc["k_crt_b"] / (gen_ms[1] * 1e-3) / INT_MAC_PEAK if len(gen_ms) > 1 else None}
-    S_chk = min(N, args.cpu_sample)
+        if use_crt:
+            wc = work_crt(nb)
+            extra["generic_crt_path"] = {
+                "value": N / (sum(gen_ms) * 1e-3), "unit": "encrypts/s per GPU",
+                "note": "r from the ChaCha20 stream and r^n by CRT exponentiation (kernels_crt.hpp); "
+                        "bit-identical to the public-key kernel and the GMP baseline",
+                "stages_ms": dict(zip(["k_crt_a", "k_crt_b", "k_crt_fin"], gen_ms)),
+                "k_crt_b_int_mac_frac": N * wc["k_crt_b"] / (gen_ms[1] * 1e-3) / INT_MAC_PEAK if len(gen_ms) > 1 else None}
+        else:
+            extra["generic_path"] = {
+                "value": n_gen / (sum(gen_ms) * 1e-3), "unit": "encrypts/s per GPU", "elements": n_gen,
+                "note": "no lane CRT at nb = 4096: r from the ChaCha20 stream, r^n mod n^2 by the public-key "
+                        "kernel k_encrypt<8>; bit-identical to the GMP baseline"}
     ct_host_check = ct_ref[:S_chk].cpu().numpy().view(np.uint32).copy()
     ex_host_check = ex[:S_chk].cpu().numpy().copy()
     ct_timed_check = ct[:S_chk].cpu().numpy().view(np.uint32).copy()
 
     # ---- the public-key path on the same input (untimed region), for the record and as a parity check
-    if use_crt and not args.no_public and solo:
+    if holder and (use_crt or use_fb) and not args.no_public and solo:
         ct2 = torch.empty_like(ct)
         ex2 = torch.empty_like(ex)
         npub = min(N, 1 << 16) if nb > 2048 else N
         ctx.set_crt(False)
+        ctx.set_fixed_base(False)
         encrypt(x, ct2, ex2, index_base_chk, npub)
         pub_ms = ctx.stage_times()[0]
         ctx.set_crt(True)
+        ctx.set_fixed_base(use_fb)
         torch.cuda.synchronize()
-        same = bool(torch.equal(ct2[:npub], ct_ref[:npub]))
+        ncmp = npub if use_crt else min(npub, S_chk)
+        same = bool(torch.equal(ct2[:ncmp], ct_ref[:ncmp]))
         extra["public_key_path"] = {"value": npub / (pub_ms * 1e-3), "unit": "encrypts/s per GPU", "elements": npub,
                                     "kernel": "k_encrypt", "kernel_ms": pub_ms,
                                     "int_mac_frac": npub * work_enc_public(nb) / (pub_ms * 1e-3) / INT_MAC_PEAK,
@@ -507,7 +530,9 @@ def main():
         achieved = N * dom_work / (dom_ms * 1e-3)
         extra["k_add_ms"] = add_ms
     else:
-        if use_crt and use_fb:
+        if grp_fb:
+            names, works = ["k_fb_digits", "k_fbg", "k_crt_fin"], work_fbg(nb, fb_info[2])
+        elif use_crt and use_fb:
             names, works = ["k_fb_digits", "k_fb", "k_fb_fin"], work_fb(nb, fb_info[2])
         elif use_crt:
             names, works = ["k_crt_a", "k_crt_b", "k_crt_fin"], work_crt(nb)
@@ -521,7 +546,7 @@ def main():
         extra["stages"] = stages
         achieved = N * dom_work / (dom_ms * 1e-3)
         enc_ms = float(sum(stage_avg))
-        extra["path"] = ("crt-fixedbase" if use_fb else "crt") if use_crt else "public"
+        extra["path"] = "crt-fixedbase" if use_fb else "crt" if use_crt else "public"
         if use_fb:
             extra["fixed_base"] = {"g_p": fb_info[0], "g_q": fb_info[1], "digits": fb_info[2], "window_bits": fb_info[3]}
         extra["encrypt_call_ms"] = enc_ms
@@ -540,7 +565,7 @@ def main():
             th = max(1, args.cpu_threads)
             cores = {"os_cpu_count": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
                      "cpu_model": cpu_model()}
-            S = min(args.cpu_sample, N)
+            S = S_chk
             t1 = time.perf_counter()
             cct, cex = gmp_oracle.encrypt_f32_chacha(pk.n, x_host[:S], rng_key, index_base_chk, th)
             cdt = time.perf_counter() - t1
@@ -594,8 +619,9 @@ def main():
         "dtype": "u32",
         "data": "synthetic: numpy default_rng(rank).standard_normal float32; seeded key "
                 "generate_paillier_keypair(nb, seed=1); device ChaCha20 obfuscators keyed by global index",
-        "config": {"workload": cfg["desc"] + " (" + ((("key holder: CRT, fixed-base r^n sampler" if use_fb else
-                                                      "key holder: CRT") if use_crt else "public-key") + " path"
+        "config": {"workload": cfg["desc"] + " (" + (("key holder: fixed-base r^n sampler on the lane-group engine"
+                                                      if grp_fb else "key holder: CRT, fixed-base r^n sampler")
+                                                     if use_fb else "key holder: CRT" if use_crt else "public-key") + " path"
                                                     + (", RCCL all-gather of ciphertext shards in the step" if world > 1 else "") + ")"),
                    "baseline_config": cfg_id, "key_bits": nb,
                    "elements_total": total if cfg["shard"] == "strong" else world * N,
@@ -606,7 +632,7 @@ def main():
                      "kernel": dom, "kernel_ms": dom_ms,
                      "work_per_unit": (f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} table "
                                        f"products per half, 32-bit limbs, kernels_fb.hpp), not SURVEY.md §8d's W_enc"
-                                       if dom == "k_fb" else f"{dom_work:.4g} canonical 32x32->64 MAC per element (SURVEY.md §8d)")},
+                                       if dom in ("k_fb", "k_fbg") else f"{dom_work:.4g} canonical 32x32->64 MAC per element (SURVEY.md §8d)")},
         "roofline_hbm": {"bound": "hbm", "achieved": extra.get("hbm_algorithmic_gbs"), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": (extra["hbm_algorithmic_gbs"] / HBM_PEAK_GBS) if "hbm_algorithmic_gbs" in extra else None,
                          "algorithmic_bytes_per_unit": alg_bytes},

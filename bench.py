@@ -602,6 +602,9 @@ def main():
                                     "decrypt_per_s": 1000 / t_d0, "encrypt_s": t_e0, "decrypt_s": t_d0,
                                     "threads": th, **cores, "kind": "port (oracle/gmp_oracle.c)"}
 
+    path_label = (("key holder: fixed-base r^n sampler on the lane-group engine" if grp_fb
+                   else "key holder: CRT, fixed-base r^n sampler") if use_fb
+                  else "key holder: CRT" if use_crt else "public-key")
     metric = {1: "Paillier-2048 encrypts/sec (device-resident), 1M-elem float32 array",
               2: "Paillier-2048 encrypt + 8-way add + decrypt, elements/sec (device-resident), 1M-elem arrays"}
     out = {
@@ -619,10 +622,8 @@ def main():
         "dtype": "u32",
         "data": "synthetic: numpy default_rng(rank).standard_normal float32; seeded key "
                 "generate_paillier_keypair(nb, seed=1); device ChaCha20 obfuscators keyed by global index",
-        "config": {"workload": cfg["desc"] + " (" + (("key holder: fixed-base r^n sampler on the lane-group engine"
-                                                      if grp_fb else "key holder: CRT, fixed-base r^n sampler")
-                                                     if use_fb else "key holder: CRT" if use_crt else "public-key") + " path"
-                                                    + (", RCCL all-gather of ciphertext shards in the step" if world > 1 else "") + ")"),
+        "config": {"workload": cfg["desc"] + " (" + path_label + " path"
+                               + (", RCCL all-gather of ciphertext shards in the step" if world > 1 else "") + ")",
                    "baseline_config": cfg_id, "key_bits": nb,
                    "elements_total": total if cfg["shard"] == "strong" else world * N,
                    "elements_per_gpu": N, "parallelism": f"dp{world}"},

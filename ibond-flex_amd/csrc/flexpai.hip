@@ -113,10 +113,20 @@ struct pai_ctx {
   bool timing = false;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   int nev = 0;
+  // host-buffer entry points (pai_encrypt / pai_decrypt / pai_add): device copies of the operands, a
+  // compute and a copy stream, one event per chunk (host_pipe below)
+  void* d_hostio = nullptr;
+  size_t hostio_bytes = 0;
+  hipStream_t s_comp = nullptr, s_copy = nullptr;
+  std::vector<hipEvent_t> hev;
   ~pai_ctx() {
     (void)hipSetDevice(device);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : hev) (void)hipEventDestroy(e);
+    if (s_comp) (void)hipStreamDestroy(s_comp);
+    if (s_copy) (void)hipStreamDestroy(s_copy);
+    if (d_hostio) (void)hipFree(d_hostio);
     for (void* p : allocs) (void)hipFree(p);
     for (void* p : priv_allocs) (void)hipFree(p);
     for (void* p : fb_mem) (void)hipFree(p);
@@ -1737,44 +1747,96 @@ int pai_matmul(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t m, siz
   return 0;
 }
 
+// ------------------------------------------------------------------ host-buffer entry points
+// The operands cross PCIe in chunks that overlap the kernels: outputs of chunk i are copied to the
+// caller while chunk i+1 computes (encrypt), inputs of chunk i+1 are copied while chunk i computes
+// (decrypt, add). Ciphertexts do not depend on the chunking (the device RNG is keyed by the global
+// element index). Device copies live in one buffer kept by the context (grown on demand).
+constexpr size_t HOST_CHUNK_MIN = (size_t)1 << 17;   // elements: large enough to fill the chip per chunk
+constexpr int HOST_CHUNKS_MAX = 16;
+
+static int host_pipe(pai_ctx* c, size_t N, size_t bytes, size_t* chunk, int* nch) {
+  if (!c->s_comp) HIPCHK(hipStreamCreateWithFlags(&c->s_comp, hipStreamNonBlocking));
+  if (!c->s_copy) HIPCHK(hipStreamCreateWithFlags(&c->s_copy, hipStreamNonBlocking));
+  while (c->hev.size() < (size_t)HOST_CHUNKS_MAX) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->hev.push_back(e);
+  }
+  *nch = (int)std::max<size_t>(1, std::min<size_t>(HOST_CHUNKS_MAX, N / HOST_CHUNK_MIN));
+  *chunk = (N + *nch - 1) / *nch;
+  *nch = (int)((N + *chunk - 1) / *chunk);
+  return ensure_buf(&c->d_hostio, &c->hostio_bytes, bytes);
+}
+
+// Carves typed regions out of the context's host-io buffer (256-byte aligned).
+struct Carve {
+  char* base;
+  size_t off = 0;
+  template <typename T>
+  T* take(size_t n) {
+    T* p = (T*)(base + off);
+    off = (off + std::max<size_t>(n, 1) * sizeof(T) + 255) & ~(size_t)255;
+    return p;
+  }
+};
+static size_t carve_bytes(std::initializer_list<size_t> sizes) {
+  size_t t = 0;
+  for (size_t b : sizes) t += (std::max<size_t>(b, 1) + 255) & ~(size_t)255;
+  return t;
+}
+
 int pai_encrypt(pai_ctx* c, int dtype, const void* x, size_t N, int exp_mode, int32_t fixed_exp, int obf_mode,
                 const uint8_t* r_le, size_t r_stride_bytes, size_t r_bytes, const uint8_t* rng_key32,
                 uint64_t index_base, uint32_t* ct_out, int32_t* exp_out, int32_t* status_out) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
   if (N == 0) return 0;
   if (!x || !ct_out || !exp_out) return fail(PAI_ERR_ARG, "pai_encrypt: null buffer");
+  if (obf_mode == PAI_OBF_GIVEN && (!r_le || r_bytes == 0)) return fail(PAI_ERR_ARG, "pai_encrypt: r required");
   HIPCHK(hipSetDevice(c->device));
-  const size_t esz = dtype == PAI_F32 ? 4 : 8;
-  DevScope ds;
-  void* dx = ds.alloc<uint8_t>(N * esz);
-  uint32_t* dct = ds.alloc<uint32_t>(N * c->ct_words);
-  int32_t* dexp = ds.alloc<int32_t>(N);
-  int32_t* dst = ds.alloc<int32_t>(N);
-  if (!dx || !dct || !dexp || !dst) return fail(PAI_ERR_HIP, "pai_encrypt: device allocation failed");
-  HIPCHK(hipMemcpy(dx, x, N * esz, hipMemcpyHostToDevice));
-  uint32_t* dr = nullptr;
-  size_t r_words = 0, r_stride_words = 0;
-  if (obf_mode == PAI_OBF_GIVEN) {
-    if (!r_le || r_bytes == 0) return fail(PAI_ERR_ARG, "pai_encrypt: r required");
-    r_words = (r_bytes + 3) / 4;
-    const size_t cnt = r_stride_bytes ? N : 1;
-    std::vector<uint32_t> hr(cnt * r_words, 0);
-    for (size_t i = 0; i < cnt; ++i) {
-      const uint8_t* src = r_le + i * r_stride_bytes;
-      std::memcpy(&hr[i * r_words], src, r_bytes);
-    }
-    dr = ds.alloc<uint32_t>(hr.size());
-    if (!dr) return fail(PAI_ERR_HIP, "pai_encrypt: device allocation failed");
-    HIPCHK(hipMemcpy(dr, hr.data(), hr.size() * 4, hipMemcpyHostToDevice));
-    r_stride_words = r_stride_bytes ? r_words : 0;
+  const size_t esz = dtype == PAI_F32 ? 4 : 8, W = c->ct_words;
+  const size_t r_words = obf_mode == PAI_OBF_GIVEN ? (r_bytes + 3) / 4 : 0;
+  const size_t r_cnt = obf_mode == PAI_OBF_GIVEN ? (r_stride_bytes ? N : 1) : 0;
+  size_t CH;
+  int nch, rc;
+  if ((rc = host_pipe(c, N, carve_bytes({N * esz, N * W * 4, N * 4, N * 4, r_cnt * r_words * 4}), &CH, &nch)))
+    return rc;
+  Carve cv{(char*)c->d_hostio};
+  void* dx = cv.take<uint8_t>(N * esz);
+  uint32_t* dct = cv.take<uint32_t>(N * W);
+  int32_t* dexp = cv.take<int32_t>(N);
+  int32_t* dst = cv.take<int32_t>(N);
+  uint32_t* dr = cv.take<uint32_t>(r_cnt * r_words);
+  hipStream_t sc = c->s_comp, sy = c->s_copy;
+  HIPCHK(hipMemcpyAsync(dx, x, N * esz, hipMemcpyHostToDevice, sc));
+  if (r_cnt) {
+    std::vector<uint32_t> hr(r_cnt * r_words, 0);
+    for (size_t i = 0; i < r_cnt; ++i) std::memcpy(&hr[i * r_words], r_le + i * r_stride_bytes, r_bytes);
+    HIPCHK(hipMemcpyAsync(dr, hr.data(), hr.size() * 4, hipMemcpyHostToDevice, sc));
+    HIPCHK(hipStreamSynchronize(sc));   // hr is released at the end of this scope
   }
-  int rc = pai_encrypt_dev(c, dtype, dx, N, exp_mode, fixed_exp, obf_mode, dr, r_stride_words, r_words, rng_key32,
-                           index_base, dct, dexp, dst, nullptr);
-  if (rc) return rc;
-  HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(ct_out, dct, N * c->ct_words * 4, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(exp_out, dexp, N * 4, hipMemcpyDeviceToHost));
-  if (status_out) HIPCHK(hipMemcpy(status_out, dst, N * 4, hipMemcpyDeviceToHost));
+  const size_t r_stride_words = r_stride_bytes ? r_words : 0;
+  // every chunk's kernels are queued first; the copy stream then drains chunk i while i+1.. compute
+  for (int i = 0; i < nch; ++i) {
+    const size_t off = (size_t)i * CH, n = std::min(CH, N - off);
+    rc = pai_encrypt_dev(c, dtype, (const char*)dx + off * esz, n, exp_mode, fixed_exp, obf_mode,
+                         dr ? dr + off * r_stride_words : nullptr, r_stride_words, r_words, rng_key32,
+                         index_base + off, dct + off * W, dexp + off, dst + off, sc);
+    if (rc) {
+      (void)hipStreamSynchronize(sc);
+      return rc;
+    }
+    HIPCHK(hipEventRecord(c->hev[i], sc));
+  }
+  for (int i = 0; i < nch; ++i) {
+    const size_t off = (size_t)i * CH, n = std::min(CH, N - off);
+    HIPCHK(hipStreamWaitEvent(sy, c->hev[i], 0));
+    HIPCHK(hipMemcpyAsync(ct_out + off * W, dct + off * W, n * W * 4, hipMemcpyDeviceToHost, sy));
+    HIPCHK(hipMemcpyAsync(exp_out + off, dexp + off, n * 4, hipMemcpyDeviceToHost, sy));
+    if (status_out) HIPCHK(hipMemcpyAsync(status_out + off, dst + off, n * 4, hipMemcpyDeviceToHost, sy));
+  }
+  HIPCHK(hipStreamSynchronize(sy));
+  HIPCHK(hipStreamSynchronize(sc));
   return 0;
 }
 
@@ -1783,24 +1845,39 @@ int pai_add(pai_ctx* c, const uint32_t* const* cts, const int32_t* const* exps, 
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
   if (N == 0) return 0;
   if (k < 1 || !cts || !exps || !ct_out || !exp_out) return fail(PAI_ERR_ARG, "pai_add: bad arguments");
-  HIPCHK(hipSetDevice(c->device));
-  DevScope ds;
-  const size_t W = c->ct_words;
-  uint32_t* dcts = ds.alloc<uint32_t>((size_t)k * N * W);
-  int32_t* dexps = ds.alloc<int32_t>((size_t)k * N);
-  uint32_t* dout = ds.alloc<uint32_t>(N * W);
-  int32_t* dexp = ds.alloc<int32_t>(N);
-  if (!dcts || !dexps || !dout || !dexp) return fail(PAI_ERR_HIP, "pai_add: device allocation failed");
-  for (int j = 0; j < k; ++j) {
+  for (int j = 0; j < k; ++j)
     if (!cts[j] || !exps[j]) return fail(PAI_ERR_ARG, "pai_add: null operand");
-    HIPCHK(hipMemcpy(dcts + (size_t)j * N * W, cts[j], N * W * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(dexps + (size_t)j * N, exps[j], N * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipSetDevice(c->device));
+  const size_t W = c->ct_words;
+  size_t CH;
+  int nch, rc;
+  if ((rc = host_pipe(c, N, carve_bytes({(size_t)k * N * W * 4, (size_t)k * N * 4, N * W * 4, N * 4}), &CH, &nch)))
+    return rc;
+  Carve cv{(char*)c->d_hostio};
+  // chunk i's operands are contiguous [k][n_i][W] at offset k off (the k_add layout of that chunk)
+  uint32_t* dcts = cv.take<uint32_t>((size_t)k * N * W);
+  int32_t* dexps = cv.take<int32_t>((size_t)k * N);
+  uint32_t* dout = cv.take<uint32_t>(N * W);
+  int32_t* dexp = cv.take<int32_t>(N);
+  hipStream_t sc = c->s_comp, sy = c->s_copy;
+  for (int i = 0; i < nch; ++i) {
+    const size_t off = (size_t)i * CH, n = std::min(CH, N - off);
+    uint32_t* cc = dcts + (size_t)k * off * W;
+    int32_t* ce = dexps + (size_t)k * off;
+    for (int j = 0; j < k; ++j) {   // inputs of chunk i cross while chunk i-1 computes
+      HIPCHK(hipMemcpyAsync(cc + (size_t)j * n * W, cts[j] + off * W, n * W * 4, hipMemcpyHostToDevice, sy));
+      HIPCHK(hipMemcpyAsync(ce + (size_t)j * n, exps[j] + off, n * 4, hipMemcpyHostToDevice, sy));
+    }
+    HIPCHK(hipEventRecord(c->hev[i], sy));
+    HIPCHK(hipStreamWaitEvent(sc, c->hev[i], 0));
+    if ((rc = pai_add_dev(c, cc, ce, k, n, dout + off * W, dexp + off, sc))) {
+      (void)hipStreamSynchronize(sc);
+      return rc;
+    }
   }
-  int rc = pai_add_dev(c, dcts, dexps, k, N, dout, dexp, nullptr);
-  if (rc) return rc;
-  HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(ct_out, dout, N * W * 4, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(exp_out, dexp, N * 4, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpyAsync(ct_out, dout, N * W * 4, hipMemcpyDeviceToHost, sc));
+  HIPCHK(hipMemcpyAsync(exp_out, dexp, N * 4, hipMemcpyDeviceToHost, sc));
+  HIPCHK(hipStreamSynchronize(sc));
   return 0;
 }
 
@@ -1811,27 +1888,37 @@ int pai_decrypt(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, do
   if (N == 0) return 0;
   if (!ct || !exp || !val_out || !status_out) return fail(PAI_ERR_ARG, "pai_decrypt: null buffer");
   HIPCHK(hipSetDevice(c->device));
-  DevScope ds;
-  uint32_t* dct = ds.alloc<uint32_t>(N * c->ct_words);
-  int32_t* dexp = ds.alloc<int32_t>(N);
-  double* dval = ds.alloc<double>(N);
-  int64_t* dmant = ds.alloc<int64_t>(N);
-  int32_t* dst = ds.alloc<int32_t>(N);
-  uint32_t* draw = raw_out ? ds.alloc<uint32_t>(N * c->pt_words) : nullptr;
-  if (!dct || !dexp || !dval || !dmant || !dst || (raw_out && !draw))
-    return fail(PAI_ERR_HIP, "pai_decrypt: device allocation failed");
-  HIPCHK(hipMemcpy(dct, ct, N * c->ct_words * 4, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(dexp, exp, N * 4, hipMemcpyHostToDevice));
-  int rc = pai_decrypt_dev(c, dct, dexp, N, dval, dmant, dst, draw, nullptr);
-  if (rc) return rc;
-  HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(val_out, dval, N * 8, hipMemcpyDeviceToHost));
-  if (mant_out) HIPCHK(hipMemcpy(mant_out, dmant, N * 8, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(status_out, dst, N * 4, hipMemcpyDeviceToHost));
-  if (raw_out) HIPCHK(hipMemcpy(raw_out, draw, N * c->pt_words * 4, hipMemcpyDeviceToHost));
+  const size_t W = c->ct_words, P = raw_out ? c->pt_words : 0;
+  size_t CH;
+  int nch, rc;
+  if ((rc = host_pipe(c, N, carve_bytes({N * W * 4, N * 4, N * 8, N * 8, N * 4, N * P * 4}), &CH, &nch))) return rc;
+  Carve cv{(char*)c->d_hostio};
+  uint32_t* dct = cv.take<uint32_t>(N * W);
+  int32_t* dexp = cv.take<int32_t>(N);
+  double* dval = cv.take<double>(N);
+  int64_t* dmant = cv.take<int64_t>(N);
+  int32_t* dst = cv.take<int32_t>(N);
+  uint32_t* draw = cv.take<uint32_t>(N * P);
+  hipStream_t sc = c->s_comp, sy = c->s_copy;
+  for (int i = 0; i < nch; ++i) {
+    const size_t off = (size_t)i * CH, n = std::min(CH, N - off);
+    HIPCHK(hipMemcpyAsync(dct + off * W, ct + off * W, n * W * 4, hipMemcpyHostToDevice, sy));
+    HIPCHK(hipMemcpyAsync(dexp + off, exp + off, n * 4, hipMemcpyHostToDevice, sy));
+    HIPCHK(hipEventRecord(c->hev[i], sy));
+    HIPCHK(hipStreamWaitEvent(sc, c->hev[i], 0));
+    if ((rc = pai_decrypt_dev(c, dct + off * W, dexp + off, n, dval + off, dmant + off, dst + off,
+                              raw_out ? draw + off * P : nullptr, sc))) {
+      (void)hipStreamSynchronize(sc);
+      return rc;
+    }
+  }
+  HIPCHK(hipMemcpyAsync(val_out, dval, N * 8, hipMemcpyDeviceToHost, sc));
+  if (mant_out) HIPCHK(hipMemcpyAsync(mant_out, dmant, N * 8, hipMemcpyDeviceToHost, sc));
+  HIPCHK(hipMemcpyAsync(status_out, dst, N * 4, hipMemcpyDeviceToHost, sc));
+  if (raw_out) HIPCHK(hipMemcpyAsync(raw_out, draw, N * P * 4, hipMemcpyDeviceToHost, sc));
+  HIPCHK(hipStreamSynchronize(sc));
   return 0;
 }
-
 
 // ------------------------------------------------------------------ debugging hook (tests / tools only)
 // Copies the per-half k_fb outputs (c0 G_h^a_h mod h^2, limbs [2][SB][n]) of the last fixed-base chunk.

@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "flexpai.h"
@@ -118,12 +119,17 @@ struct pai_ctx {
   void* d_hostio = nullptr;
   size_t hostio_bytes = 0;
   hipStream_t s_comp = nullptr, s_copy = nullptr;
-  std::vector<hipEvent_t> hev;
+  std::vector<hipEvent_t> hev, pev;   // per chunk: kernels done / staging copy done
+  void* h_pin[2] = {nullptr, nullptr};  // pinned staging slots (PCIe at full rate, truly asynchronous)
+  size_t pin_bytes = 0;
   ~pai_ctx() {
     (void)hipSetDevice(device);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
     for (auto& e : hev) (void)hipEventDestroy(e);
+    for (auto& e : pev) (void)hipEventDestroy(e);
+    for (void* p : h_pin)
+      if (p) (void)hipHostFree(p);
     if (s_comp) (void)hipStreamDestroy(s_comp);
     if (s_copy) (void)hipStreamDestroy(s_copy);
     if (d_hostio) (void)hipFree(d_hostio);
@@ -315,6 +321,10 @@ static int blocks_per_cu(K kernel, int threads, size_t lds) {
 
 // C-linkage comes from the declarations in flexpai.h.
 const char* pai_last_error(void) { return g_last_error.c_str(); }
+
+namespace fpai {
+int set_error(int code, const char* msg) { return fail(code, msg); }   // for the other translation units
+}
 
 int pai_device_mem_info(int device, uint64_t* free_bytes, uint64_t* total_bytes) {
   HIPCHK(hipSetDevice(device));
@@ -1754,19 +1764,50 @@ int pai_matmul(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t m, siz
 // element index). Device copies live in one buffer kept by the context (grown on demand).
 constexpr size_t HOST_CHUNK_MIN = (size_t)1 << 17;   // elements: large enough to fill the chip per chunk
 constexpr int HOST_CHUNKS_MAX = 16;
+constexpr size_t PIN_SLOT_MAX = (size_t)64 << 20;     // bytes per pinned staging slot (two slots)
 
-static int host_pipe(pai_ctx* c, size_t N, size_t bytes, size_t* chunk, int* nch) {
+// Chunking for N elements moving stage_per_elem bytes each through the pinned slots; grows the
+// context's device buffer to dev_bytes, the pinned slots and the per-chunk events.
+static int host_pipe(pai_ctx* c, size_t N, size_t dev_bytes, size_t stage_per_elem, size_t* chunk, int* nch) {
   if (!c->s_comp) HIPCHK(hipStreamCreateWithFlags(&c->s_comp, hipStreamNonBlocking));
   if (!c->s_copy) HIPCHK(hipStreamCreateWithFlags(&c->s_copy, hipStreamNonBlocking));
-  while (c->hev.size() < (size_t)HOST_CHUNKS_MAX) {
-    hipEvent_t e;
-    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    c->hev.push_back(e);
-  }
-  *nch = (int)std::max<size_t>(1, std::min<size_t>(HOST_CHUNKS_MAX, N / HOST_CHUNK_MIN));
-  *chunk = (N + *nch - 1) / *nch;
+  size_t k = std::max<size_t>(1, std::min<size_t>(HOST_CHUNKS_MAX, N / HOST_CHUNK_MIN));
+  k = std::max(k, (N * stage_per_elem + PIN_SLOT_MAX - 1) / PIN_SLOT_MAX);
+  *chunk = (N + k - 1) / k;
   *nch = (int)((N + *chunk - 1) / *chunk);
-  return ensure_buf(&c->d_hostio, &c->hostio_bytes, bytes);
+  for (auto* v : {&c->hev, &c->pev})
+    while (v->size() < (size_t)*nch) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      v->push_back(e);
+    }
+  const size_t slot = *chunk * stage_per_elem;
+  if (slot > c->pin_bytes) {
+    for (void*& p : c->h_pin) {
+      if (p) HIPCHK(hipHostFree(p));
+      p = nullptr;
+    }
+    c->pin_bytes = 0;
+    for (void*& p : c->h_pin) HIPCHK(hipHostMalloc(&p, slot, hipHostMallocDefault));
+    c->pin_bytes = slot;
+  }
+  return ensure_buf(&c->d_hostio, &c->hostio_bytes, dev_bytes);
+}
+
+// memcpy between the pinned slots and caller memory on several host threads (a single thread moves
+// ~10 GB/s, below the PCIe rate).
+static void par_copy(void* dst, const void* src, size_t bytes) {
+  const size_t hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t T = bytes < ((size_t)4 << 20) ? 1 : std::min<size_t>(16, hw);
+  if (T == 1) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  const size_t part = ((bytes + T - 1) / T + 4095) & ~(size_t)4095;
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < T && t * part < bytes; ++t)
+    th.emplace_back([=] { std::memcpy((char*)dst + t * part, (const char*)src + t * part, std::min(part, bytes - t * part)); });
+  for (auto& x : th) x.join();
 }
 
 // Carves typed regions out of the context's host-io buffer (256-byte aligned).
@@ -1799,7 +1840,7 @@ int pai_encrypt(pai_ctx* c, int dtype, const void* x, size_t N, int exp_mode, in
   const size_t r_cnt = obf_mode == PAI_OBF_GIVEN ? (r_stride_bytes ? N : 1) : 0;
   size_t CH;
   int nch, rc;
-  if ((rc = host_pipe(c, N, carve_bytes({N * esz, N * W * 4, N * 4, N * 4, r_cnt * r_words * 4}), &CH, &nch)))
+  if ((rc = host_pipe(c, N, carve_bytes({N * esz, N * W * 4, N * 4, N * 4, r_cnt * r_words * 4}), W * 4, &CH, &nch)))
     return rc;
   Carve cv{(char*)c->d_hostio};
   void* dx = cv.take<uint8_t>(N * esz);
@@ -1828,15 +1869,26 @@ int pai_encrypt(pai_ctx* c, int dtype, const void* x, size_t N, int exp_mode, in
     }
     HIPCHK(hipEventRecord(c->hev[i], sc));
   }
-  for (int i = 0; i < nch; ++i) {
+  // ciphertext words: device -> pinned slot (i & 1) on the copy stream, then the host threads move the
+  // slot into the caller's buffer while chunk i+1 crosses PCIe and later chunks compute
+  auto d2h = [&](int i) -> int {
     const size_t off = (size_t)i * CH, n = std::min(CH, N - off);
     HIPCHK(hipStreamWaitEvent(sy, c->hev[i], 0));
-    HIPCHK(hipMemcpyAsync(ct_out + off * W, dct + off * W, n * W * 4, hipMemcpyDeviceToHost, sy));
-    HIPCHK(hipMemcpyAsync(exp_out + off, dexp + off, n * 4, hipMemcpyDeviceToHost, sy));
-    if (status_out) HIPCHK(hipMemcpyAsync(status_out + off, dst + off, n * 4, hipMemcpyDeviceToHost, sy));
+    HIPCHK(hipMemcpyAsync(c->h_pin[i & 1], dct + off * W, n * W * 4, hipMemcpyDeviceToHost, sy));
+    HIPCHK(hipEventRecord(c->pev[i], sy));
+    return 0;
+  };
+  if ((rc = d2h(0))) return rc;
+  for (int i = 0; i < nch; ++i) {
+    if (i + 1 < nch && (rc = d2h(i + 1))) return rc;   // its slot's previous chunk (i - 1) is consumed
+    const size_t off = (size_t)i * CH, n = std::min(CH, N - off);
+    HIPCHK(hipEventSynchronize(c->pev[i]));
+    par_copy(ct_out + off * W, c->h_pin[i & 1], n * W * 4);
   }
-  HIPCHK(hipStreamSynchronize(sy));
+  HIPCHK(hipMemcpyAsync(exp_out, dexp, N * 4, hipMemcpyDeviceToHost, sc));
+  if (status_out) HIPCHK(hipMemcpyAsync(status_out, dst, N * 4, hipMemcpyDeviceToHost, sc));
   HIPCHK(hipStreamSynchronize(sc));
+  HIPCHK(hipStreamSynchronize(sy));
   return 0;
 }
 
@@ -1851,7 +1903,8 @@ int pai_add(pai_ctx* c, const uint32_t* const* cts, const int32_t* const* exps, 
   const size_t W = c->ct_words;
   size_t CH;
   int nch, rc;
-  if ((rc = host_pipe(c, N, carve_bytes({(size_t)k * N * W * 4, (size_t)k * N * 4, N * W * 4, N * 4}), &CH, &nch)))
+  if ((rc = host_pipe(c, N, carve_bytes({(size_t)k * N * W * 4, (size_t)k * N * 4, N * W * 4, N * 4}),
+                     (size_t)k * W * 4, &CH, &nch)))
     return rc;
   Carve cv{(char*)c->d_hostio};
   // chunk i's operands are contiguous [k][n_i][W] at offset k off (the k_add layout of that chunk)
@@ -1864,10 +1917,13 @@ int pai_add(pai_ctx* c, const uint32_t* const* cts, const int32_t* const* exps, 
     const size_t off = (size_t)i * CH, n = std::min(CH, N - off);
     uint32_t* cc = dcts + (size_t)k * off * W;
     int32_t* ce = dexps + (size_t)k * off;
-    for (int j = 0; j < k; ++j) {   // inputs of chunk i cross while chunk i-1 computes
-      HIPCHK(hipMemcpyAsync(cc + (size_t)j * n * W, cts[j] + off * W, n * W * 4, hipMemcpyHostToDevice, sy));
+    // inputs of chunk i: caller -> pinned slot (host threads, while chunk i-1 computes) -> device
+    if (i >= 2) HIPCHK(hipEventSynchronize(c->hev[i - 2]));   // the slot's previous upload is done
+    uint32_t* slot = (uint32_t*)c->h_pin[i & 1];
+    for (int j = 0; j < k; ++j) par_copy(slot + (size_t)j * n * W, cts[j] + off * W, n * W * 4);
+    HIPCHK(hipMemcpyAsync(cc, slot, (size_t)k * n * W * 4, hipMemcpyHostToDevice, sy));
+    for (int j = 0; j < k; ++j)
       HIPCHK(hipMemcpyAsync(ce + (size_t)j * n, exps[j] + off, n * 4, hipMemcpyHostToDevice, sy));
-    }
     HIPCHK(hipEventRecord(c->hev[i], sy));
     HIPCHK(hipStreamWaitEvent(sc, c->hev[i], 0));
     if ((rc = pai_add_dev(c, cc, ce, k, n, dout + off * W, dexp + off, sc))) {
@@ -1891,7 +1947,8 @@ int pai_decrypt(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, do
   const size_t W = c->ct_words, P = raw_out ? c->pt_words : 0;
   size_t CH;
   int nch, rc;
-  if ((rc = host_pipe(c, N, carve_bytes({N * W * 4, N * 4, N * 8, N * 8, N * 4, N * P * 4}), &CH, &nch))) return rc;
+  if ((rc = host_pipe(c, N, carve_bytes({N * W * 4, N * 4, N * 8, N * 8, N * 4, N * P * 4}), W * 4, &CH, &nch)))
+    return rc;
   Carve cv{(char*)c->d_hostio};
   uint32_t* dct = cv.take<uint32_t>(N * W);
   int32_t* dexp = cv.take<int32_t>(N);
@@ -1902,7 +1959,9 @@ int pai_decrypt(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, do
   hipStream_t sc = c->s_comp, sy = c->s_copy;
   for (int i = 0; i < nch; ++i) {
     const size_t off = (size_t)i * CH, n = std::min(CH, N - off);
-    HIPCHK(hipMemcpyAsync(dct + off * W, ct + off * W, n * W * 4, hipMemcpyHostToDevice, sy));
+    if (i >= 2) HIPCHK(hipEventSynchronize(c->hev[i - 2]));   // the slot's previous upload is done
+    par_copy(c->h_pin[i & 1], ct + off * W, n * W * 4);
+    HIPCHK(hipMemcpyAsync(dct + off * W, c->h_pin[i & 1], n * W * 4, hipMemcpyHostToDevice, sy));
     HIPCHK(hipMemcpyAsync(dexp + off, exp + off, n * 4, hipMemcpyHostToDevice, sy));
     HIPCHK(hipEventRecord(c->hev[i], sy));
     HIPCHK(hipStreamWaitEvent(sc, c->hev[i], 0));

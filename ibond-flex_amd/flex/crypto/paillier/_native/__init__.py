@@ -29,7 +29,9 @@ EXPORTED = ("pai_device_count", "pai_device_mem_info", "pai_ctx_create", "pai_ct
             "pai_ctx_fixed_base_prepare", "pai_ctx_fixed_base_setup",
             "pai_encrypt", "pai_add", "pai_decrypt", "pai_encrypt_dev", "pai_add_dev", "pai_decrypt_dev",
             "pai_mul", "pai_mul_dev", "pai_matmul", "pai_matmul_dev", "pai_add_plain", "pai_add_plain_dev",
-            "pai_segment_add", "pai_segment_add_dev")
+            "pai_segment_add", "pai_segment_add_dev", "pai_comm_unique_id", "pai_comm_create", "pai_comm_destroy",
+            "pai_allgather_dev", "pai_allgather_shards_dev")
+PAI_COMM_ID_BYTES = 128
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -78,8 +80,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.pai_segment_add_dev.argtypes = [P, P, P, S, P, P, S, P, P, P]
         lib.pai_matmul.argtypes = [P, P, P, S, S, I, P, S, P, P]
         lib.pai_matmul_dev.argtypes = [P, P, P, S, S, I, P, S, P, P, P]
+        lib.pai_comm_unique_id.argtypes = [P]
+        lib.pai_comm_create.argtypes = [P, I, I, I, ctypes.POINTER(ctypes.c_void_p)]
+        lib.pai_comm_destroy.argtypes = [P]
+        lib.pai_comm_destroy.restype = None
+        lib.pai_allgather_dev.argtypes = [P, P, S, P, P]
+        lib.pai_allgather_shards_dev.argtypes = [P, P, P, S, I, P, P, P]
         for name in EXPORTED:
-            if name not in ("pai_ctx_destroy", "pai_last_error"):
+            if name not in ("pai_ctx_destroy", "pai_last_error", "pai_comm_destroy"):
                 getattr(lib, name).restype = ctypes.c_int
         _lib = lib
         return lib
@@ -97,6 +105,42 @@ def device_mem_info(device: int = 0):
     fr, tot = ctypes.c_uint64(), ctypes.c_uint64()
     _check(load_library().pai_device_mem_info(device, ctypes.byref(fr), ctypes.byref(tot)))
     return fr.value, tot.value
+
+
+class Comm:
+    """RCCL communicator of the C ABI's shard all-gather (pai_comm_*): one per rank, one process per GPU.
+    Rank 0 makes the id (Comm.unique_id()) and passes it to the others over any channel."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * PAI_COMM_ID_BYTES)()
+        _check(load_library().pai_comm_unique_id(buf))
+        return bytes(buf)
+
+    def __init__(self, uid: bytes, world: int, rank: int, device: int = 0):
+        if len(uid) != PAI_COMM_ID_BYTES:
+            raise ValueError("communicator id must be %d bytes" % PAI_COMM_ID_BYTES)
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        _check(self.lib.pai_comm_create(uid, world, rank, device, ctypes.byref(h)))
+        self._h, self.world, self.rank = h, world, rank
+
+    def allgather_shards(self, d_ct: int, d_exp: int, n_per_rank: int, ct_words: int, d_ct_all: int,
+                         d_exp_all: int, stream: int = 0):
+        """Device pointers (e.g. torch tensor .data_ptr()); asynchronous on `stream`."""
+        _check(self.lib.pai_allgather_shards_dev(self._h, d_ct, d_exp, n_per_rank, ct_words, d_ct_all, d_exp_all,
+                                                 stream or None))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.pai_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def _check(rc: int):

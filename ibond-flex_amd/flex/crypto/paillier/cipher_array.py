@@ -402,27 +402,56 @@ def add_plain(a, y):
 #   magic "FPAW1\0" | u32 ndim | i64 shape[ndim] | u32 n_bytes | n (little-endian) | u32 W |
 #   i32 exponents[N] | u8 obfuscated[N] | u32 words[N][W]
 # i.e. 4 W + 5 bytes per element plus a header; ciphertext i = int.from_bytes(words[i], "little").
-# Pickling a PaillierArray still yields a plain object ndarray, so unmodified peers are unaffected.
+# PaillierArray pickles through this format (see the module docstring; FLEXPAI_PICKLE_PLAIN=1 for mixed
+# deployments); from_wire(lazy=True) reads it into a CiphertextBuffer without per-element objects.
 _WIRE_MAGIC = b"FPAW1\0"
 
 
+def _wire_bytes(n: int, shape, exps, obf, words) -> bytes:
+    nb = (n.bit_length() + 7) // 8
+    head = [_WIRE_MAGIC, np.uint32(len(shape)).tobytes(), np.asarray(shape, dtype="<i8").tobytes(),
+            np.uint32(nb).tobytes(), n.to_bytes(nb, "little"), np.uint32(words.shape[1]).tobytes()]
+    return b"".join(head + [np.ascontiguousarray(exps, dtype="<i4").tobytes(),
+                            np.ascontiguousarray(obf, dtype=np.uint8).tobytes(),
+                            np.ascontiguousarray(words, dtype="<u4").tobytes()])
+
+
 def to_wire(arr) -> bytes:
-    """Serialise an array of PaillierEncryptedNumber (one public key) into the bulk format."""
+    """Serialise an array of PaillierEncryptedNumber (one public key), or a CiphertextBuffer, into the
+    bulk format."""
+    from .cipher_buffer import CiphertextBuffer
+    if isinstance(arr, CiphertextBuffer):
+        return arr.to_wire()
     A, pk = _encrypted_operand(arr)
     if A is None:
         raise TypeError("to_wire needs a non-empty array of PaillierEncryptedNumber with one public key")
     words, exps, _ = pack(arr if isinstance(arr, PaillierArray) else A, pk)
     obf = np.fromiter((e._is_obfuscated() for e in A.reshape(-1)), dtype=np.uint8, count=A.size)
-    nb = (pk.n.bit_length() + 7) // 8
-    head = [_WIRE_MAGIC, np.uint32(A.ndim).tobytes(), np.asarray(A.shape, dtype="<i8").tobytes(),
-            np.uint32(nb).tobytes(), pk.n.to_bytes(nb, "little"), np.uint32(words.shape[1]).tobytes()]
-    return b"".join(head + [np.ascontiguousarray(exps, dtype="<i4").tobytes(), obf.tobytes(),
-                            np.ascontiguousarray(words, dtype="<u4").tobytes()])
+    return _wire_bytes(pk.n, A.shape, exps, obf, words)
 
 
-def from_wire(buf, public_key=None) -> PaillierArray:
+def _rows_below(words: np.ndarray, limit: int) -> bool:
+    """True when every row of little-endian words, read as an integer, is < limit (vectorised: the most
+    significant word where a row differs from the limit decides)."""
+    N, W = words.shape
+    lw = np.frombuffer(limit.to_bytes(4 * W, "little"), dtype="<u4")
+    step = max(1, (1 << 24) // max(W, 1))
+    for o in range(0, N, step):
+        w = words[o:o + step]
+        ne = w != lw
+        if not ne.any(axis=1).all():
+            return False                                  # a row equal to the limit
+        j = W - 1 - np.argmax(ne[:, ::-1], axis=1)
+        if not (w[np.arange(w.shape[0]), j] < lw[j]).all():
+            return False
+    return True
+
+
+def from_wire(buf, public_key=None, lazy: bool = False):
     """Inverse of to_wire. `public_key` (optional) must match the key in the buffer (ValueError
-    otherwise, like encrypted_number.py:169-170); without it a PaillierPublicKey is rebuilt from n."""
+    otherwise, like encrypted_number.py:169-170); without it a PaillierPublicKey is rebuilt from n.
+    lazy=True returns a CiphertextBuffer (cipher_buffer.py): the validated words and exponents, no
+    Python object per element."""
     from .keypair import PaillierPublicKey
     mv = memoryview(buf).cast("B")
     bad = ValueError("corrupted ciphertext array")
@@ -444,17 +473,18 @@ def from_wire(buf, public_key=None) -> PaillierArray:
     if len(mv) != o + N * (4 * W + 5):
         raise ValueError("corrupted ciphertext array (length mismatch)")
     exps = np.frombuffer(mv, "<i4", N, o).astype(np.int32); o += 4 * N
-    obf = np.frombuffer(mv, np.uint8, N, o); o += N
+    obf = np.frombuffer(mv, np.uint8, N, o).copy(); o += N
     words = np.frombuffer(mv, "<u4", N * W, o).reshape(N, W).copy(); o += 4 * N * W
     if public_key is None:
         public_key = PaillierPublicKey(n)
     elif public_key.n != n:
         raise ValueError("ciphertext array was encrypted under a different public key")
-    res = materialize(public_key, words, exps, shape, obfuscated=obf != 0)
-    nsq = public_key.nsquare
-    if any(c >= nsq for c in res._packed.ints):
+    if not _rows_below(words, public_key.nsquare):
         raise ValueError("corrupted ciphertext array (ciphertext >= n^2)")
-    return res
+    if lazy:
+        from .cipher_buffer import CiphertextBuffer
+        return CiphertextBuffer(public_key, words, exps, obf, shape)
+    return materialize(public_key, words, exps, shape, obfuscated=obf != 0)
 
 
 def _from_pickle(buf) -> PaillierArray:

@@ -1,8 +1,10 @@
 """PaillierDecryptor — same API and errors as flex/crypto/paillier/decryptor.py:28-127.
 
-Arrays decrypt in ONE GPU launch: both CRT half-exponentiations c^(p-1) mod p^2 and
-c^(q-1) mod q^2, the L-function, the CRT recombination and the fixed-point decode to float64
-run on the device (kernels.hpp k_decrypt)."""
+Arrays decrypt in ONE device call: both CRT half-exponentiations c^(p-1) mod p^2 and c^(q-1) mod q^2,
+the L-function, the CRT recombination and the fixed-point decode to float64 run on the GPU -- the
+lane-engine kernels k_dec_pre / k_dec_pow / k_dec_fin (kernels_dec.hpp) for 1024- and 2048-bit keys,
+the lane-group kernel k_decrypt (kernels.hpp) for larger ones. A CiphertextBuffer (cipher_buffer.py)
+decrypts straight from its words, without per-element objects."""
 from __future__ import annotations
 
 from typing import Union
@@ -43,7 +45,6 @@ class PaillierDecryptor(object):
 
     def _decrypt_numpy(self, encrypted_number_numpy: np.ndarray) -> np.ndarray:
         """decryptor.py:91-112, one batched GPU launch."""
-        from . import _native, _runtime
         from .cipher_array import pack
         s = encrypted_number_numpy.shape
         flat = np.asarray(encrypted_number_numpy).reshape(-1)
@@ -52,6 +53,10 @@ class PaillierDecryptor(object):
         for e in flat:
             self._check(e)
         words, exps, _ = pack(encrypted_number_numpy, self.pub_key)
+        return self._decrypt_words(words, exps, s)
+
+    def _decrypt_words(self, words: np.ndarray, exps: np.ndarray, s) -> np.ndarray:
+        from . import _native, _runtime
         ctx = _runtime.context(self.pub_key, self.priv_key)
         val, mant, st, _ = ctx.decrypt(words, exps)
         if np.all(st == _native.EL_OK):
@@ -65,7 +70,7 @@ class PaillierDecryptor(object):
             _, _, _, raw_words = ctx.decrypt(words, exps, want_raw=True)
             raw = _runtime.words_to_ints(raw_words)
         values = []
-        for i in range(flat.size):
+        for i in range(exps.size):
             if st[i] == _native.EL_OK:
                 values.append(float(val[i]))
             elif st[i] == _native.EL_INT:
@@ -75,7 +80,14 @@ class PaillierDecryptor(object):
         return np.array(values).reshape(s)
 
     def decrypt(self, encrypted_number):
-        """decryptor.py:114-127"""
+        """decryptor.py:114-127 (plus CiphertextBuffer, cipher_buffer.py)"""
+        from .cipher_buffer import CiphertextBuffer
+        if isinstance(encrypted_number, CiphertextBuffer):
+            if encrypted_number.public_key != self.pub_key:
+                raise ValueError("encrypted_number was encrypted against a different key!")
+            if encrypted_number.size == 0:
+                return np.array([]).reshape(encrypted_number.shape)
+            return self._decrypt_words(encrypted_number.words, encrypted_number.exps, encrypted_number.shape)
         if isinstance(encrypted_number, np.ndarray):
             return self._decrypt_numpy(encrypted_number)
         return self._decrypt(encrypted_number)

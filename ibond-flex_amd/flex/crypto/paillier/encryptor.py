@@ -100,6 +100,33 @@ class PaillierEncryptor(object):
             out = PaillierArray(objs.reshape(s))
         return out
 
+    def encrypt_to_buffer(self, values: np.ndarray, precision: int = None):
+        """Encrypt an array into a CiphertextBuffer (cipher_buffer.py): the device words, exponents and
+        obfuscation flags, no PaillierEncryptedNumber per element. Same ciphertext distribution as
+        encrypt(values); for callers that ship (to_wire) or sum ciphertexts without touching them."""
+        from . import _native, _runtime
+        from .cipher_buffer import CiphertextBuffer
+        values = np.asarray(values)
+        s = values.shape
+        x, _ = _device_input(values.reshape(-1))
+        if x is None:
+            raise TypeError(f"encrypt_to_buffer: unsupported input dtype {values.dtype}")
+        exp_mode, fixed_exp = _native.PAI_EXP_AUTO, 0
+        if precision is not None:
+            exp_mode, fixed_exp = _native.PAI_EXP_FIXED, math.floor(math.log(precision, FixedPointNumber.BASE))
+        ctx = _runtime.context(self.pub_key)
+        ct, ex, st = ctx.encrypt(x, exp_mode, fixed_exp, _native.PAI_OBF_RNG)
+        bad_idx = np.nonzero(st != _native.EL_OK)[0]
+        if bad_idx.size:
+            # beyond the device's 64-bit fixed-point range: the host encoder (raises like the reference)
+            ct = ct.copy()
+            ex = ex.copy()
+            for i in bad_idx.tolist():
+                e = self._encrypt(values.reshape(-1)[i], precision)
+                ct[i] = _runtime.ints_to_words([e.ciphertext(False)], ct.shape[1])[0]
+                ex[i] = e.exponent
+        return CiphertextBuffer(self.pub_key, ct, ex, 1, s)
+
     def encrypt(self, value, precision: int = None, random_value: int = None):
         """encryptor.py:99-114"""
         if isinstance(value, np.ndarray):

@@ -24,6 +24,9 @@
  *   pai_matmul[_dev]      <- ndarray.dot of encrypted by plain (he_otp_lr_ft1/train.py:160,
  *                            he_otp_lr_ft2/train.py:188): per output sum_k c_ik (x) x_kj, i.e. __mul__ then
  *                            __add__ (encrypted_number.py:65-69, 86-113, 166-185)
+ *   pai_comm_* / pai_allgather_*  <- (no reference counterpart: the reference encrypts on one host's CPU
+ *                            pool, encryptor.py:71-97) reassembly of ciphertext shards encrypted on
+ *                            several GPUs, one RCCL all-gather over xGMI
  *
  * Conventions
  *   - Integers cross the boundary as little-endian bytes (key material) or little-endian 32-bit
@@ -46,6 +49,7 @@ extern "C" {
 #endif
 
 typedef struct pai_ctx pai_ctx;
+typedef struct pai_comm pai_comm;
 
 /* return codes */
 #define PAI_OK 0
@@ -193,6 +197,20 @@ int pai_segment_add_dev(pai_ctx* ctx, const uint32_t* d_ct, const int32_t* d_exp
                         const int64_t* seg_off, size_t nseg, uint32_t* d_out, int32_t* d_exp_out, void* stream);
 int pai_matmul_dev(pai_ctx* ctx, const uint32_t* d_ct, const int32_t* d_exp, size_t m, size_t K, int dtype,
                    const void* d_x, size_t d, uint32_t* d_out, int32_t* d_exp_out, void* stream);
+
+/* Multi-GPU: ciphertext shards -> every rank (RCCL, opened with dlopen on first use; one process per GPU).
+ * Rank 0 calls pai_comm_unique_id and hands the PAI_COMM_ID_BYTES bytes to the other ranks over any
+ * channel; every rank then calls pai_comm_create (collective). */
+#define PAI_COMM_ID_BYTES 128
+int pai_comm_unique_id(uint8_t* id_out);
+int pai_comm_create(const uint8_t* id, int world, int rank, int device, pai_comm** out);
+void pai_comm_destroy(pai_comm* comm);
+/* d_recv[r * bytes_per_rank ...] <- rank r's d_send; asynchronous on `stream` (a hipStream_t). */
+int pai_allgather_dev(pai_comm* comm, const void* d_send, size_t bytes_per_rank, void* d_recv, void* stream);
+/* Both halves of a ciphertext shard (words [n_per_rank][ct_words], exponents [n_per_rank]) in one grouped
+ * launch: d_ct_all [world * n_per_rank][ct_words], d_exp_all [world * n_per_rank]. */
+int pai_allgather_shards_dev(pai_comm* comm, const uint32_t* d_ct, const int32_t* d_exp, size_t n_per_rank,
+                             int ct_words, uint32_t* d_ct_all, int32_t* d_exp_all, void* stream);
 
 #ifdef __cplusplus
 }

@@ -62,3 +62,46 @@ def test_wire_errors_and_pickle(golden, monkeypatch):
     monkeypatch.setenv("FLEXPAI_PICKLE_PLAIN", "1")
     plain = pickle.loads(pickle.dumps(arr))
     assert type(plain) is np.ndarray and plain.dtype == object
+
+
+def test_lazy_from_wire_buffer_round_trip(golden):
+    """from_wire(lazy=True) -> CiphertextBuffer: the same words / exponents / flags / shape without objects;
+    its to_wire is byte-identical; to_array / from_array convert both ways; ciphertexts >= n^2 and rows
+    equal to n^2 are rejected (vectorised check)."""
+    from flex.crypto.paillier.cipher_array import from_wire, to_wire
+    from flex.crypto.paillier.cipher_buffer import CiphertextBuffer
+    arr, pk = _array(golden, (3, 4))
+    buf = to_wire(arr)
+    cb = from_wire(buf, pk, lazy=True)
+    assert isinstance(cb, CiphertextBuffer) and cb.shape == (3, 4) and cb.size == 12
+    assert cb.to_wire() == buf and to_wire(cb) == buf
+    assert CiphertextBuffer.from_array(arr).to_wire() == buf
+    back = cb.to_array()
+    assert back.shape == arr.shape
+    for a, b in zip(np.asarray(arr).reshape(-1), np.asarray(back).reshape(-1)):
+        assert (a.ciphertext(False), a.exponent, a._is_obfuscated()) == (b.ciphertext(False), b.exponent, b._is_obfuscated())
+    assert cb.reshape(12).shape == (12,) and cb.reshape(4, 3).to_wire() != buf
+    W = cb.words.shape[1]
+    nsq = pk.nsquare
+    for bad in (nsq, nsq + 1, (1 << (32 * W)) - 1):
+        t = bytearray(buf)
+        t[-4 * W:] = bad.to_bytes(4 * W, "little")
+        with pytest.raises(ValueError):
+            from_wire(bytes(t), lazy=True)
+    t = bytearray(buf)
+    t[-4 * W:] = (nsq - 1).to_bytes(4 * W, "little")
+    assert from_wire(bytes(t), lazy=True).size == 12
+    with pytest.raises(ValueError):
+        CiphertextBuffer(pk, cb.words[:, :-1], cb.exps)
+
+
+def test_buffer_operators_need_gpu_without_one(golden, monkeypatch):
+    from flex.crypto.paillier import _runtime
+    from flex.crypto.paillier.cipher_array import from_wire, to_wire
+    arr, pk = _array(golden, (5,))
+    cb = from_wire(to_wire(arr), lazy=True)
+    monkeypatch.setattr(_runtime, "gpu_available", lambda: False)
+    with pytest.raises(RuntimeError):
+        cb + cb
+    with pytest.raises(ValueError):
+        cb * cb

@@ -497,16 +497,27 @@ def main():
     if not args.no_host and solo and cfg_id in (1, 3):
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        hct, hex_, _ = ctx.encrypt(x_host, obf_mode=_native.PAI_OBF_RNG, rng_key=rng_key, index_base=index_base)
-        t_host = time.perf_counter() - t1
+        hct, hex_, hst = ctx.encrypt(x_host, obf_mode=_native.PAI_OBF_RNG, rng_key=rng_key, index_base=index_base)
+        t_fresh = time.perf_counter() - t1
+        t_host = float("inf")
+        for _ in range(2):                        # a streaming sender reuses its output buffers
+            t1 = time.perf_counter()
+            ctx.encrypt(x_host, obf_mode=_native.PAI_OBF_RNG, rng_key=rng_key, index_base=index_base,
+                        out=(hct, hex_, hst))
+            t_host = min(t_host, time.perf_counter() - t1)
         hb = {"host_buffers_encrypts_per_s": N / t_host,
+              "host_buffers_fresh_outputs_per_s": N / t_fresh,
               "host_buffers_note": "pai_encrypt: H2D float32 x, kernels, D2H ciphertext words "
-                                   f"({N * W * 4 / 2**20:.0f} MiB) into caller (pageable) memory",
+                                   f"({N * W * 4 / 2**20:.0f} MiB) through pinned staging into caller (pageable) "
+                                   "memory, chunks overlapped with the kernels; caller buffers reused (out=), "
+                                   "best of 2; fresh_outputs: new numpy arrays (page faults on first write)",
+              "host_vs_device": None,
               "host_buffers_bit_identical": bool(np.array_equal(hct[: len(ct_timed_check)], ct_timed_check))}
         from flex.crypto.paillier import _runtime
         from flex.crypto.paillier.encryptor import PaillierEncryptor
         _runtime.register_private(pk, sk)        # this process holds the key (CRT path, as above)
         enc = PaillierEncryptor(pk)
+        enc.encrypt(x_host[:4096])               # the runtime's own context + fixed-base tables: setup, untimed
         hs = min(args.host_sample, N)
         t1 = time.perf_counter()
         objs = enc.encrypt(x_host[:hs])
@@ -515,6 +526,25 @@ def main():
         hb["python_objects_note"] = (f"PaillierEncryptor.encrypt(ndarray[{hs}]) -> object ndarray of "
                                      "PaillierEncryptedNumber (encryptor.py:99-114 API), incl. materialisation")
         del objs
+        # object-free path (cipher_buffer.py): encrypt into words, serialise, receive without objects
+        from flex.crypto.paillier.cipher_array import from_wire
+        t1 = time.perf_counter()
+        buf = enc.encrypt_to_buffer(x_host)
+        t_buf = time.perf_counter() - t1
+        t1 = time.perf_counter()
+        wire = buf.to_wire()
+        t_wire = time.perf_counter() - t1
+        t1 = time.perf_counter()
+        back = from_wire(wire, pk, lazy=True)
+        t_recv = time.perf_counter() - t1
+        hb["buffer_encrypts_per_s"] = N / t_buf
+        hb["buffer_to_wire_per_s"] = N / t_wire
+        hb["buffer_from_wire_lazy_per_s"] = N / t_recv
+        hb["buffer_note"] = ("PaillierEncryptor.encrypt_to_buffer(ndarray[N]) -> CiphertextBuffer (words, no objects), "
+                             f".to_wire() ({len(wire) / 2**20:.0f} MiB), from_wire(lazy=True) incl. the < n^2 check")
+        hb["buffer_round_trip_identical"] = bool(np.array_equal(back.words, buf.words))
+        del buf, back, wire
+        hb["host_vs_device"] = hb["host_buffers_encrypts_per_s"] / value
         extra["host_boundary"] = hb
 
     if rank != 0:

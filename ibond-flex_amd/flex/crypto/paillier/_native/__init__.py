@@ -288,7 +288,10 @@ class Context:
     # ----------------------------------------------------------------- host-buffer ops
     def encrypt(self, x: np.ndarray, exp_mode: int = PAI_EXP_AUTO, fixed_exp: int = 0,
                 obf_mode: int = PAI_OBF_RNG, r: Optional[Sequence[int]] = None, r_scalar: Optional[int] = None,
-                rng_key: Optional[bytes] = None, index_base: int = 0) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+                rng_key: Optional[bytes] = None, index_base: int = 0,
+                out: Optional[Tuple[np.ndarray, np.ndarray, np.ndarray]] = None) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Host buffers in and out. `out` = (ct [N, W] uint32, exp [N] int32, status [N] int32) to reuse
+        caller buffers (a streaming sender's), else fresh arrays."""
         x = np.ascontiguousarray(x)
         if x.dtype == np.float32:
             dt = PAI_F32
@@ -299,9 +302,16 @@ class Context:
         else:
             raise TypeError(f"unsupported dtype {x.dtype}")
         N = x.size
-        ct = np.empty((N, self.ct_words), dtype=np.uint32)
-        ex = np.empty(N, dtype=np.int32)
-        st = np.empty(N, dtype=np.int32)
+        if out is not None:
+            ct, ex, st = out
+            if not (ct.dtype == np.uint32 and ct.shape == (N, self.ct_words) and ct.flags.c_contiguous and
+                    ex.dtype == np.int32 and ex.shape == (N,) and ex.flags.c_contiguous and
+                    st.dtype == np.int32 and st.shape == (N,) and st.flags.c_contiguous):
+                raise ValueError("out must be C-contiguous (uint32 [N, ct_words], int32 [N], int32 [N])")
+        else:
+            ct = np.empty((N, self.ct_words), dtype=np.uint32)
+            ex = np.empty(N, dtype=np.int32)
+            st = np.empty(N, dtype=np.int32)
         r_buf, r_stride, r_bytes = None, 0, 0
         if obf_mode == PAI_OBF_GIVEN:
             r_bytes = self.ct_words * 4

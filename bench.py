@@ -151,8 +151,11 @@ def main():
     ap.add_argument("--path", choices=("crt", "public"), default="crt")
     ap.add_argument("--obf", choices=("fixedbase", "generic"), default="fixedbase",
                     help="device-RNG sampler of r^n on the CRT path (kernels_fb.hpp vs r from ChaCha20)")
-    ap.add_argument("--fb-window", type=int, default=20, choices=(8, 12, 16, 20),
-                    help="digit window of the fixed-base tables (20: 52 products per half, 13.4 GB per half)")
+    ap.add_argument("--fb-window", type=int, default=22, choices=(8, 12, 16, 20, 22, 23, 24),
+                    help="largest digit window of the fixed-base tables; the library takes the largest one <= this "
+                         "whose tables fit the free HBM (nb = 2048: W = 22, 47 products per half, 2 x 50.5 GB; "
+                         "nb = 4096: W = 20, 103 products per half, 2 x 63.9 GB). W = 23 (2 x 96.6 GB) measured "
+                         "only 0.8 %% faster than 22 at nb = 2048 (TLB reach), so 22 is the default")
     ap.add_argument("--cpu-sample", type=int, default=16384)
     ap.add_argument("--cpu-threads", type=int, default=os.cpu_count() or 1,
                     help="threads of the GMP CPU baseline (default os.cpu_count(), like the reference's Pool)")
@@ -214,7 +217,7 @@ def main():
     grp_fb = use_fb and not use_crt          # 4096-bit keys: k_fb_digits, k_fbg, k_crt_fin<8>
     fb_info = None
     if use_fb:
-        ctx.set_fb_window(args.fb_window)     # a dedicated encrypt GPU: 2 x 13.4 GB of tables at W = 20
+        ctx.set_fb_window(args.fb_window)     # a dedicated encrypt GPU: the largest tables that fit its HBM
         t0 = time.perf_counter()
         try:
             ctx.prepare_fixed_base()

@@ -1,6 +1,7 @@
 // flexpai: host context + C ABI for the MI355X Paillier engine (see include/flexpai.h).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -460,10 +461,13 @@ static int upload_fb(pai_ctx* c, const std::vector<T>& v, T** out) {
   return 0;
 }
 
+// Digit windows the table builder supports (lo/hi half-digit tables of at most FB_LO entries)
+static bool fb_window_ok(int w) { return w == 8 || w == 12 || w == 16 || w == 20 || w == 22 || w == 23 || w == 24; }
+
 static int fb_default_window() {
   const char* e = getenv("FLEXPAI_FB_WINDOW");
   const int w = e ? atoi(e) : 16;
-  return (w == 8 || w == 12 || w == 16 || w == 20) ? w : 16;
+  return fb_window_ok(w) ? w : 16;
 }
 
 // 32-bit words of one table row: packed words for the lane kernels, S canonical limbs for the group kernel
@@ -526,7 +530,7 @@ static int ensure_fb(pai_ctx* c) {
   if (!c->fb_W) c->fb_W = fb_default_window();
   const uint64_t budget = fb_budget(c);
   int W = 0;
-  for (int w : {20, 16, 12, 8})
+  for (int w : {24, 23, 22, 20, 16, 12, 8})
     if (w <= c->fb_W && fb_bytes(c, w) <= budget) {
       W = w;
       break;
@@ -544,6 +548,7 @@ static int ensure_fb(pai_ctx* c) {
   std::memset(red, 0, sizeof(red));
   int rc;
   void* t[2] = {nullptr, nullptr};
+  void* lohi[2] = {nullptr, nullptr};
   for (int h = 0; h < 2; ++h) {
     if (!c->fb_g[h] && !(c->fb_g[h] = fb_base(primes[h]))) return fb_unavailable(c, "no base found");
     const HBig& m2 = sq[h];
@@ -577,9 +582,12 @@ static int ensure_fb(pai_ctx* c) {
     if ((rc = upload_fb(c, m2.limbs(sb, LB), &dm)) ||
         (rc = upload_fb(c, mul_pow2_mod(HBig(1), 2 * RB, m2).limbs(sb, LB), &dR2)) ||
         (rc = upload_fb(c, mul_pow2_mod(HBig(1), RB, m2).limbs(sb, LB), &done)) || (rc = upload_fb(c, bl, &dbases)) ||
-        (rc = upload_fb(c, std::vector<uint32_t>((size_t)K * 2 * FB_LO * sb, 0u), &dlohi)) ||
         (rc = upload_fb(c, nm, &dnm)) || (rc = upload_fb(c, mul(m2, pow2(PB)).limbs(sb, LB), &dpbig)))
       return fb_unavailable(c, pai_last_error());
+    // lo/hi half-digit tables: build scratch only, released once the table is filled
+    if (hipMalloc(&lohi[h], (size_t)K * 2 * FB_LO * sb * 4) != hipSuccess) return fb_unavailable(c, "table allocation failed");
+    c->fb_mem.push_back(lohi[h]);
+    dlohi = (uint32_t*)lohi[h];
     if (hipMalloc(&t[h], ((size_t)K << W) * (TW / 4) * sizeof(uint4)) != hipSuccess)
       return fb_unavailable(c, "table allocation failed");
     c->fb_mem.push_back(t[h]);
@@ -612,6 +620,10 @@ static int ensure_fb(pai_ctx* c) {
                             : fb_build_tables(sb, c->d_fb_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
   if (be != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return fb_unavailable(c, "table construction failed");
+  for (void* p : lohi) {
+    c->fb_mem.erase(std::find(c->fb_mem.begin(), c->fb_mem.end(), p));
+    (void)hipFree(p);
+  }
   const auto t2 = std::chrono::steady_clock::now();
   c->fb_host_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
   c->fb_dev_ms = std::chrono::duration<float, std::milli>(t2 - t1).count();
@@ -838,8 +850,7 @@ int pai_ctx_set_option(pai_ctx* c, int option, int value) {
     case PAI_OPT_LANE_DECRYPT: c->dec_lane_enabled = value != 0; return 0;
     case PAI_OPT_FIXED_BASE: c->fb_enabled = value != 0; return 0;
     case PAI_OPT_FB_WINDOW:
-      if (value != 8 && value != 12 && value != 16 && value != 20)
-        return fail(PAI_ERR_ARG, "fixed-base window must be 8, 12, 16 or 20");
+      if (!fb_window_ok(value)) return fail(PAI_ERR_ARG, "fixed-base window must be 8, 12, 16, 20, 22, 23 or 24");
       if (value == c->fb_W) return 0;
       c->fb_W = value;
       HIPCHK(hipSetDevice(c->device));

@@ -39,7 +39,7 @@ namespace fpai {
 constexpr uint32_t FB_NONCE = 0x66786230u;   // ChaCha20 nonce word 2 (+ half) of the exponent stream
 constexpr int FB_RAW_MAX = 80;               // words of the raw exponent per element (5 ChaCha blocks)
 constexpr int FB_DIG_BLOCK = 128;            // threads per block of k_fb_digits
-constexpr int FB_LO = 1024;                  // entries of the per-position small tables (k_fb_lohi): W <= 20
+constexpr int FB_LO = 4096;                  // entries of the per-position small tables (k_fb_lohi): W <= 24
 
 // Compile-time geometry per lane size SB (limbs of p_h^2): TW = 32-bit words per table row (the
 // canonical values are < p_h^2 < 2^(32 TW)); c0 = 1 + n M is folded in as NC chunks of CB bits of |M|,

@@ -225,6 +225,36 @@ __device__ __forceinline__ void emit_words(uint32_t* slot, const uint32_t (&x)[L
   wave_lds_fence();
 }
 
+// Inverse of emit_words for a ciphertext-sized operand: the group copies `nwords` words (16-byte aligned,
+// nwords % 4 == 0, nwords + 2 <= S) into its LDS slot with 16-byte loads, then each lane cuts its L limbs
+// out of the slot (two words and one alignbit per limb). Used inside step loops, where the per-limb,
+// bounds-checked word loads of words_to_limbs (74 scalar loads, 37 branches) spill registers.
+template <int TPI>
+__device__ __forceinline__ void stage_words_to_limbs(uint32_t* slot, const uint32_t* __restrict__ src, int nwords,
+                                                     uint32_t (&x)[L], int tig) {
+  const uint4* s4 = reinterpret_cast<const uint4*>(src);
+  uint4* d4 = reinterpret_cast<uint4*>(slot);
+  wave_lds_fence();                                   // earlier readers of the slot are done
+  for (int q = tig; q < nwords / 4; q += TPI) d4[q] = s4[q];
+  if (tig == 0) {
+    slot[nwords] = 0u;
+    slot[nwords + 1] = 0u;
+  }
+  wave_lds_fence();
+  // opaque copy: stops LICM from hoisting the L per-limb (word index, shift) pairs out of the caller's
+  // step loop, which would pin ~2L VGPRs for the whole kernel
+  int t = tig;
+  asm volatile("" : "+v"(t));
+  const int base = t * L * LB;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int bit = base + i * LB, j = bit >> 5;
+    const uint32_t lo = j < nwords + 2 ? slot[j] : 0u, hi = j + 1 < nwords + 2 ? slot[j + 1] : 0u;
+    x[i] = __builtin_amdgcn_alignbit(hi, lo, bit & 31) & LMASK;
+  }
+  wave_lds_fence();                                   // the slot is rewritten next (write_limbs_lds)
+}
+
 // ================================================================= encrypt
 // PaillierEncryptor.encrypt over an array (encryptor.py:71-114): encode -> c0 -> c0 * r^n mod n^2.
 // The op list (host: build_encrypt_program) computes r~ = r R, the odd powers r~^1..r~^31 into
@@ -404,7 +434,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_add(AddParams p) {
     bool done = empty;
     if (!empty) {
       while (add_exp(p, add_src(p, el, jc)) != cur) ++jc;
-      words_to_limbs(p.cts + add_src(p, el, jc) * p.ct_words, p.ct_words, a, tig);   // rho = 0
+      stage_words_to_limbs<TPI>(slot, p.cts + add_src(p, el, jc) * p.ct_words, p.ct_words, a, tig);   // rho = 0
       ++jc;
       mcount = 1;
     } else {
@@ -456,7 +486,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_add(AddParams p) {
       {
         const uint32_t* src = op == 1 ? p.cts + osrc * p.ct_words : p.RS + (size_t)s * p.ct_words;
         uint32_t t[L];
-        words_to_limbs(src, p.ct_words, t, tig);
+        stage_words_to_limbs<TPI>(slot, src, p.ct_words, t, tig);
 #pragma unroll
         for (int i = 0; i < L; ++i) t[i] = op == 0 ? a[i] : t[i];
         write_limbs_lds<TPI>(slot, t, tig);

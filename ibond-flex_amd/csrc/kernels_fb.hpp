@@ -281,14 +281,21 @@ __device__ __forceinline__ void fbw_mont_mul(uint32_t (&a)[S], uint32_t addr, co
   lane::normalize<S>(P, a);
 }
 
-// DMA table row `row` -> LDS buffer (the wave's 64-lane slice of each quad row)
+// DMA table row `row` -> LDS buffer (the wave's 64-lane slice of each quad row). The LDS destination of
+// each instruction (M0) is formed right here from one scalar base: left to the compiler, the TQ constant
+// destinations are precomputed once, spilled under the product's register pressure and reloaded with a
+// vmcnt(0) wait before every DMA instruction -- serialising the row stream.
 template <int TQ>
 __device__ __forceinline__ void fb_row_to_lds(const uint4* __restrict__ table, size_t row, uint4* wave_row0) {
+  typedef __attribute__((address_space(3))) uint4 lds_uint4;
   const uint4* r = table + row * TQ;   // quad g at an immediate offset
+  const uint32_t lb = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds_uint4*)wave_row0);
 #pragma unroll
-  for (int g = 0; g < TQ; ++g)
-    __builtin_amdgcn_global_load_lds((const void*)(r + g),
-                                     (__attribute__((address_space(3))) void*)(wave_row0 + g * LANE_BLOCK), 16, 0, 0);
+  for (int g = 0; g < TQ; ++g) {
+    uint32_t dst = lb + (uint32_t)(g * LANE_BLOCK * 16);
+    asm volatile("" : "+s"(dst));
+    __builtin_amdgcn_global_load_lds((const void*)(r + g), (__attribute__((address_space(3))) void*)(size_t)dst, 16, 0, 0);
+  }
 }
 
 // 32-bit word WI of a number held as S canonical 28-bit limbs (4 WI mod 28 <= 24: two limbs suffice)

@@ -462,7 +462,7 @@ static int upload_fb(pai_ctx* c, const std::vector<T>& v, T** out) {
 }
 
 // Digit windows the table builder supports (lo/hi half-digit tables of at most FB_LO entries)
-static bool fb_window_ok(int w) { return w == 8 || w == 12 || w == 16 || w == 20 || w == 22 || w == 23 || w == 24; }
+static bool fb_window_ok(int w) { return w == 8 || w == 12 || w == 16 || (w >= 20 && w <= 24); }
 
 static int fb_default_window() {
   const char* e = getenv("FLEXPAI_FB_WINDOW");
@@ -530,7 +530,7 @@ static int ensure_fb(pai_ctx* c) {
   if (!c->fb_W) c->fb_W = fb_default_window();
   const uint64_t budget = fb_budget(c);
   int W = 0;
-  for (int w : {24, 23, 22, 20, 16, 12, 8})
+  for (int w : {24, 23, 22, 21, 20, 16, 12, 8})
     if (w <= c->fb_W && fb_bytes(c, w) <= budget) {
       W = w;
       break;
@@ -850,7 +850,7 @@ int pai_ctx_set_option(pai_ctx* c, int option, int value) {
     case PAI_OPT_LANE_DECRYPT: c->dec_lane_enabled = value != 0; return 0;
     case PAI_OPT_FIXED_BASE: c->fb_enabled = value != 0; return 0;
     case PAI_OPT_FB_WINDOW:
-      if (!fb_window_ok(value)) return fail(PAI_ERR_ARG, "fixed-base window must be 8, 12, 16, 20, 22, 23 or 24");
+      if (!fb_window_ok(value)) return fail(PAI_ERR_ARG, "fixed-base window must be 8, 12, 16 or 20 .. 24");
       if (value == c->fb_W) return 0;
       c->fb_W = value;
       HIPCHK(hipSetDevice(c->device));

@@ -91,7 +91,7 @@ typedef struct pai_comm pai_comm;
                                     r^n through fixed bases (G_p^a_p, G_q^a_q: same distribution as
                                     r^n for uniform r, see pai_ctx_fixed_base_info); 0: r from the
                                     ChaCha20 stream and r^n by exponentiation. Read back: 1 when used */
-#define PAI_OPT_FB_WINDOW 6      /* digit window of the fixed-base tables: 8, 12, 16, 20, 22, 23 or 24 bits (default 16, or
+#define PAI_OPT_FB_WINDOW 6      /* digit window of the fixed-base tables: 8, 12, 16 or 20 .. 24 bits (default 16, or
                                     $FLEXPAI_FB_WINDOW); setting it drops the tables (rebuilt lazily). Read
                                     back: the window of the resident tables, which is the largest one <= the
                                     requested window whose 2 K 2^W rows fit $FLEXPAI_FB_MAX_BYTES (default:

@@ -116,12 +116,14 @@ def work_add(exps: "torch.Tensor", nb: int) -> float:
     return float((n * (k - 1) + sq) * _M(nb // 16))
 
 
-def load_traffic(kernel: str, n: int, nb: int):
+def load_traffic(kernel: str, n: int, nb: int, window=None):
+    """Measured HBM bytes per launch of `kernel` (profiles/pmc_<kernel>_latest.json, tools/pmc_traffic.py),
+    only when that profile was taken at the same size, key and fixed-base window."""
     path = os.path.join(ROOT, "profiles", f"pmc_{kernel}_latest.json")
     try:
         with open(path) as f:
             pm = json.load(f)
-        if pm.get("n") == n and pm.get("nb") == nb:
+        if pm.get("n") == n and pm.get("nb") == nb and pm.get("window") == window:
             return pm.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -662,7 +664,7 @@ def main():
                    "elements_per_gpu": N, "parallelism": f"dp{world}"},
         "roofline": {"bound": "valu-int-mac", "achieved": achieved / 1e12, "peak": INT_MAC_PEAK / 1e12,
                      "unit": "TMAC/s", "frac": achieved / INT_MAC_PEAK,
-                     "traffic": load_traffic(dom, N, nb),
+                     "traffic": load_traffic(dom, N, nb, fb_info[3] if (use_fb and dom in ("k_fb", "k_fbg")) else None),
                      "kernel": dom, "kernel_ms": dom_ms,
                      "work_per_unit": (f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} table "
                                        f"products per half, 32-bit limbs, kernels_fb.hpp), not SURVEY.md §8d's W_enc"

@@ -23,7 +23,8 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/pmc2_$c -o run -- python3 $R/bench.py --config 2 --steps 1 --warmup 0 --no-cpu-baseline --no-public > $O/pmc2_$c.log 2>&1 || { echo "pmc2 $c failed rc=$?"; tail -20 $O/pmc2_$c.log; exit 1; }
 done
 cd $R
-for k in k_fb k_fb_fin k_fb_digits; do
+python3 tools/pmc_traffic.py $O/pmc_FETCH_SIZE/run_counter_collection.csv $O/pmc_WRITE_SIZE/run_counter_collection.csv --kernel k_fb --n 1048576 --nb 2048 --window 22 -o $O/pmc_k_fb_latest.json || exit 1
+for k in k_fb_fin k_fb_digits; do
   python3 tools/pmc_traffic.py $O/pmc_FETCH_SIZE/run_counter_collection.csv $O/pmc_WRITE_SIZE/run_counter_collection.csv --kernel $k --n 1048576 --nb 2048 -o $O/pmc_${k}_latest.json || exit 1
 done
 python3 tools/pmc_traffic.py $O/pmc2_FETCH_SIZE/run_counter_collection.csv $O/pmc2_WRITE_SIZE/run_counter_collection.csv --kernel k_add --n 1048576 --nb 2048 -o $O/pmc_k_add_latest.json || exit 1

@@ -15,7 +15,8 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $O/pmc4_$c -o run -- python3 $R/bench.py --config 4 --steps 1 --warmup 0 --no-cpu-baseline --no-decrypt --no-public > $O/pmc4_$c.log 2>&1 || { echo "pmc $c failed rc=$?"; tail -20 $O/pmc4_$c.log; exit 1; }
 done
 cd $R
-for k in k_fbg k_crt_fin k_fb_digits; do
+python3 tools/pmc_traffic.py $O/pmc4_FETCH_SIZE/run_counter_collection.csv $O/pmc4_WRITE_SIZE/run_counter_collection.csv --kernel k_fbg --n 4194304 --nb 4096 --window 21 -o $O/pmc_k_fbg_latest.json || exit 1
+for k in k_crt_fin k_fb_digits; do
   python3 tools/pmc_traffic.py $O/pmc4_FETCH_SIZE/run_counter_collection.csv $O/pmc4_WRITE_SIZE/run_counter_collection.csv --kernel $k --n 4194304 --nb 4096 -o $O/pmc_${k}_4096_latest.json || exit 1
 done
 echo ALLDONE

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--kernel", default="k_encrypt")
     ap.add_argument("--n", type=int, required=True)
     ap.add_argument("--nb", type=int, required=True)
+    ap.add_argument("--window", type=int, default=None, help="fixed-base digit window of the run (fixed-base kernels)")
     ap.add_argument("-o", default=None, help="default: profiles/pmc_<kernel>_latest.json (read by bench.py)")
     a = ap.parse_args()
     if a.o is None:
@@ -40,7 +41,7 @@ def main():
                            f"pmc_{a.kernel}_latest.json")
     f, nf = per_launch(a.fetch_csv, "FETCH_SIZE", a.kernel)
     w, nw = per_launch(a.write_csv, "WRITE_SIZE", a.kernel)
-    out = {"kernel": a.kernel, "n": a.n, "nb": a.nb,
+    out = {"kernel": a.kernel, "n": a.n, "nb": a.nb, "window": a.window,
            "fetch_size_kib_raw": f, "write_size_kib_raw": w, "launches": [nf, nw],
            "hbm_read_bytes_per_launch": 2 * f * 1024, "hbm_write_bytes_per_launch": w * 1024,
            "hbm_bytes_per_launch": (2 * f + w) * 1024,

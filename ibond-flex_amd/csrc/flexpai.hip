@@ -113,8 +113,11 @@ struct pai_ctx {
   int cus = 0;
   // optional per-stage timing of the last encrypt call (PAI_OPT_STAGE_TIMING)
   bool timing = false;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  int nev = 0;
+  // HIP events between the kernels of each chunk of the last encrypt / decrypt call; the stage times
+  // are summed over its chunks (a call of more than CRT_CHUNK elements runs several)
+  static constexpr int EV_CHUNKS = 64;
+  hipEvent_t ev[EV_CHUNKS][4] = {};
+  int nev = 0, nchunk_ev = 0;
   // host-buffer entry points (pai_encrypt / pai_decrypt / pai_add): device copies of the operands, a
   // compute and a copy stream, one event per chunk (host_pipe below)
   void* d_hostio = nullptr;
@@ -125,8 +128,9 @@ struct pai_ctx {
   size_t pin_bytes = 0;
   ~pai_ctx() {
     (void)hipSetDevice(device);
-    for (auto& e : ev)
-      if (e) (void)hipEventDestroy(e);
+    for (auto& ch : ev)
+      for (auto& e : ch)
+        if (e) (void)hipEventDestroy(e);
     for (auto& e : hev) (void)hipEventDestroy(e);
     for (auto& e : pev) (void)hipEventDestroy(e);
     for (void* p : h_pin)
@@ -306,11 +310,25 @@ static int ensure_work(pai_ctx* c, size_t bytes) {
   return 0;
 }
 
+static void stage_reset(pai_ctx* c) {
+  c->nev = 0;
+  c->nchunk_ev = 0;
+}
+// The events of a new chunk (nullptr when timing is off or the call has more than EV_CHUNKS chunks)
+static hipEvent_t* stage_chunk(pai_ctx* c) {
+  if (!c->timing || c->nchunk_ev >= pai_ctx::EV_CHUNKS) return nullptr;
+  hipEvent_t* e = c->ev[c->nchunk_ev++];
+  for (int i = 0; i < 4; ++i)
+    if (!e[i]) (void)hipEventCreate(&e[i]);
+  return e;
+}
+// mark i (0..3) of the current chunk; mark 0 opens a new chunk
 static void stage_mark(pai_ctx* c, int i, hipStream_t st) {
   if (!c->timing || i >= 4) return;
-  if (!c->ev[i]) (void)hipEventCreate(&c->ev[i]);
-  (void)hipEventRecord(c->ev[i], st);
-  c->nev = i + 1;
+  if (i == 0 && !stage_chunk(c)) return;
+  if (c->nchunk_ev == 0) return;
+  (void)hipEventRecord(c->ev[c->nchunk_ev - 1][i], st);
+  c->nev = std::max(c->nev, i + 1);
 }
 
 template <typename K>
@@ -846,7 +864,7 @@ int pai_ctx_set_option(pai_ctx* c, int option, int value) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
   switch (option) {
     case PAI_OPT_CRT_ENCRYPT: c->crt_enabled = value != 0; return 0;
-    case PAI_OPT_STAGE_TIMING: c->timing = value != 0; c->nev = 0; return 0;
+    case PAI_OPT_STAGE_TIMING: c->timing = value != 0; stage_reset(c); return 0;
     case PAI_OPT_LANE_DECRYPT: c->dec_lane_enabled = value != 0; return 0;
     case PAI_OPT_FIXED_BASE: c->fb_enabled = value != 0; return 0;
     case PAI_OPT_FB_WINDOW:
@@ -881,11 +899,18 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
 int pai_ctx_stage_times(pai_ctx* c, float* ms_out, int max_out, int* count) {
   if (!c || !count) return fail(PAI_ERR_ARG, "null argument");
   *count = 0;
-  if (c->nev < 2) return 0;
+  if (c->nev < 2 || c->nchunk_ev < 1) return 0;
   HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipEventSynchronize(c->ev[c->nev - 1]));
+  HIPCHK(hipEventSynchronize(c->ev[c->nchunk_ev - 1][c->nev - 1]));
   const int k = std::min(c->nev - 1, max_out);
-  for (int i = 0; i < k; ++i) HIPCHK(hipEventElapsedTime(&ms_out[i], c->ev[i], c->ev[i + 1]));
+  for (int i = 0; i < k; ++i) {
+    ms_out[i] = 0.f;
+    for (int ch = 0; ch < c->nchunk_ev; ++ch) {
+      float t = 0.f;
+      HIPCHK(hipEventElapsedTime(&t, c->ev[ch][i], c->ev[ch][i + 1]));
+      ms_out[i] += t;
+    }
+  }
   *count = k;
   return 0;
 }
@@ -1145,6 +1170,7 @@ int pai_encrypt_dev(pai_ctx* c, int dtype, const void* d_x, size_t N, int exp_mo
   if (obf_mode == PAI_OBF_RNG && !rng_key32) return fail(PAI_ERR_ARG, "pai_encrypt_dev: rng key required");
   if (obf_mode < 0 || obf_mode > 2) return fail(PAI_ERR_ARG, "pai_encrypt_dev: bad obf_mode");
   HIPCHK(hipSetDevice(c->device));
+  stage_reset(c);
   EncParams p{};
   p.x = d_x;
   p.dtype = dtype;
@@ -1276,16 +1302,10 @@ static int launch_dec_lane(pai_ctx* c, const DecParams& d, hipStream_t st) {
   if (rc) return rc;
   const int SB = c->crt_sb;
   if ((rc = ensure_work(c, (size_t)2 * SB * chunk * 4))) return rc;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  if (c->timing) {
-    for (int i = 0; i < 4; ++i) {
-      if (!c->ev[i]) HIPCHK(hipEventCreate(&c->ev[i]));
-      ev[i] = c->ev[i];
-    }
-    c->nev = 4;
-  }
   for (long long off = 0; off < N; off += chunk) {
     const long long n = std::min(chunk, N - off);
+    hipEvent_t* ev = stage_chunk(c);
+    if (ev) c->nev = 4;
     uint32_t* xw = (uint32_t*)c->d_work;   // [2][SB][n]: c~, then x_h in place
     DecPreParams pre{c->d_dec_halves, n, d.ct + (size_t)off * c->ct_words, c->ct_words, c->dec_kchunks, xw};
     CrtParams pw{};
@@ -1322,6 +1342,7 @@ int pai_decrypt_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size
   if (N == 0) return 0;
   if (!d_ct || !d_exp || !d_val || !d_status) return fail(PAI_ERR_ARG, "pai_decrypt_dev: bad arguments");
   HIPCHK(hipSetDevice(c->device));
+  stage_reset(c);
   DecParams p{};
   p.ct = d_ct;
   p.exp = d_exp;

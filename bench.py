@@ -97,10 +97,10 @@ def work_fb(nb: int, digits: int) -> dict:
 
 def work_fbg(nb: int, digits: int) -> dict:
     """Per-element MACs of the 4096-bit key holder's fixed-base path (kernels_grp.hpp), counted like work_fb:
-    k_fbg = K table products mod p_h^2 per half plus the coefficient product; k_crt_fin<8> = three products
-    mod n^2 (u_p q^2, u_q p^2, times c0)."""
+    k_fbg = K table products mod p_h^2 per half (c0 folded into the first); Garner = one product mod p^2
+    (k_fbg_garner) + one product mod n^2 (k_fbg_fin), timed together."""
     s = nb // 32
-    return {"k_fb_digits": 0.0, "k_fbg": float(2 * (digits + 1) * _M(s)), "k_crt_fin": float(3 * _M(nb // 16))}
+    return {"k_fb_digits": 0.0, "k_fbg": float(2 * digits * _M(s)), "k_fbg_fin": float(_M(s) + _M(nb // 16))}
 
 
 def work_dec(nb: int) -> float:
@@ -216,7 +216,7 @@ def main():
     ctx.set_crt(holder)
     use_fb = holder and args.obf == "fixedbase" and ctx.fixed_base
     ctx.set_fixed_base(use_fb)
-    grp_fb = use_fb and not use_crt          # 4096-bit keys: k_fb_digits, k_fbg, k_crt_fin<8>
+    grp_fb = use_fb and not use_crt          # 4096-bit keys: k_fb_digits, k_fbg, k_fbg_garner + k_fbg_fin
     fb_info = None
     if use_fb:
         ctx.set_fb_window(args.fb_window)     # a dedicated encrypt GPU: the largest tables that fit its HBM
@@ -566,7 +566,7 @@ def main():
         extra["k_add_ms"] = add_ms
     else:
         if grp_fb:
-            names, works = ["k_fb_digits", "k_fbg", "k_crt_fin"], work_fbg(nb, fb_info[2])
+            names, works = ["k_fb_digits", "k_fbg", "k_fbg_fin"], work_fbg(nb, fb_info[2])
         elif use_crt and use_fb:
             names, works = ["k_fb_digits", "k_fb", "k_fb_fin"], work_fb(nb, fb_info[2])
         elif use_crt:

@@ -9,6 +9,9 @@ constexpr int GRP_TPI = 4;                  // S = 148 limbs: p_h^2 of a 4096-bi
 int grp_occupancy(int* occ_fb);
 // launches on grid (gx, 2): blockIdx.y = half
 hipError_t grp_launch_fb(const FbParams& p, int gx, hipStream_t st);
+hipError_t grp_launch_garner(const FbgGarnerParams& p, int gx, hipStream_t st);
+hipError_t grp_launch_fin(const FbgFinParams& p, int gx, hipStream_t st);   // TPI 8 (n^2 of a 4096-bit key)
+int grp_fin_occupancy(int* occ_garner, int* occ_fin);
 hipError_t grp_build_tables(const FbHalf* d_halves, uint32_t* t0, uint32_t* t1, int K, int W, hipStream_t st);
 size_t grp_lds_bytes();
 

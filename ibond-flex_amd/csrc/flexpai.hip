@@ -85,6 +85,7 @@ struct pai_ctx {
   FbHalf* d_fb_halves = nullptr;
   FbRed* d_fb_red = nullptr;
   uint32_t *d_fb_m8 = nullptr, *d_fb_coefR = nullptr, *d_fb_q2 = nullptr, *d_fb_m0 = nullptr;
+  uint32_t* d_fb_q2Rn = nullptr;  // 4096-bit keys: q^2 R mod n^2 (k_fbg_fin)
   uint32_t fb_mprime0 = 0;      // p^2 (Garner)
   uint32_t fb_g[2] = {0, 0};   // the bases g_p, g_q (generators of Z_p*, Z_q*)
   std::vector<void*> fb_mem;    // tables and their constants (rebuilt when the window changes)
@@ -579,17 +580,12 @@ static int ensure_fb(pai_ctx* c) {
       std::copy(v.begin(), v.end(), bl.begin() + (size_t)k * sb);
       for (int q = 0; q < W; ++q) x = M2.mul(x, x);
     }
-    // c0 folding: n 2^(CB c) mod p_h^2 (c < NC) and 2^PB p_h^2; the group kernel instead finishes with
-    // the CRT coefficient (other^2)^-1 mod p_h^2 and leaves c0 to k_crt_fin
+    // c0 folding: n 2^(CB c) mod p_h^2 (c < NC) and 2^PB p_h^2 (the group kernel uses 74's geometry:
+    // 16-bit chunks, PB = 20)
     std::vector<uint32_t> nm;
-    int PB = 0;
-    if (grp) {
-      const HBig coef = inv_mod(sq[1 - h], m2);
-      if (coef.is_zero()) return fb_unavailable(c, "p^2, q^2 not coprime");
-      nm = coef.limbs(sb, LB);
-    } else {
-      const int CB = sb == 37 ? FbGeom<37>::CB : FbGeom<74>::CB, NC = sb == 37 ? FbGeom<37>::NC : FbGeom<74>::NC;
-      PB = sb == 37 ? FbGeom<37>::PB : FbGeom<74>::PB;
+    const int CB = sb == 37 ? FbGeom<37>::CB : FbGeom<74>::CB, NC = sb == 37 ? FbGeom<37>::NC : FbGeom<74>::NC;
+    const int PB = sb == 37 ? FbGeom<37>::PB : FbGeom<74>::PB;
+    {
       const HBig nmod = mod(c->n, m2);
       for (int k = 0; k < NC; ++k) {
         const std::vector<uint32_t> v = mul_pow2_mod(nmod, (size_t)CB * k, m2).limbs(sb, LB);
@@ -631,7 +627,8 @@ static int ensure_fb(pai_ctx* c) {
   if ((rc = upload_fb(c, v, &c->d_fb_halves)) || (rc = upload_fb(c, vr, &c->d_fb_red)) ||
       (rc = upload_fb(c, mul(sq[0], HBig(8)).limbs(sb, LB), &c->d_fb_m8)) ||
       (rc = upload_fb(c, mul_pow2_mod(coef, RB, sq[0]).limbs(sb, LB), &c->d_fb_coefR)) ||
-      (rc = upload_fb(c, sq[1].limbs(sb, LB), &c->d_fb_q2)))
+      (rc = upload_fb(c, sq[1].limbs(sb, LB), &c->d_fb_q2)) ||
+      (grp && (rc = upload_fb(c, mul_pow2_mod(sq[1], (size_t)LB * c->S_e, c->N).limbs(c->S_e, LB), &c->d_fb_q2Rn))))
     return fb_unavailable(c, pai_last_error());
   const auto t1 = std::chrono::steady_clock::now();
   const hipError_t be = grp ? grp_build_tables(c->d_fb_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
@@ -1040,25 +1037,14 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     stage_mark(c, 2, st);
     c->fb_last_w = w;
     c->fb_last_n = n;
-    if (grp) {   // u_h = G_h^(a_h) coef_h mod p_h^2 -> c = (u_p q^2 + u_q p^2) c0 mod n^2 (kernels_crt.hpp)
-      CrtFinParams f{};
-      f.x = pf.x;
-      f.dtype = e.dtype;
-      f.exp_mode = e.exp_mode;
-      f.fexp = e.fexp;
-      f.u = w;
-      f.sb = SB;
-      f.n = n;
-      f.N = c->d_N;
-      f.nl = c->d_nl;
-      f.kq = c->d_kq;
-      f.kp = c->d_kp;
-      f.mprime = c->mprime_N;
-      f.ct = e.ct + (size_t)off * c->ct_words;
-      f.exp = pf.exp;
-      f.status = pf.status;
-      f.ct_words = c->ct_words;
-      if ((rc = launch_crt_fin<8>(c, f, st))) return rc;
+    if (grp) {   // w_h = c0 G_h^(a_h) mod p_h^2 -> Garner: h mod p^2 (S = 148), c = w_q + q^2 h mod n^2 (S = 296)
+      int occH = 1, occC = 1;
+      grp_fin_occupancy(&occH, &occC);
+      const long long gb4 = (n + BLOCK / GRP_TPI - 1) / (BLOCK / GRP_TPI), gb8 = (n + BLOCK / 8 - 1) / (BLOCK / 8);
+      FbgGarnerParams gh{w, n, c->d_fb_m0, c->d_fb_m8, c->d_fb_coefR, c->fb_mprime0};
+      HIPCHK(grp_launch_garner(gh, (int)std::max<long long>(1, std::min<long long>(gb4, (long long)occH * c->cus)), st));
+      FbgFinParams gf{w, SB, n, c->d_N, c->d_fb_q2Rn, c->mprime_N, e.ct + (size_t)off * c->ct_words, c->ct_words};
+      HIPCHK(grp_launch_fin(gf, (int)std::max<long long>(1, std::min<long long>(gb8, (long long)occC * c->cus)), st));
       stage_mark(c, 3, st);
       continue;
     }

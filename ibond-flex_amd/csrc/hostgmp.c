@@ -15,6 +15,8 @@
 #include <Python.h>
 #include <longintrepr.h>
 #include <gmp.h>
+#include <stdint.h>
+#include <string.h>
 
 /* Work registers, allocated once and reused (every call holds the GIL, so they are never shared
  * concurrently); results go to a register distinct from the inputs, so GMP needs no temporaries. */
@@ -150,7 +152,132 @@ static PyObject* g_mul(PyObject* self, PyObject* const* args, Py_ssize_t nargs) 
   return from_mpz(T);
 }
 
+/* PyLong from nl little-endian 64-bit limbs (non-negative), repacking into 30-bit digits directly */
+static PyObject* long_from_limbs(const uint64_t* w, size_t nl) {
+  while (nl > 0 && w[nl - 1] == 0) --nl;
+  if (nl == 0) return PyLong_FromLong(0);
+  const int top = 64 - __builtin_clzll(w[nl - 1]);
+  const size_t bits = (nl - 1) * 64 + (size_t)top;
+  const size_t n = (bits + PyLong_SHIFT - 1) / PyLong_SHIFT;
+  PyLongObject* l = _PyLong_New((Py_ssize_t)n);
+  if (!l) return NULL;
+  const digit mask = ((digit)1 << PyLong_SHIFT) - 1;
+  size_t k = 0;
+  int pos = 0;
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t v = k < nl ? w[k] >> pos : 0;
+    const int have = 64 - pos;
+    if (have < PyLong_SHIFT && k + 1 < nl) v |= w[k + 1] << have;
+    l->ob_digit[i] = (digit)(v & mask);
+    pos += PyLong_SHIFT;
+    if (pos >= 64) {
+      pos -= 64;
+      ++k;
+    }
+  }
+  return (PyObject*)l;
+}
+
+/* words_to_ints(buf, nwords): rows of `nwords` little-endian 32-bit words -> list of non-negative ints
+ * (the device ciphertext layout; one C loop instead of a Python slice + int.from_bytes per row) */
+static PyObject* g_words_to_ints(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  (void)self;
+  if (nargs != 2) {
+    PyErr_SetString(PyExc_TypeError, "words_to_ints(buf, nwords)");
+    return NULL;
+  }
+  const Py_ssize_t nw = PyLong_AsSsize_t(args[1]);
+  if (nw <= 0) {
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "nwords must be positive");
+    return NULL;
+  }
+  Py_buffer view;
+  if (PyObject_GetBuffer(args[0], &view, PyBUF_C_CONTIGUOUS) < 0) return NULL;
+  const Py_ssize_t row = 4 * nw;
+  if (view.len % row != 0) {
+    PyBuffer_Release(&view);
+    PyErr_SetString(PyExc_ValueError, "buffer length is not a multiple of the row size");
+    return NULL;
+  }
+  const Py_ssize_t n = view.len / row;
+  PyObject* out = PyList_New(n);
+  if (!out) {
+    PyBuffer_Release(&view);
+    return NULL;
+  }
+  const unsigned char* b = (const unsigned char*)view.buf;
+  const size_t nl = (size_t)(nw + 1) / 2;
+  uint64_t stackbuf[256];
+  uint64_t* limbs = nl <= 256 ? stackbuf : (uint64_t*)PyMem_Malloc(nl * sizeof(uint64_t));
+  if (!limbs) {
+    Py_DECREF(out);
+    PyBuffer_Release(&view);
+    return PyErr_NoMemory();
+  }
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    limbs[nl - 1] = 0;
+    memcpy(limbs, b + i * row, (size_t)row);          /* little-endian host: words pair into limbs */
+    PyObject* v = long_from_limbs(limbs, nl);
+    if (!v) {
+      if (limbs != stackbuf) PyMem_Free(limbs);
+      Py_DECREF(out);
+      PyBuffer_Release(&view);
+      return NULL;
+    }
+    PyList_SET_ITEM(out, i, v);
+  }
+  if (limbs != stackbuf) PyMem_Free(limbs);
+  PyBuffer_Release(&view);
+  return out;
+}
+
+/* ints_to_words(seq, nwords) -> bytes of len(seq) rows of `nwords` little-endian 32-bit words
+ * (OverflowError when a value does not fit, ValueError for negatives) */
+static PyObject* g_ints_to_words(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  (void)self;
+  if (nargs != 2) {
+    PyErr_SetString(PyExc_TypeError, "ints_to_words(seq, nwords)");
+    return NULL;
+  }
+  const Py_ssize_t nw = PyLong_AsSsize_t(args[1]);
+  if (nw <= 0) {
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "nwords must be positive");
+    return NULL;
+  }
+  PyObject* seq = PySequence_Fast(args[0], "ints_to_words: expected a sequence");
+  if (!seq) return NULL;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  const Py_ssize_t row = 4 * nw;
+  PyObject* out = PyBytes_FromStringAndSize(NULL, n * row);
+  if (!out) {
+    Py_DECREF(seq);
+    return NULL;
+  }
+  unsigned char* b = (unsigned char*)PyBytes_AS_STRING(out);
+  PyObject** items = PySequence_Fast_ITEMS(seq);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* v = items[i];
+    if (!PyLong_Check(v)) {
+      v = PyNumber_Index(v);
+      if (!v) goto fail;
+    } else {
+      Py_INCREF(v);
+    }
+    const int rc = _PyLong_AsByteArray((PyLongObject*)v, b + i * row, (size_t)row, 1, 0);
+    Py_DECREF(v);
+    if (rc < 0) goto fail;
+  }
+  Py_DECREF(seq);
+  return out;
+fail:
+  Py_DECREF(seq);
+  Py_DECREF(out);
+  return NULL;
+}
+
 static PyMethodDef methods[] = {
+    {"words_to_ints", (PyCFunction)(void (*)(void))g_words_to_ints, METH_FASTCALL, "rows of LE 32-bit words -> ints"},
+    {"ints_to_words", (PyCFunction)(void (*)(void))g_ints_to_words, METH_FASTCALL, "ints -> rows of LE 32-bit words"},
     {"mulmod", (PyCFunction)(void (*)(void))g_mulmod, METH_FASTCALL, "(a * b) % c"},
     {"powmod", (PyCFunction)(void (*)(void))g_powmod, METH_FASTCALL, "a ** b % c (GMP mpz_powm)"},
     {"invert", (PyCFunction)(void (*)(void))g_invert, METH_FASTCALL, "a^-1 mod b"},

@@ -436,15 +436,29 @@ def scalar_dtype(x: np.ndarray) -> int:
     raise TypeError(f"unsupported dtype {x.dtype}")
 
 
+try:                                        # the package's C conversions (csrc/hostgmp.c), when built
+    from .._gmp import ints_to_words as _c_ints_to_words, words_to_ints as _c_words_to_ints
+except ImportError:                         # pragma: no cover - build() always builds it
+    _c_ints_to_words = _c_words_to_ints = None
+
+
 def words_to_ints(words: np.ndarray):
-    """[N, W] little-endian uint32 words -> list of Python ints (zero-copy bytes view)."""
+    """[N, W] little-endian uint32 words -> list of Python ints."""
     w = np.ascontiguousarray(words, dtype="<u4")
+    if w.ndim != 2:
+        w = w.reshape(len(w), -1)
+    if _c_words_to_ints is not None and w.size:
+        return _c_words_to_ints(w, w.shape[1])
     b = w.tobytes()
     step = w.shape[1] * 4
     return [int.from_bytes(b[i * step:(i + 1) * step], "little") for i in range(w.shape[0])]
 
 
 def ints_to_words(vals, nwords: int) -> np.ndarray:
-    nbytes = nwords * 4
-    buf = b"".join(int(v).to_bytes(nbytes, "little") for v in vals)
+    vals = list(vals)
+    if _c_ints_to_words is not None:
+        buf = _c_ints_to_words(vals, nwords)
+    else:
+        nbytes = nwords * 4
+        buf = b"".join(int(v).to_bytes(nbytes, "little") for v in vals)
     return np.frombuffer(buf, dtype="<u4").reshape(len(vals), nwords).copy()

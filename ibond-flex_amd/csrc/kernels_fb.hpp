@@ -39,7 +39,10 @@ namespace fpai {
 constexpr uint32_t FB_NONCE = 0x66786230u;   // ChaCha20 nonce word 2 (+ half) of the exponent stream
 constexpr int FB_RAW_MAX = 80;               // words of the raw exponent per element (5 ChaCha blocks)
 constexpr int FB_DIG_BLOCK = 128;            // threads per block of k_fb_digits
-constexpr int FB_LO = 4096;                  // entries of the per-position small tables (k_fb_lohi): W <= 24
+constexpr int FB_LO = 4096;
+#ifndef FPAI_FB_NBUF
+#define FPAI_FB_NBUF 1                       // k_fb row buffers: 1 (two waves per SIMD) or 2 (one wave, in-wave prefetch)
+#endif                  // entries of the per-position small tables (k_fb_lohi): W <= 24
 
 // Compile-time geometry per lane size SB (limbs of p_h^2): TW = 32-bit words per table row (the
 // canonical values are < p_h^2 < 2^(32 TW)); c0 = 1 + n M is folded in as NC chunks of CB bits of |M|,
@@ -354,10 +357,10 @@ __device__ __forceinline__ void fb_c0(int64_t M, const FbHalf* __restrict__ H, u
 // One LDS row buffer per wave (64 KB per 4-wave block at SB = 74): two blocks -- two waves per SIMD --
 // fit a CU, so a wave waiting for its next table row is covered by the other wave's product.
 template <int SB>
-__global__ __launch_bounds__(LANE_BLOCK, 2) void k_fb(FbParams p) {
+__global__ __launch_bounds__(LANE_BLOCK, 3 - FPAI_FB_NBUF) void k_fb(FbParams p) {
   using G = FbGeom<SB>;
   constexpr int TW = G::TW, TQ = TW / 4;
-  __shared__ uint4 lbuf[TQ * LANE_BLOCK];
+  __shared__ uint4 lbuf[FPAI_FB_NBUF * TQ * LANE_BLOCK];
   const int half = blockIdx.y;
   const FbHalf* H = p.halves + half;
   uint32_t m[SB];
@@ -394,6 +397,19 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fb(FbParams p) {
     }
     uint32_t a[SB];
     fb_c0<SB>(M, H, a);
+#if FPAI_FB_NBUF == 2
+    // two row buffers, one wave per SIMD: row k+1 streams in while product k runs
+    uint4* brow1 = brow + TQ * LANE_BLOCK;
+    const uint32_t addr1 = addr0 + TQ * LANE_BLOCK * 16;
+    for (int k = 0; k < K; ++k) {
+      lds_dma_wait();                                     // row k landed, digit k+1 loaded
+      if (k + 1 < K) {
+        fb_row_to_lds<TQ>(table, ((size_t)(k + 1) << W) + dn, (k & 1) ? brow : brow1);
+        if (k + 2 < K) dn = dg[(size_t)(k + 2) * p.n];
+      }
+      fbw_mont_mul<SB, TW>(a, (k & 1) ? addr1 : addr0, m, mprime);   // every read of the row completes inside
+    }
+#else
     uint32_t dn2 = K > 2 ? dg[2 * p.n] : 0u;               // digit 2, in flight
     for (int k = 0; k < K; ++k) {
       lds_dma_wait();                                     // row k landed, digit k+2 loaded
@@ -405,6 +421,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fb(FbParams p) {
         fb_row_to_lds<TQ>(table, ((size_t)(k + 1) << W) + dk1, brow);
       }
     }
+#endif
     if (i < p.n) {
 #pragma unroll
       for (int j = 0; j < SB; ++j) p.out[((size_t)half * SB + j) * p.n + i] = a[j];

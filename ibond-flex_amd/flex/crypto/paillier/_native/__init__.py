@@ -14,7 +14,7 @@ from typing import Optional, Sequence, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libflexpai.so")
+LIB_PATH = os.environ.get("FLEXPAI_LIB") or os.path.join(_HERE, "libflexpai.so")   # override: experiments only
 
 PAI_F32, PAI_F64, PAI_I64 = 0, 1, 2
 PAI_OBF_NONE, PAI_OBF_GIVEN, PAI_OBF_RNG = 0, 1, 2

@@ -58,3 +58,48 @@ def test_full_size_add8(ctx2048):
     for j, i in enumerate(idx):
         C, E = O.add_k([Nn.words_to_ints(c[i:i + 1])[0] for c in cts], [int(e[i]) for e in exs], key)
         assert (got[j], int(es[i])) == (C, E)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_encrypt_equals_single(ctx2048, world):
+    """configs[3]'s contract on one GPU: the contiguous shards of `world` ranks (sharding.shard_bounds, each
+    encrypting with index_base = its first global index, as bench.py does) reassemble into exactly the
+    ciphertexts of one unsharded call -- ciphertexts do not depend on the GPU count."""
+    from flex.crypto.paillier import _native as Nn
+    from flex.crypto.paillier.sharding import shard_bounds
+    ctx, _ = ctx2048
+    total = 3 * 65536 + 17                                  # ragged: the last shard is shorter
+    x = np.random.default_rng(3).standard_normal(total, dtype=np.float32)
+    rk = bytes(range(50, 82))
+    whole, wex, _ = ctx.encrypt(x, obf_mode=Nn.PAI_OBF_RNG, rng_key=rk, index_base=0)
+    parts, pex = [], []
+    for r in range(world):
+        lo, hi = shard_bounds(total, world, r)
+        c, e, _ = ctx.encrypt(x[lo:hi], obf_mode=Nn.PAI_OBF_RNG, rng_key=rk, index_base=lo)
+        parts.append(c)
+        pex.append(e)
+    assert np.array_equal(np.concatenate(parts), whole) and np.array_equal(np.concatenate(pex), wex)
+
+
+def test_full_size_4096_sample(golden):
+    """configs[4]'s key (nb = 4096) on 262 144 elements of the fixed-base group path: exact round trip,
+    oracle sample, and the chunk-independent ciphertexts of a split call."""
+    from flex.crypto.paillier import _native as Nn
+    k = golden["keys"]["4096"]
+    key = O.Key(int(k["n"], 16), int(k["p"], 16), int(k["q"], 16))
+    ctx = Nn.Context(key.n, 0, key.p, key.q)
+    ctx.set_fb_window(16)
+    n = 1 << 18
+    x = np.random.default_rng(4).standard_normal(n, dtype=np.float32)
+    rk = bytes(range(9, 41))
+    ct, ex, st = ctx.encrypt(x, obf_mode=Nn.PAI_OBF_RNG, rng_key=rk, index_base=7)
+    assert np.all(st == 0)
+    val, _, dst, _ = ctx.decrypt(ct, ex)
+    assert np.all(dst == 0) and np.array_equal(val, x.astype(np.float64))
+    params = ctx.fixed_base_info()
+    idx = [0, n // 2, n - 1]
+    got = Nn.words_to_ints(ct[idx])
+    for j, i in enumerate(idx):
+        assert (got[j], int(ex[i])) == O.fb_encrypt_value(x[i], key, rk, 7 + i, params)
+    half, _, _ = ctx.encrypt(x[n // 2:], obf_mode=Nn.PAI_OBF_RNG, rng_key=rk, index_base=7 + n // 2)
+    assert np.array_equal(half, ct[n // 2:])

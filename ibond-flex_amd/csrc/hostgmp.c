@@ -14,6 +14,12 @@
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 #include <longintrepr.h>
+#include <structmember.h>
+#include <pthread.h>
+#include <unistd.h>
+
+#define W2I_THREADS_MAX 16                                 /* the GPU box grants 16 cores per GPU */
+#define W2I_ROWS_MIN 8192                                  /* rows per thread below which one thread does it */
 #include <gmp.h>
 #include <stdint.h>
 #include <string.h>
@@ -152,15 +158,8 @@ static PyObject* g_mul(PyObject* self, PyObject* const* args, Py_ssize_t nargs) 
   return from_mpz(T);
 }
 
-/* PyLong from nl little-endian 64-bit limbs (non-negative), repacking into 30-bit digits directly */
-static PyObject* long_from_limbs(const uint64_t* w, size_t nl) {
-  while (nl > 0 && w[nl - 1] == 0) --nl;
-  if (nl == 0) return PyLong_FromLong(0);
-  const int top = 64 - __builtin_clzll(w[nl - 1]);
-  const size_t bits = (nl - 1) * 64 + (size_t)top;
-  const size_t n = (bits + PyLong_SHIFT - 1) / PyLong_SHIFT;
-  PyLongObject* l = _PyLong_New((Py_ssize_t)n);
-  if (!l) return NULL;
+/* repack nl limbs into the n 30-bit digits of an allocated PyLong (no Python API: thread-safe) */
+static void fill_digits(digit* d, size_t n, const uint64_t* w, size_t nl) {
   const digit mask = ((digit)1 << PyLong_SHIFT) - 1;
   size_t k = 0;
   int pos = 0;
@@ -168,18 +167,37 @@ static PyObject* long_from_limbs(const uint64_t* w, size_t nl) {
     uint64_t v = k < nl ? w[k] >> pos : 0;
     const int have = 64 - pos;
     if (have < PyLong_SHIFT && k + 1 < nl) v |= w[k + 1] << have;
-    l->ob_digit[i] = (digit)(v & mask);
+    d[i] = (digit)(v & mask);
     pos += PyLong_SHIFT;
     if (pos >= 64) {
       pos -= 64;
       ++k;
     }
   }
-  return (PyObject*)l;
 }
 
-/* words_to_ints(buf, nwords): rows of `nwords` little-endian 32-bit words -> list of non-negative ints
- * (the device ciphertext layout; one C loop instead of a Python slice + int.from_bytes per row) */
+/* words_to_ints fill phase: rows [lo, hi) of the word buffer into the PyLongs allocated for them */
+typedef struct {
+  const unsigned char* b;
+  Py_ssize_t row, lo, hi;
+  size_t nl;
+  PyObject** items;
+} w2i_job;
+
+static void* w2i_fill(void* arg) {
+  const w2i_job* j = (const w2i_job*)arg;
+  uint64_t limbs[256];
+  for (Py_ssize_t i = j->lo; i < j->hi; ++i) {
+    PyLongObject* l = (PyLongObject*)j->items[i];
+    const Py_ssize_t n = Py_SIZE(l);
+    if (n == 0) continue;                                 /* the shared small int 0 */
+    limbs[j->nl - 1] = 0;
+    memcpy(limbs, j->b + i * j->row, (size_t)j->row);
+    fill_digits(l->ob_digit, (size_t)n, limbs, j->nl);
+  }
+  return NULL;
+}
+
 static PyObject* g_words_to_ints(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
   (void)self;
   if (nargs != 2) {
@@ -207,26 +225,68 @@ static PyObject* g_words_to_ints(PyObject* self, PyObject* const* args, Py_ssize
   }
   const unsigned char* b = (const unsigned char*)view.buf;
   const size_t nl = (size_t)(nw + 1) / 2;
-  uint64_t stackbuf[256];
-  uint64_t* limbs = nl <= 256 ? stackbuf : (uint64_t*)PyMem_Malloc(nl * sizeof(uint64_t));
-  if (!limbs) {
+  if (nl > 256) {
     Py_DECREF(out);
     PyBuffer_Release(&view);
-    return PyErr_NoMemory();
+    PyErr_SetString(PyExc_ValueError, "words_to_ints: at most 512 words per row");
+    return NULL;
   }
+  /* phase 1 (GIL): size and allocate every PyLong -- allocation needs the interpreter; phase 2 (no GIL,
+   * threads): repack the rows into the digits, the part that scales with the key size */
+  uint64_t top[2];
   for (Py_ssize_t i = 0; i < n; ++i) {
-    limbs[nl - 1] = 0;
-    memcpy(limbs, b + i * row, (size_t)row);          /* little-endian host: words pair into limbs */
-    PyObject* v = long_from_limbs(limbs, nl);
+    const unsigned char* r = b + i * row;
+    size_t k = nl;
+    size_t nd;
+    for (;;) {                                           /* highest non-zero limb decides the digit count */
+      if (k == 0) {
+        nd = 0;
+        break;
+      }
+      top[0] = 0;
+      top[1] = 0;
+      const size_t off = (k - 1) * 8;
+      memcpy(top, r + off, (size_t)row - off < 8 ? (size_t)row - off : 8);
+      if (top[0]) {
+        const int tb = 64 - __builtin_clzll(top[0]);
+        nd = ((k - 1) * 64 + (size_t)tb + PyLong_SHIFT - 1) / PyLong_SHIFT;
+        break;
+      }
+      --k;
+    }
+    PyObject* v = nd ? (PyObject*)_PyLong_New((Py_ssize_t)nd) : PyLong_FromLong(0);
     if (!v) {
-      if (limbs != stackbuf) PyMem_Free(limbs);
-      Py_DECREF(out);
+      Py_DECREF(out);                                    /* digits of the allocated longs are never read */
       PyBuffer_Release(&view);
       return NULL;
     }
     PyList_SET_ITEM(out, i, v);
   }
-  if (limbs != stackbuf) PyMem_Free(limbs);
+  PyObject** items = ((PyListObject*)out)->ob_item;
+  long nt = sysconf(_SC_NPROCESSORS_ONLN);
+  if (nt > W2I_THREADS_MAX) nt = W2I_THREADS_MAX;
+  if (nt > n / W2I_ROWS_MIN) nt = (long)(n / W2I_ROWS_MIN);
+  if (nt < 1) nt = 1;
+  w2i_job jobs[W2I_THREADS_MAX];
+  pthread_t th[W2I_THREADS_MAX];
+  int started[W2I_THREADS_MAX] = {0};
+  const Py_ssize_t per = (n + nt - 1) / nt;
+  for (long t = 0; t < nt; ++t) {
+    jobs[t].b = b;
+    jobs[t].row = row;
+    jobs[t].lo = t * per < n ? t * per : n;
+    jobs[t].hi = (t + 1) * per < n ? (t + 1) * per : n;
+    jobs[t].nl = nl;
+    jobs[t].items = items;
+  }
+  Py_BEGIN_ALLOW_THREADS
+  for (long t = 1; t < nt; ++t) started[t] = pthread_create(&th[t], NULL, w2i_fill, &jobs[t]) == 0;
+  w2i_fill(&jobs[0]);
+  for (long t = 1; t < nt; ++t) {
+    if (started[t]) pthread_join(th[t], NULL);
+    else w2i_fill(&jobs[t]);                             /* no thread: do its rows here */
+  }
+  Py_END_ALLOW_THREADS
   PyBuffer_Release(&view);
   return out;
 }
@@ -275,7 +335,92 @@ fail:
   return NULL;
 }
 
+/* make_numbers(cls, public_key, ints, exps, obf) -> list of cls instances with the slots public_key,
+ * exponent, _<cls>__ciphertext, _<cls>__is_obfuscator set directly (PaillierEncryptedNumber._make without a
+ * Python call per element). exps: int32 buffer of len(ints); obf: uint8 buffer of len(ints), or a bool for
+ * every element. */
+static Py_ssize_t slot_offset(PyObject* cls, const char* name) {
+  PyObject* d = PyObject_GetAttrString(cls, name);
+  if (!d) return -1;
+  Py_ssize_t off = -1;
+  if (Py_TYPE(d) == &PyMemberDescr_Type) off = ((PyMemberDescrObject*)d)->d_member->offset;
+  else PyErr_Format(PyExc_TypeError, "%s is not a slot", name);
+  Py_DECREF(d);
+  return off;
+}
+
+static PyObject* g_make_numbers(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  (void)self;
+  if (nargs != 5 || !PyType_Check(args[0])) {
+    PyErr_SetString(PyExc_TypeError, "make_numbers(cls, public_key, ints, exps, obf)");
+    return NULL;
+  }
+  PyTypeObject* cls = (PyTypeObject*)args[0];
+  const char* cname = cls->tp_name;
+  const char* dot = strrchr(cname, '.');
+  if (dot) cname = dot + 1;
+  char nct[256], nob[256];
+  snprintf(nct, sizeof nct, "_%s__ciphertext", cname);
+  snprintf(nob, sizeof nob, "_%s__is_obfuscator", cname);
+  Py_ssize_t o_pk, o_ex, o_ct, o_ob;
+  if ((o_pk = slot_offset(args[0], "public_key")) < 0 || (o_ex = slot_offset(args[0], "exponent")) < 0 ||
+      (o_ct = slot_offset(args[0], nct)) < 0 || (o_ob = slot_offset(args[0], nob)) < 0)
+    return NULL;
+  PyObject* ints = PySequence_Fast(args[2], "make_numbers: ints must be a sequence");
+  if (!ints) return NULL;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(ints);
+  Py_buffer ev, ov;
+  if (PyObject_GetBuffer(args[3], &ev, PyBUF_C_CONTIGUOUS) < 0) {
+    Py_DECREF(ints);
+    return NULL;
+  }
+  const int obf_all = PyBool_Check(args[4]);
+  if (!obf_all && PyObject_GetBuffer(args[4], &ov, PyBUF_C_CONTIGUOUS) < 0) {
+    PyBuffer_Release(&ev);
+    Py_DECREF(ints);
+    return NULL;
+  }
+  PyObject* out = NULL;
+  if (ev.len != n * 4 || (!obf_all && ov.len != n)) {
+    PyErr_SetString(PyExc_ValueError, "make_numbers: exps / obf do not match the number of ciphertexts");
+    goto done;
+  }
+  out = PyList_New(n);
+  if (!out) goto done;
+  const int32_t* e = (const int32_t*)ev.buf;
+  const uint8_t* ob = obf_all ? NULL : (const uint8_t*)ov.buf;
+  PyObject** it = PySequence_Fast_ITEMS(ints);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* obj = cls->tp_alloc(cls, 0);
+    PyObject* ex = PyLong_FromLong(e[i]);
+    if (!obj || !ex) {
+      Py_XDECREF(obj);
+      Py_XDECREF(ex);
+      Py_CLEAR(out);
+      goto done;
+    }
+    PyObject* flag = (obf_all ? PyObject_IsTrue(args[4]) : ob[i] != 0) ? Py_True : Py_False;
+    Py_INCREF(args[1]);
+    Py_INCREF(it[i]);
+    Py_INCREF(flag);
+    *(PyObject**)((char*)obj + o_pk) = args[1];
+    *(PyObject**)((char*)obj + o_ex) = ex;
+    *(PyObject**)((char*)obj + o_ct) = it[i];
+    *(PyObject**)((char*)obj + o_ob) = flag;
+    /* the slots hold two ints, a bool and the public key: no cycle can pass through the number, so it
+     * stays out of the collector (which otherwise rescans every survivor as the list grows) */
+    if (PyObject_IS_GC(obj)) PyObject_GC_UnTrack(obj);
+    PyList_SET_ITEM(out, i, obj);
+  }
+done:
+  PyBuffer_Release(&ev);
+  if (!obf_all) PyBuffer_Release(&ov);
+  Py_DECREF(ints);
+  return out;
+}
+
 static PyMethodDef methods[] = {
+    {"make_numbers", (PyCFunction)(void (*)(void))g_make_numbers, METH_FASTCALL, "bulk slot construction"},
     {"words_to_ints", (PyCFunction)(void (*)(void))g_words_to_ints, METH_FASTCALL, "rows of LE 32-bit words -> ints"},
     {"ints_to_words", (PyCFunction)(void (*)(void))g_ints_to_words, METH_FASTCALL, "ints -> rows of LE 32-bit words"},
     {"mulmod", (PyCFunction)(void (*)(void))g_mulmod, METH_FASTCALL, "(a * b) % c"},

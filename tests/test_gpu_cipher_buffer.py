@@ -26,6 +26,7 @@ def no_objects(monkeypatch):
         raise AssertionError("a PaillierEncryptedNumber was built on the object-free path")
     monkeypatch.setattr(PaillierEncryptedNumber, "_make", classmethod(boom))
     monkeypatch.setattr(PaillierEncryptedNumber, "__init__", boom)
+    monkeypatch.setattr("flex.crypto.paillier.cipher_array._make_numbers", boom)   # the C bulk constructor
 
 
 def test_wire_add_chain_without_objects(keys, no_objects):

@@ -157,6 +157,49 @@ def test_host_gmp_binding_matches_python_ints():
             assert _bigint.invert(a, c) == inv
 
 
+def test_bulk_word_conversions_and_object_construction():
+    """words_to_ints (threaded digit fill), ints_to_words and make_numbers (slots set in C, untracked by the
+    cyclic collector) give the same values and objects as int.from_bytes / PaillierEncryptedNumber._make."""
+    import gc
+    import sys
+    from flex.crypto.paillier import _gmp, _runtime
+    from flex.crypto.paillier.cipher_array import materialize
+    from flex.crypto.paillier.encrypted_number import PaillierEncryptedNumber
+    from flex.crypto.paillier.keypair import PaillierPublicKey
+    rng = np.random.default_rng(5)
+    for nw in (1, 3, 64, 65, 128):
+        n = 20000                                   # above the per-thread minimum: several fill threads
+        w = rng.integers(0, 2 ** 32, size=(n, nw), dtype=np.uint32)
+        w[::7, nw // 2:] = 0
+        w[::11] = 0
+        ints = _runtime.words_to_ints(w)
+        assert ints == [int.from_bytes(r.tobytes(), "little") for r in w]
+        assert np.array_equal(np.frombuffer(_runtime.ints_to_words(ints, nw), dtype=np.uint32).reshape(n, nw), w)
+    pk = PaillierPublicKey(1000003 * 1000033)
+    w = rng.integers(0, 2 ** 20, size=(50, 2), dtype=np.uint32)
+    ex = rng.integers(-5, 30, size=50).astype(np.int32)
+    ob = rng.integers(0, 2, size=50).astype(bool)
+    ints = _runtime.words_to_ints(w)
+    ref_before = sys.getrefcount(pk)
+    objs = _gmp.make_numbers(PaillierEncryptedNumber, pk, ints, ex, ob.astype(np.uint8))
+    assert sys.getrefcount(pk) == ref_before + 50
+    for o, c, e, f in zip(objs, ints, ex.tolist(), ob.tolist()):
+        want = PaillierEncryptedNumber._make(pk, c, e, f)
+        assert type(o) is PaillierEncryptedNumber and not gc.is_tracked(o)
+        assert (o.public_key, o.ciphertext(False), o.exponent, o._is_obfuscated()) == \
+            (want.public_key, want.ciphertext(False), want.exponent, want._is_obfuscated())
+        assert pickle.dumps(o) == pickle.dumps(want)             # the reference's slot-state pickle
+    del objs, o, want
+    assert sys.getrefcount(pk) == ref_before
+    arr = materialize(pk, w, ex, (5, 10), True)
+    assert arr.shape == (5, 10) and all(e._is_obfuscated() for e in arr.reshape(-1))
+    assert gc.isenabled()
+    with pytest.raises(ValueError):
+        _gmp.make_numbers(PaillierEncryptedNumber, pk, ints, ex[:-1], True)
+    with pytest.raises(AttributeError):
+        _gmp.make_numbers(int, pk, ints, ex, True)              # no such slots
+
+
 def test_operators_without_gpu_follow_the_reference(golden):
     """On a host without a GPU (this container) the operators on unpickled ciphertext arrays run the
     reference's per-element computation (numpy's object loop over PaillierEncryptedNumber on GMP):

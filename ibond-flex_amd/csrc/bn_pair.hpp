@@ -1,0 +1,152 @@
+// p-adic pair arithmetic mod p^2 in one lane (lane engine sizes: S limbs of p, LB = 28).
+//
+// A residue v mod p^2 is held as a pair (A, B), 0 <= A, B < 2p (S canonical limbs each), with
+//   v == A + p B  (mod p^2).
+// With R = 2^(LB S) (the radix of p, not of p^2), the CIOS product of the A parts gives
+// A1 A2 = U R - m p exactly (U = (A1 A2 + m p) / R, m the q-digits of the reduction), so
+//   (A1 + p B1)(A2 + p B2) R^-1 == U + p (A1 B2 + A2 B1 - m) R^-1        (mod p^2)
+// and the Montgomery product mod p^2 with radix R is the pair
+//   (U, REDC_p(A1 B2 + A2 B1 - m)).
+// Both CIOS run in lock-step over the digits j: the second consumes the first's digit q1_j at the
+// position where it is produced. Cost 5 S^2 MACs (square: 3.5 S^2) against 2 (2S)^2 (square
+// 1.5 (2S)^2) for a Montgomery product over the 2S limbs of p^2: 0.625x (0.58x) of the work, with the
+// register footprint of a 2S-limb lane product (A, B: 2S; two accumulators: 4S VGPRs).
+//
+// Bounds (checked limb by limb in tools/pair_model.py): with R > 8p and operands < 2p, U < 2p and
+// REDC(.) < (A1 B2 + A2 B1) / R + p < 2p. The second accumulator is SIGNED: subtracting q1_j can take a
+// position below zero, so its carries are arithmetic shifts; its final value is >= 0 because
+// (Z + q2 p) / R > -m / R > -1. It receives per digit at most two a*b products and one q2*p product
+// (< 2^57 + 2^57 + 2^56 for a square's doubled digit), so S * 1.25 * 2^58 < 2^63 for S <= 37.
+#pragma once
+#include "bn_lane.hpp"
+
+#include <type_traits>
+
+namespace fpai {
+namespace pair {
+
+using lane::LB;
+using lane::LMASK;
+
+template <int S>
+__device__ __forceinline__ void pin2(uint64_t (&P1)[S], uint64_t (&P2)[S]) {
+#pragma unroll
+  for (int i = 0; i < S; ++i) asm volatile("" : "+v"(P1[i]), "+v"(P2[i]));
+}
+
+// reductions of digit J: P1 by q1 (its own digit), P2 by q2 after subtracting q1 at position J
+template <int S, int J>
+__device__ __forceinline__ void red2(uint64_t (&P1)[S], uint64_t (&P2)[S], const uint32_t (&m)[S], uint32_t mprime) {
+  const uint32_t q1 = ((uint32_t)P1[J] * mprime) & LMASK;
+  P2[J] -= (uint64_t)q1;
+  const uint32_t q2 = ((uint32_t)P2[J] * mprime) & LMASK;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    P1[(i + J) % S] += (uint64_t)q1 * m[i];
+    P2[(i + J) % S] += (uint64_t)q2 * m[i];
+  }
+  P1[(J + 1) % S] += P1[J] >> LB;
+  P2[(J + 1) % S] += (uint64_t)((int64_t)P2[J] >> LB);
+  P1[J] = 0;
+  P2[J] = 0;
+  pin2<S>(P1, P2);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// digit J of a product with the multiplier's digits (a2j, b2j)
+template <int S, int J>
+__device__ __forceinline__ void mul_digit(uint64_t (&P1)[S], uint64_t (&P2)[S], const uint32_t (&A)[S], const uint32_t (&B)[S],
+                                          uint32_t a2j, uint32_t b2j) {
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    P1[(i + J) % S] += (uint64_t)A[i] * a2j;
+    P2[(i + J) % S] += (uint64_t)B[i] * a2j + (uint64_t)A[i] * b2j;
+  }
+}
+
+// digit J of a square: upper triangle of A^2, and 2 A B (B's digit doubled)
+template <int S, int J>
+__device__ __forceinline__ void sqr_digit(uint64_t (&P1)[S], uint64_t (&P2)[S], const uint32_t (&A)[S], const uint32_t (&B)[S]) {
+  const uint32_t aj = A[J], aj2 = aj << 1, bj2 = B[J] << 1;
+  P1[(2 * J) % S] += (uint64_t)aj * aj;
+#pragma unroll
+  for (int i = J + 1; i < S; ++i) P1[(i + J) % S] += (uint64_t)A[i] * aj2;
+#pragma unroll
+  for (int i = 0; i < S; ++i) P2[(i + J) % S] += (uint64_t)A[i] * bj2;
+}
+
+template <int S>
+__device__ __forceinline__ void normalize_signed(const uint64_t (&P)[S], uint32_t (&r)[S]) {
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const int64_t v = (int64_t)P[i] + c;
+    r[i] = (uint32_t)v & LMASK;
+    c = v >> LB;
+  }
+}
+
+template <int S>
+__device__ __forceinline__ void zero2(uint64_t (&P1)[S], uint64_t (&P2)[S]) {
+#pragma unroll
+  for (int i = 0; i < S; ++i) P1[i] = P2[i] = 0;
+}
+
+// (A, B) <- (A, B)^2 R^-1
+template <int S, int... Js>
+__device__ __forceinline__ void sqr_all(uint64_t (&P1)[S], uint64_t (&P2)[S], const uint32_t (&A)[S], const uint32_t (&B)[S],
+                                        const uint32_t (&m)[S], uint32_t mprime, std::integer_sequence<int, Js...>) {
+  ((sqr_digit<S, Js>(P1, P2, A, B), red2<S, Js>(P1, P2, m, mprime)), ...);
+}
+template <int S>
+__device__ __forceinline__ void mont_sqr(uint32_t (&A)[S], uint32_t (&B)[S], const uint32_t (&m)[S], uint32_t mprime) {
+  uint64_t P1[S], P2[S];
+  zero2<S>(P1, P2);
+  sqr_all<S>(P1, P2, A, B, m, mprime, std::make_integer_sequence<int, S>{});
+  lane::normalize<S>(P1, A);
+  normalize_signed<S>(P2, B);
+}
+
+// (A, B) <- (A, B) (A2, B2) R^-1 with the multiplier's digit pair J from get(J) (a uint2: x = A2[J],
+// y = B2[J]); get is called once per digit, in order.
+template <int S, int J, class Get>
+__device__ __forceinline__ void mul_step(uint64_t (&P1)[S], uint64_t (&P2)[S], const uint32_t (&A)[S], const uint32_t (&B)[S],
+                                         Get& get, const uint32_t (&m)[S], uint32_t mprime) {
+  const uint2 d = get(std::integral_constant<int, J>{});
+  mul_digit<S, J>(P1, P2, A, B, d.x, d.y);
+  red2<S, J>(P1, P2, m, mprime);
+}
+template <int S, class Get, int... Js>
+__device__ __forceinline__ void mul_all(uint64_t (&P1)[S], uint64_t (&P2)[S], const uint32_t (&A)[S], const uint32_t (&B)[S],
+                                        Get& get, const uint32_t (&m)[S], uint32_t mprime, std::integer_sequence<int, Js...>) {
+  (mul_step<S, Js>(P1, P2, A, B, get, m, mprime), ...);
+}
+template <int S, class Get>
+__device__ __forceinline__ void mont_mul(uint32_t (&A)[S], uint32_t (&B)[S], Get&& get, const uint32_t (&m)[S], uint32_t mprime) {
+  uint64_t P1[S], P2[S];
+  zero2<S>(P1, P2);
+  mul_all<S>(P1, P2, A, B, get, m, mprime, std::make_integer_sequence<int, S>{});
+  lane::normalize<S>(P1, A);
+  normalize_signed<S>(P2, B);
+}
+
+// (A, B) with A, B < 2p -> the canonical pair A < p, B < p of the same residue mod p^2
+// (A - p + p (B + 1) == A + p B)
+template <int S>
+__device__ __forceinline__ void canon(uint32_t (&A)[S], uint32_t (&B)[S], const uint32_t (&m)[S]) {
+  uint32_t d[S];
+  const bool lt = lane::sub<S>(A, m, d);
+  uint32_t c = lt ? 0u : 1u;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    A[i] = lt ? A[i] : d[i];
+    const uint32_t v = B[i] + c;
+    B[i] = v & LMASK;
+    c = v >> LB;
+  }
+  lane::cond_sub<S>(B, m);   // B <= 2p
+  lane::cond_sub<S>(B, m);
+}
+
+}  // namespace pair
+}  // namespace fpai

@@ -1,0 +1,36 @@
+// Pair fixed-base kernels (kernels_fbp.hpp): instantiations and launches.
+#include "engine_fbp.hpp"
+
+namespace fpai {
+
+int fbp_occupancy(int s, int* occ) {
+  hipError_t e;
+  if (s == 19) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, k_fbp<19>, LANE_BLOCK, 0);
+  else if (s == 37) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, k_fbp<37>, LANE_BLOCK, 0);
+  else return -1;
+  if (e != hipSuccess || *occ < 1) *occ = 1;
+  return 0;
+}
+
+hipError_t fbp_launch(int s, const FbpParams& p, int gx, hipStream_t st) {
+  if (s == 19) hipLaunchKernelGGL(k_fbp<19>, dim3(gx, 2), dim3(LANE_BLOCK), 0, st, p);
+  else if (s == 37) hipLaunchKernelGGL(k_fbp<37>, dim3(gx, 2), dim3(LANE_BLOCK), 0, st, p);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t fbp_build_tables(int s, const FbpHalf* d_halves, uint4* t0, uint4* t1, int K, int W, hipStream_t st) {
+  const int per = ((1 << W) + LANE_BLOCK - 1) / LANE_BLOCK;
+  if (s == 19) {
+    hipLaunchKernelGGL(k_fbp_lohi<19>, dim3(K, 2), dim3(LANE_BLOCK), 0, st, d_halves, K, W);
+    hipLaunchKernelGGL(k_fbp_fill<19>, dim3(K * per, 2), dim3(LANE_BLOCK), 0, st, d_halves, K, W, t0, t1);
+  } else if (s == 37) {
+    hipLaunchKernelGGL(k_fbp_lohi<37>, dim3(K, 2), dim3(LANE_BLOCK), 0, st, d_halves, K, W);
+    hipLaunchKernelGGL(k_fbp_fill<37>, dim3(K * per, 2), dim3(LANE_BLOCK), 0, st, d_halves, K, W, t0, t1);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace fpai

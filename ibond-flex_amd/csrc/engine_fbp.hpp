@@ -1,0 +1,13 @@
+// Host interface of the pair fixed-base translation unit (engine_fbp.hip).
+#pragma once
+#include "kernels_fbp.hpp"
+
+namespace fpai {
+
+// blocks per CU of k_fbp<s>; -1 if s is unsupported (19: 1024-bit keys, 37: 2048-bit keys)
+int fbp_occupancy(int s, int* occ);
+hipError_t fbp_launch(int s, const FbpParams& p, int gx, hipStream_t st);
+// builds both halves' pair tables (K digit positions of W bits) on `st`
+hipError_t fbp_build_tables(int s, const FbpHalf* d_halves, uint4* t0, uint4* t1, int K, int W, hipStream_t st);
+
+}  // namespace fpai

@@ -17,6 +17,7 @@
 #include "engine_dec.hpp"
 #include "engine_lane.hpp"
 #include "engine_fb.hpp"
+#include "engine_fbp.hpp"
 #include "engine_grp.hpp"
 #include "engine_mul.hpp"
 
@@ -83,6 +84,8 @@ struct pai_ctx {
   int fb_W_used = 0;            // window of the resident tables (may be below fb_W under a memory cap)
   int fb_raw_bits = 0;
   FbHalf* d_fb_halves = nullptr;
+  FbpHalf* d_fbp_halves = nullptr;  // pair tables (kernels_fbp.hpp): the default for 1024/2048-bit keys
+  int fb_pair_s = 0;            // limbs of p_h of the resident pair tables; 0 = k_fb tables
   FbRed* d_fb_red = nullptr;
   uint32_t *d_fb_m8 = nullptr, *d_fb_coefR = nullptr, *d_fb_q2 = nullptr, *d_fb_m0 = nullptr;
   uint32_t* d_fb_q2Rn = nullptr;  // 4096-bit keys: q^2 R mod n^2 (k_fbg_fin)
@@ -516,6 +519,8 @@ static void fb_release(pai_ctx* c) {
   for (void* p : c->fb_mem) (void)hipFree(p);
   c->fb_mem.clear();
   c->d_fb_halves = nullptr;
+  c->d_fbp_halves = nullptr;
+  c->fb_pair_s = 0;
   c->d_fb_red = nullptr;
 }
 
@@ -562,6 +567,16 @@ static int ensure_fb(pai_ctx* c) {
   const int K = fb_digit_count(c, W);
   const size_t RB = (size_t)LB * sb;
   const HBig primes[2] = {c->fb_p, c->fb_q};
+  // pair products (kernels_fbp.hpp) over the S limbs of p_h: needs p_h < 2^(32 PW) and R = 2^(28 S) >=
+  // 2^12 p_h (bounds of the first product, kernels_fbp.hpp); $FLEXPAI_FB_PAIR=0 selects k_fb
+  const int ps = sb == 37 ? 19 : sb == 74 ? 37 : 0;
+  const int pw = sb == 37 ? FbpGeom<19>::PW : FbpGeom<37>::PW;
+  bool pair_ok = ps && !grp;
+  if (const char* e = getenv("FLEXPAI_FB_PAIR")) pair_ok = pair_ok && atoi(e) != 0;
+  for (int h = 0; h < 2 && pair_ok; ++h)
+    pair_ok = primes[h].bits() <= (size_t)32 * pw && primes[h].bits() + FBP_PB + 1 <= (size_t)LB * ps;
+  const int lohi_limbs = pair_ok ? std::max(sb, 2 * ps) : sb;
+  FbpHalf pv[2];
   FbHalf hv[2];
   FbRed red[2];
   std::memset(red, 0, sizeof(red));
@@ -599,13 +614,46 @@ static int ensure_fb(pai_ctx* c) {
         (rc = upload_fb(c, nm, &dnm)) || (rc = upload_fb(c, mul(m2, pow2(PB)).limbs(sb, LB), &dpbig)))
       return fb_unavailable(c, pai_last_error());
     // lo/hi half-digit tables: build scratch only, released once the table is filled
-    if (hipMalloc(&lohi[h], (size_t)K * 2 * FB_LO * sb * 4) != hipSuccess) return fb_unavailable(c, "table allocation failed");
+    if (hipMalloc(&lohi[h], (size_t)K * 2 * FB_LO * lohi_limbs * 4) != hipSuccess) return fb_unavailable(c, "table allocation failed");
     c->fb_mem.push_back(lohi[h]);
     dlohi = (uint32_t*)lohi[h];
     if (hipMalloc(&t[h], ((size_t)K << W) * (TW / 4) * sizeof(uint4)) != hipSuccess)
       return fb_unavailable(c, "table allocation failed");
     c->fb_mem.push_back(t[h]);
     hv[h] = FbHalf{(const uint4*)t[h], dm, dR2, done, dbases, dlohi, dnm, dpbig, mont_prime(m2, LB)};
+    if (pair_ok) {
+      // pair constants: (x mod p_h, x div p_h) of Montgomery-form values x = v R mod p_h^2, R = 2^(28 S)
+      const HBig& P = primes[h];
+      const size_t RS = (size_t)LB * ps;
+      auto split = [&](const HBig& v, std::vector<uint32_t>& out) {
+        const HBig qt = div_big(v, P), rm = sub(v, mul(qt, P));
+        const std::vector<uint32_t> a = rm.limbs(ps, LB), b = qt.limbs(ps, LB);
+        out.insert(out.end(), a.begin(), a.end());
+        out.insert(out.end(), b.begin(), b.end());
+      };
+      std::vector<uint32_t> one_p, bases_p, nm_p;
+      split(mul_pow2_mod(HBig(1), RS, m2), one_p);
+      const int LOb = W / 2;
+      HBig y = M2.to(M2.pow(HBig(c->fb_g[h]), c->n));   // G in M2's domain
+      for (int k = 0; k < K; ++k) {
+        HBig z = y;
+        split(mul_pow2_mod(M2.from(z), RS, m2), bases_p);                 // B_k R
+        for (int q = 0; q < LOb; ++q) z = M2.mul(z, z);
+        split(mul_pow2_mod(M2.from(z), RS, m2), bases_p);                 // B_k^(2^LO) R
+        for (int q = 0; q < W; ++q) y = M2.mul(y, y);
+      }
+      const HBig other = primes[1 - h];
+      for (int k = 0; k < FBP_NC; ++k) {
+        const std::vector<uint32_t> v = mul_pow2_mod(mod(other, P), (size_t)FBP_CB * k, P).limbs(ps, LB);
+        nm_p.insert(nm_p.end(), v.begin(), v.end());
+      }
+      uint32_t *pp, *pone, *pbases, *pnm, *ppbig;
+      if ((rc = upload_fb(c, P.limbs(ps, LB), &pp)) || (rc = upload_fb(c, one_p, &pone)) ||
+          (rc = upload_fb(c, bases_p, &pbases)) || (rc = upload_fb(c, nm_p, &pnm)) ||
+          (rc = upload_fb(c, mul(P, pow2(FBP_PB)).limbs(ps, LB), &ppbig)))
+        return fb_unavailable(c, pai_last_error());
+      pv[h] = FbpHalf{(const uint4*)t[h], pp, pone, pbases, dlohi, pnm, ppbig, mont_prime(P, LB)};
+    }
     if (h == 0) {
       c->d_fb_m0 = dm;
       c->fb_mprime0 = mont_prime(m2, LB);
@@ -631,8 +679,13 @@ static int ensure_fb(pai_ctx* c) {
       (grp && (rc = upload_fb(c, mul_pow2_mod(sq[1], (size_t)LB * c->S_e, c->N).limbs(c->S_e, LB), &c->d_fb_q2Rn))))
     return fb_unavailable(c, pai_last_error());
   const auto t1 = std::chrono::steady_clock::now();
-  const hipError_t be = grp ? grp_build_tables(c->d_fb_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
-                            : fb_build_tables(sb, c->d_fb_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
+  if (pair_ok) {
+    std::vector<FbpHalf> pvv(pv, pv + 2);
+    if ((rc = upload_fb(c, pvv, &c->d_fbp_halves))) return fb_unavailable(c, pai_last_error());
+  }
+  const hipError_t be = grp       ? grp_build_tables(c->d_fb_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
+                        : pair_ok ? fbp_build_tables(ps, c->d_fbp_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr)
+                                  : fb_build_tables(sb, c->d_fb_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
   if (be != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return fb_unavailable(c, "table construction failed");
   for (void* p : lohi) {
@@ -644,6 +697,7 @@ static int ensure_fb(pai_ctx* c) {
   c->fb_dev_ms = std::chrono::duration<float, std::milli>(t2 - t1).count();
   c->fb_table_bytes = fb_bytes(c, W);
   c->fb_K = K;
+  c->fb_pair_s = pair_ok ? ps : 0;
   c->fb_W_used = W;
   c->fb_raw_bits = raw_bits;
   c->fb_state = pai_ctx::FB_READY;
@@ -993,6 +1047,7 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
   int occF = 1, occG = 1;
   if (grp) grp_occupancy(&occF);
   else if (fb_occupancy(SB, &occF, &occG)) return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
+  if (c->fb_pair_s && fbp_occupancy(c->fb_pair_s, &occF)) return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
   // elements per block: one per lane, or one per lane group (grp)
   const int EPB = grp ? BLOCK / GRP_TPI : LANE_BLOCK;
   const long long lane_blocks = (chunk + EPB - 1) / EPB;
@@ -1033,7 +1088,12 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     pf.exp = e.exp + off;
     pf.status = e.status ? e.status + off : nullptr;
     const int gF = (int)std::min<long long>(gxF, (n + EPB - 1) / EPB);
-    HIPCHK(grp ? grp_launch_fb(pf, gF, st) : fb_launch(SB, pf, gF, st));
+    if (c->fb_pair_s) {
+      const FbpParams pp{c->d_fbp_halves, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
+      HIPCHK(fbp_launch(c->fb_pair_s, pp, gF, st));
+    } else {
+      HIPCHK(grp ? grp_launch_fb(pf, gF, st) : fb_launch(SB, pf, gF, st));
+    }
     stage_mark(c, 2, st);
     c->fb_last_w = w;
     c->fb_last_n = n;

@@ -1,0 +1,273 @@
+// Fixed-base obfuscation on p-adic pairs (bn_pair.hpp): the sampler of kernels_fb.hpp with every
+// product mod p_h^2 done as a pair product over the S limbs of p_h (5 S^2 MACs) instead of a Montgomery
+// product over the 2S limbs of p_h^2 (8 S^2 MACs). Same distribution, same ciphertext bits.
+//
+// Table rows hold the canonical pair (A, B) of T_k[d] R mod p_h^2 (R = 2^(28 S)): PW 32-bit words of A
+// then PW words of B -- 256 B for a 2048-bit key, the row size of k_fb. The accumulator starts at c0 =
+// 1 + n M = 1 + p_h (n / p_h) M, i.e. the pair (1, (n / p_h) M mod p_h), with the second component an
+// unreduced sum of 8-bit chunks of |M| (< 2^PB p_h; the first product keeps B < 2 p_h while R >= 2^(PB+1) p_h).
+// Every product multiplies a plain pair by a Montgomery-form row, so the result stays plain: after the
+// K products the pair is c0 G_h^(a_h) mod p_h^2, written as w = A + p_h B (< 2 p_h^2, SB limbs) for
+// k_fb_fin's Garner recombination (unchanged).
+#pragma once
+#include "bn_pair.hpp"
+#include "kernels_fb.hpp"
+
+namespace fpai {
+
+template <int S>
+struct FbpGeom;
+template <>
+struct FbpGeom<19> {   // 1024-bit keys: p_h < 2^512
+  static constexpr int SB = 37, PW = 16;
+};
+template <>
+struct FbpGeom<37> {   // 2048-bit keys: p_h < 2^1024
+  static constexpr int SB = 74, PW = 32;
+};
+constexpr int FBP_CB = 8, FBP_NC = 8, FBP_PB = 11;    // c0 chunks: 8 x 8 bits of |M| (sum < 2^11 p_h); offset 2^11 p_h
+
+struct FbpHalf {
+  const uint4* table;      // [K][2^W][2 PW / 4] quads: words of A, then of B, of the pair of T_k[d] R mod p_h^2
+  const uint32_t* p;       // p_h, S limbs
+  const uint32_t* oneR;    // pair of R mod p_h^2 (2S limbs: A then B)
+  const uint32_t* bases;   // [K][2][2S] pairs of B_k R and B_k^(2^LO) R mod p_h^2 (table construction)
+  uint32_t* lohi;          // [K][2][FB_LO][2S] scratch of the table construction
+  const uint32_t* nm;      // [NC][S] (n / p_h) 2^(CB c) mod p_h
+  const uint32_t* pbig;    // [S] 2^PB p_h
+  uint32_t mprime;         // -p_h^-1 mod 2^28
+};
+
+struct FbpParams {
+  const FbpHalf* halves;   // [2]
+  long long n;
+  int K, W;
+  const uint32_t* digits;  // [2][K][n]
+  uint32_t* out;           // w [2][SB][n]
+  const void* x;
+  int dtype, exp_mode, fexp;
+  int32_t* exp;
+  int32_t* status;
+};
+
+// The multiplier's digit pairs from this lane's word row in LDS ([quad][lane] layout, A words then B
+// words), read D words ahead: digit J needs words (28 J) / 32 and (28 J + 27) / 32 of each half-row.
+template <int S, int PW, int D>
+struct FbpRowDigits {
+  uint32_t addr;
+  uint32_t wa[PW], wb[PW];
+  static constexpr int lo(int J) { return (28 * J) >> 5; }
+  static constexpr int hi(int J) { return (28 * J + 27) >> 5 < PW - 1 ? (28 * J + 27) >> 5 : PW - 1; }
+  static constexpr int issued(int J) { return J < 0 ? -1 : (hi(J) + D < PW - 1 ? hi(J) + D : PW - 1); }
+  template <int WI>
+  __device__ __forceinline__ void issue_word() {
+    wa[WI] = lds_read_word<(WI / 4) * LANE_BLOCK * 16 + (WI % 4) * 4>(addr);
+    wb[WI] = lds_read_word<((PW + WI) / 4) * LANE_BLOCK * 16 + ((PW + WI) % 4) * 4>(addr);
+  }
+  template <int W0, int... Ws>
+  __device__ __forceinline__ void issue(std::integer_sequence<int, Ws...>) {
+    (issue_word<W0 + Ws>(), ...);
+  }
+  template <int J>
+  __device__ __forceinline__ uint2 operator()(std::integral_constant<int, J>) {
+    constexpr int from = issued(J - 1) + 1, to = issued(J);
+    issue<from>(std::make_integer_sequence<int, (to >= from ? to - from + 1 : 0)>{});
+    constexpr int l = lo(J), h = hi(J);
+    constexpr int pending = 2 * (to - h);   // reads issued after the words digit J needs
+    static_assert(pending <= 15, "lgkmcnt range");
+    if constexpr (l == h) asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(wa[l]), "+v"(wb[l]) : "i"(pending));
+    else asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(wa[l]), "+v"(wa[h]), "+v"(wb[l]), "+v"(wb[h]) : "i"(pending));
+    constexpr int bit = 28 * J, sh = bit & 31;
+    uint32_t x, y;
+    if constexpr (l >= PW) {
+      x = y = 0u;
+    } else if constexpr (sh + 28 <= 32) {
+      x = (wa[l] >> sh) & lane::LMASK;
+      y = (wb[l] >> sh) & lane::LMASK;
+    } else if constexpr (l + 1 < PW) {
+      x = __builtin_amdgcn_alignbit(wa[l + 1], wa[l], sh) & lane::LMASK;
+      y = __builtin_amdgcn_alignbit(wb[l + 1], wb[l], sh) & lane::LMASK;
+    } else {
+      x = wa[l] >> sh;
+      y = wb[l] >> sh;
+    }
+    return make_uint2(x, y);
+  }
+};
+
+// c0 = 1 + n M as the pair (1, (n / p_h) M mod p_h), second component partially reduced (header)
+template <int S>
+__device__ __forceinline__ void fbp_c0(int64_t M, const FbpHalf* __restrict__ H, uint32_t (&A)[S], uint32_t (&B)[S]) {
+  const bool neg = M < 0;
+  const uint64_t mag = neg ? (uint64_t)0 - (uint64_t)M : (uint64_t)M;
+  uint32_t mc[FBP_NC];
+#pragma unroll
+  for (int c = 0; c < FBP_NC; ++c) mc[c] = (uint32_t)((mag >> (FBP_CB * c)) & ((1ull << FBP_CB) - 1ull));
+  const uint32_t* nm = opaque_uniform(H->nm);
+  const uint32_t* pb = opaque_uniform(H->pbig);
+  int64_t carry = 0;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    uint64_t s = 0;
+#pragma unroll
+    for (int c = 0; c < FBP_NC; ++c) s += (uint64_t)nm[c * S + j] * mc[c];
+    const int64_t v = carry + (neg ? (int64_t)pb[j] - (int64_t)s : (int64_t)s);
+    B[j] = (uint32_t)v & lane::LMASK;
+    carry = v >> lane::LB;
+    A[j] = j == 0 ? 1u : 0u;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// limb K of w = A + p B (product scanning; p in SGPRs)
+template <int S, int K>
+__device__ __forceinline__ uint64_t fbp_col(const uint32_t (&A)[S], const uint32_t (&B)[S], const uint32_t (&m)[S]) {
+  uint64_t s = K < S ? (uint64_t)A[K] : 0ull;
+  constexpr int lo = K < S ? 0 : K - S + 1, hi = K < S ? K : S - 1;
+#pragma unroll
+  for (int i = lo; i <= hi; ++i) s += (uint64_t)B[i] * m[K - i];
+  return s;
+}
+template <int S, int SB, int... Ks>
+__device__ __forceinline__ void fbp_store_w(const uint32_t (&A)[S], const uint32_t (&B)[S], const uint32_t (&m)[S], uint32_t* out,
+                                            long long n, std::integer_sequence<int, Ks...>) {
+  uint64_t acc = 0;
+  ((acc += fbp_col<S, Ks>(A, B, m), out[(size_t)Ks * n] = (uint32_t)acc & lane::LMASK, acc >>= lane::LB), ...);
+}
+
+// Per element and half: c0 prod_k T_k[d_k] mod p_h^2 by pair products; row k in LDS (DMA one digit
+// ahead, one buffer per wave, two waves per SIMD), as k_fb.
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp(FbpParams p) {
+  using G = FbpGeom<S>;
+  constexpr int SB = G::SB, PW = G::PW, TQ = 2 * PW / 4;
+  __shared__ uint4 lbuf[TQ * LANE_BLOCK];
+  const int half = blockIdx.y;
+  const FbpHalf* H = p.halves + half;
+  uint32_t m[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) m[j] = H->p[j];
+  const uint32_t mprime = H->mprime;
+  const uint4* table = H->table;
+  const int K = p.K, W = p.W;
+  uint4* brow = lbuf + (threadIdx.x & ~63u);
+  typedef __attribute__((address_space(3))) uint4 lds_uint4;
+  const uint32_t addr0 = (uint32_t)(size_t)(lds_uint4*)(lbuf + threadIdx.x);
+  for (long long base = (long long)blockIdx.x * LANE_BLOCK; base < p.n; base += (long long)gridDim.x * LANE_BLOCK) {
+    const long long i = base + threadIdx.x;
+    const long long ii = i < p.n ? i : p.n - 1;
+    const uint32_t* dg = p.digits + (size_t)half * K * p.n + ii;
+    uint32_t d0 = dg[0];
+    uint32_t dn = K > 1 ? dg[p.n] : 0u;
+    double xv;
+    int64_t xi = 0;
+    if (p.dtype == 0) xv = (double)((const float*)p.x)[ii];
+    else if (p.dtype == 1) xv = ((const double*)p.x)[ii];
+    else { xi = ((const int64_t*)p.x)[ii]; xv = 0.0; }
+    asm volatile("" : "+v"(d0), "+v"(dn), "+v"(xv), "+v"(xi));
+    fb_row_to_lds<TQ>(table, d0, brow);
+    int64_t M = 0;
+    int e = 0, st;
+    const bool fixed = p.exp_mode != 0;
+    if (p.dtype == 2) st = encode_int(xi, fixed, p.fexp, M, e);
+    else st = encode_float(xv, fixed, p.fexp, M, e);
+    if (half == 0 && i < p.n) {
+      p.exp[i] = e;
+      if (p.status) p.status[i] = st;
+    }
+    uint32_t A[S], B[S];
+    fbp_c0<S>(M, H, A, B);
+    uint32_t dn2 = K > 2 ? dg[2 * p.n] : 0u;
+    for (int k = 0; k < K; ++k) {
+      lds_dma_wait();                                     // row k landed, digit k+2 loaded
+      {
+        FbpRowDigits<S, PW, 2> rd{addr0};
+        pair::mont_mul<S>(A, B, rd, m, mprime);           // every read of the row completes inside
+      }
+      if (k + 1 < K) {
+        const uint32_t dk1 = dn;
+        dn = dn2;
+        if (k + 3 < K) dn2 = dg[(size_t)(k + 3) * p.n];
+        fb_row_to_lds<TQ>(table, ((size_t)(k + 1) << W) + dk1, brow);
+      }
+    }
+    if (i < p.n) {
+      pair::canon<S>(A, B, m);
+      fbp_store_w<S, SB>(A, B, m, p.out + (size_t)half * SB * p.n + i, p.n, std::make_integer_sequence<int, SB>{});
+    }
+  }
+}
+
+// ---------------------------------------------------------------- per-key table in pair form
+// k_fbp_lohi: per position k, lo[j] = B_k^j R (j < 2^LO) and hi[j] = B_k^(2^LO j) R (j < 2^(W-LO)) by
+// square-and-multiply from R (the pair of one); k_fbp_fill: T_k[d] R = lo[d & (2^LO - 1)] hi[d >> LO] R^-1,
+// one pair product per entry, canonicalised and stored as words.
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK) void k_fbp_lohi(const FbpHalf* halves, int K, int W) {
+  const int k = blockIdx.x, half = blockIdx.y;
+  const FbpHalf* H = halves + half;
+  const int LO = W / 2, HI = W - LO;
+  uint32_t m[S], A[S], B[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) m[i] = H->p[i];
+  for (int s = 0; s < 2; ++s) {
+    const int bits = s ? HI : LO;
+    const uint32_t* x = H->bases + ((size_t)k * 2 + s) * 2 * S;
+    for (uint32_t j = threadIdx.x; j < (1u << bits); j += blockDim.x) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        A[i] = H->oneR[i];
+        B[i] = H->oneR[S + i];
+      }
+      for (int b = bits - 1; b >= 0; --b) {
+        pair::mont_sqr<S>(A, B, m, H->mprime);
+        if ((j >> b) & 1u)
+          pair::mont_mul<S>(A, B, [&](auto J) { return make_uint2(x[decltype(J)::value], x[S + decltype(J)::value]); }, m,
+                            H->mprime);
+      }
+      uint32_t* o = H->lohi + (((size_t)k * 2 + s) * FB_LO + j) * 2 * S;
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        o[i] = A[i];
+        o[S + i] = B[i];
+      }
+    }
+  }
+}
+
+template <int S, int... Gs>
+__device__ __forceinline__ void fbp_store_row(uint4* __restrict__ dst, const uint32_t (&A)[S], const uint32_t (&B)[S],
+                                              std::integer_sequence<int, Gs...>) {
+  ((dst[Gs] = make_uint4(fb_word<S, 4 * Gs>(A), fb_word<S, 4 * Gs + 1>(A), fb_word<S, 4 * Gs + 2>(A), fb_word<S, 4 * Gs + 3>(A))), ...);
+  ((dst[sizeof...(Gs) + Gs] =
+        make_uint4(fb_word<S, 4 * Gs>(B), fb_word<S, 4 * Gs + 1>(B), fb_word<S, 4 * Gs + 2>(B), fb_word<S, 4 * Gs + 3>(B))),
+   ...);
+}
+
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK) void k_fbp_fill(const FbpHalf* halves, int K, int W, uint4* table0, uint4* table1) {
+  constexpr int PW = FbpGeom<S>::PW, TQ = 2 * PW / 4;
+  const int ent = 1 << W;
+  const int per = (ent + LANE_BLOCK - 1) / LANE_BLOCK;
+  const int k = blockIdx.x / per;
+  const int d = (blockIdx.x % per) * LANE_BLOCK + threadIdx.x;
+  if (d >= ent) return;
+  const int half = blockIdx.y;
+  const FbpHalf* H = halves + half;
+  uint4* table = half ? table1 : table0;
+  const int LO = W / 2;
+  const uint32_t* lo = H->lohi + (((size_t)k * 2 + 0) * FB_LO + (d & ((1 << LO) - 1))) * 2 * S;
+  const uint32_t* hi = H->lohi + (((size_t)k * 2 + 1) * FB_LO + (d >> LO)) * 2 * S;
+  uint32_t m[S], A[S], B[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    m[i] = H->p[i];
+    A[i] = lo[i];
+    B[i] = lo[S + i];
+  }
+  pair::mont_mul<S>(A, B, [&](auto J) { return make_uint2(hi[decltype(J)::value], hi[S + decltype(J)::value]); }, m, H->mprime);
+  pair::canon<S>(A, B, m);
+  fbp_store_row<S>(table + ((size_t)k * ent + d) * TQ, A, B, std::make_integer_sequence<int, PW / 4>{});
+}
+
+}  // namespace fpai

@@ -95,6 +95,19 @@ def work_fb(nb: int, digits: int) -> dict:
     return {"k_fb_digits": 0.0, "k_fb": float(2 * digits * _M(s)), "k_fb_fin": float(_M(s) + s * s)}
 
 
+def _Mp(s: int) -> int:
+    """Pair product mod p^2 over s 32-bit limbs of p (bn_pair.hpp): A1 A2 + q1 p, and B1 A2 + A1 B2 + q2 p,
+    5 s^2 MACs, + 2 s for the two digit reductions (the analogue of M(s)'s + s)."""
+    return 5 * s * s + 2 * s
+
+
+def work_fbp(nb: int, digits: int) -> dict:
+    """Per-element MACs of the pair fixed-base path (kernels_fbp.hpp): k_fbp = K pair products per half
+    (s = nb/64 limbs of p_h) + the c0 chunk sum and w = A + p B (s^2); Garner as work_fb."""
+    s = nb // 64
+    return {"k_fb_digits": 0.0, "k_fbp": float(2 * (digits * _Mp(s) + s * s)), "k_fb_fin": float(_M(2 * s) + 4 * s * s)}
+
+
 def work_fbg(nb: int, digits: int) -> dict:
     """Per-element MACs of the 4096-bit key holder's fixed-base path (kernels_grp.hpp), counted like work_fb:
     k_fbg = K table products mod p_h^2 per half (c0 folded into the first); Garner = one product mod p^2
@@ -105,6 +118,12 @@ def work_fbg(nb: int, digits: int) -> dict:
 
 def work_dec(nb: int) -> float:
     return float(2 * (_P(nb // 2) + 2) * _M(nb // 32))
+
+
+def work_dec_pair(nb: int) -> float:
+    """W_dec with every product mod p_h^2 a pair product over the nb/64 32-bit limbs of p_h (kernels_pair.hpp;
+    squarings counted as products, like §8d's W_dec)."""
+    return float(2 * (_P(nb // 2) + 2) * _Mp(nb // 64))
 
 
 def work_add(exps: "torch.Tensor", nb: int) -> float:
@@ -218,6 +237,7 @@ def main():
     ctx.set_fixed_base(use_fb)
     grp_fb = use_fb and not use_crt          # 4096-bit keys: k_fb_digits, k_fbg, k_fbg_garner + k_fbg_fin
     fb_info = None
+    fb_pair = 0
     if use_fb:
         ctx.set_fb_window(args.fb_window)     # a dedicated encrypt GPU: the largest tables that fit its HBM
         t0 = time.perf_counter()
@@ -227,11 +247,12 @@ def main():
             setup["fixed_base_unavailable"] = str(exc)
         setup["fixed_base_build_wall_ms"] = (time.perf_counter() - t0) * 1e3
         use_fb = ctx.fb_ready
+        fb_pair = ctx.fb_pair if use_fb else 0
         if use_fb:
             fb_info = ctx.fixed_base_info()
             h_ms, d_ms, tbytes = ctx.fixed_base_setup()
             setup.update({"fixed_base_host_ms": h_ms, "fixed_base_device_ms": d_ms, "fixed_base_table_bytes": tbytes,
-                          "fixed_base_note": "once per key: bases + B_k on the host, hipMalloc, k_fb_lohi + k_fb_fill; "
+                          "fixed_base_note": "once per key: bases + B_k on the host, hipMalloc, k_fb(p)_lohi + k_fb(p)_fill; "
                                              "outside the timed region (the tables stay resident)"})
     ctx.set_stage_timing(True)
     lib = _native.load_library()
@@ -386,18 +407,20 @@ def main():
         torch.cuda.synchronize()
         dec_ms = d0.elapsed_time(d1)
         dst = ctx.stage_times()
+        dec_pair = bool(ctx.pair_paths & 1)
+        wd = work_dec_pair(nb) if dec_pair else work_dec(nb)
         if ctx.lane_decrypt and len(dst) == 3:
-            wd = work_dec(nb)
             extra["decrypt_stages"] = {
                 "k_dec_pre": {"kernel_ms": dst[0]},
                 "k_dec_pow": {"kernel_ms": dst[1], "work_mac_per_elem": wd,
                               "achieved_tmac_s": N * wd / (dst[1] * 1e-3) / 1e12},
                 "k_dec_fin": {"kernel_ms": dst[2]}}
-        extra["decrypt_path"] = "lane" if ctx.lane_decrypt else "group"
+        extra["decrypt_path"] = ("lane-pair" if dec_pair else "lane") if ctx.lane_decrypt else "group"
         ok = bool(torch.equal(val[:n_real], x[:n_real].double())) and int((stt[:n_real] > 1).sum().item()) == 0
         extra["decrypt_per_s_per_gpu"] = N / (dec_ms * 1e-3)
         extra["decrypt_kernel_ms"] = dec_ms
-        extra["decrypt_int_mac_frac"] = N * work_dec(nb) / (dec_ms * 1e-3) / INT_MAC_PEAK
+        extra["decrypt_int_mac_frac"] = N * wd / (dec_ms * 1e-3) / INT_MAC_PEAK
+        extra["decrypt_w_dec_equivalent_frac"] = N * work_dec(nb) / (dec_ms * 1e-3) / INT_MAC_PEAK
         extra["roundtrip_exact"] = ok
         if not ok:
             raise SystemExit("decrypt(encrypt(x)) != x on the device")
@@ -419,6 +442,8 @@ def main():
         torch.cuda.synchronize()
         if use_crt:
             wc = work_crt(nb)
+            if ctx.pair_paths & 2:   # stage B on pairs: (P(h) + 2) pair products per half
+                wc["k_crt_b"] = float(2 * (_P(nb // 2) + 2) * _Mp(nb // 64))
             extra["generic_crt_path"] = {
                 "value": N / (sum(gen_ms) * 1e-3), "unit": "encrypts/s per GPU",
                 "note": "r from the ChaCha20 stream and r^n by CRT exponentiation (kernels_crt.hpp); "
@@ -567,6 +592,8 @@ def main():
     else:
         if grp_fb:
             names, works = ["k_fb_digits", "k_fbg", "k_fbg_fin"], work_fbg(nb, fb_info[2])
+        elif use_crt and use_fb and fb_pair:
+            names, works = ["k_fb_digits", "k_fbp", "k_fb_fin"], work_fbp(nb, fb_info[2])
         elif use_crt and use_fb:
             names, works = ["k_fb_digits", "k_fb", "k_fb_fin"], work_fb(nb, fb_info[2])
         elif use_crt:
@@ -581,7 +608,7 @@ def main():
         extra["stages"] = stages
         achieved = N * dom_work / (dom_ms * 1e-3)
         enc_ms = float(sum(stage_avg))
-        extra["path"] = "crt-fixedbase" if use_fb else "crt" if use_crt else "public"
+        extra["path"] = ("crt-fixedbase-pair" if fb_pair else "crt-fixedbase") if use_fb else "crt" if use_crt else "public"
         if use_fb:
             extra["fixed_base"] = {"g_p": fb_info[0], "g_q": fb_info[1], "digits": fb_info[2], "window_bits": fb_info[3]}
         extra["encrypt_call_ms"] = enc_ms
@@ -664,9 +691,12 @@ def main():
                    "elements_per_gpu": N, "parallelism": f"dp{world}"},
         "roofline": {"bound": "valu-int-mac", "achieved": achieved / 1e12, "peak": INT_MAC_PEAK / 1e12,
                      "unit": "TMAC/s", "frac": achieved / INT_MAC_PEAK,
-                     "traffic": load_traffic(dom, N, nb, fb_info[3] if (use_fb and dom in ("k_fb", "k_fbg")) else None),
+                     "traffic": load_traffic(dom, N, nb, fb_info[3] if (use_fb and dom in ("k_fb", "k_fbp", "k_fbg")) else None),
                      "kernel": dom, "kernel_ms": dom_ms,
-                     "work_per_unit": (f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} table "
+                     "work_per_unit": (f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} pair "
+                                       f"products mod p_h^2 per half, 5 s^2 + 2 s each over s = nb/64 32-bit limbs of p_h, "
+                                       f"kernels_fbp.hpp), not SURVEY.md §8d's W_enc" if dom == "k_fbp" else
+                                       f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} table "
                                        f"products per half, 32-bit limbs, kernels_fb.hpp), not SURVEY.md §8d's W_enc"
                                        if dom in ("k_fb", "k_fbg") else f"{dom_work:.4g} canonical 32x32->64 MAC per element (SURVEY.md §8d)")},
         "roofline_hbm": {"bound": "hbm", "achieved": extra.get("hbm_algorithmic_gbs"), "peak": HBM_PEAK_GBS,

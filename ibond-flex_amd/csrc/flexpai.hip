@@ -18,6 +18,7 @@
 #include "engine_lane.hpp"
 #include "engine_fb.hpp"
 #include "engine_fbp.hpp"
+#include "engine_pair.hpp"
 #include "engine_grp.hpp"
 #include "engine_mul.hpp"
 
@@ -69,6 +70,14 @@ struct pai_ctx {
   bool dec_lane_enabled = true;
   int dec_kchunks = 0;
   DecLaneHalf* d_dec_halves = nullptr;
+  // p-adic pair exponentiations (kernels_pair.hpp): decryption and CRT stage B on the S limbs of p_h;
+  // the default for 1024/2048-bit keys ($FLEXPAI_PAIR=0 selects the 2S-limb lane kernels)
+  bool dec_pair_ok = false, crt_pair_ok = false;
+  DecPairHalf* d_decp_halves = nullptr;
+  CrtHalf* d_decp_pow = nullptr;
+  CrtHalf* d_crtp_b = nullptr;
+  uint32_t *d_decp_nl = nullptr, *d_decp_maxint = nullptr;
+  int decp_kchunks = 0;
   CrtHalf* d_dec_pow = nullptr;   // [2] exponentiation halves: p_h^2, op list for p_h - 1
   uint32_t *d_dec_p = nullptr, *d_dec_q = nullptr, *d_dec_qinvR = nullptr, *d_dec_nl = nullptr, *d_dec_maxint = nullptr;
   uint32_t dec_pprime = 0;
@@ -726,7 +735,7 @@ static int setup_fbg(pai_ctx* c, const HBig& p, const HBig& q) {
 
 // CRT encryption constants (kernels_crt.hpp). p < q here (sorted like keypair.py:57-62).
 static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
-  c->crt_ok = c->fbg_ok = false;
+  c->crt_ok = c->fbg_ok = c->dec_pair_ok = c->crt_pair_ok = false;
   const size_t pb = std::max(p.bits(), q.bits());
   int sa = 0, sb = 0;
   for (auto cand : {std::pair<int, int>{19, 37}, std::pair<int, int>{37, 74}}) {
@@ -826,6 +835,55 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
     c->dec_kchunks = kd;
     c->dec_lane_ok = true;
   }
+  // pair kernels: residues mod p_h^2 as (A, B) over the sa limbs of p_h, R = 2^(28 sa) >= 2^12 p_h
+  bool pair = true;
+  if (const char* e = getenv("FLEXPAI_PAIR")) pair = atoi(e) != 0;
+  if (pair && (size_t)LB * sa >= pb + 12) {
+    const int S2 = 2 * sa;
+    auto split = [&](const HBig& v, const HBig& P) {   // canonical pair of v < P^2
+      const HBig qt = div_big(v, P), rm = sub(v, mul(qt, P));
+      std::vector<uint32_t> out = rm.limbs(sa, LB), b = qt.limbs(sa, LB);
+      out.insert(out.end(), b.begin(), b.end());
+      return out;
+    };
+    const int kp = (int)((32 * (size_t)c->ct_words + RA - 1) / RA);
+    std::vector<uint32_t> one(S2, 0);
+    one[0] = 1;
+    DecPairHalf dp[2];
+    CrtHalf pw[2], pbh[2];
+    for (int h = 0; h < 2; ++h) {
+      const HBig& ph = primes[h];
+      const HBig& other = primes[1 - h];
+      const HBig& m2 = sq[h];
+      std::vector<uint32_t> pd, pe;
+      if (!build_lane_program(sub(ph, HBig(1)), pd) || !build_lane_program(ph, pe)) return 0;
+      HBig oi = inv_mod(mod(other, ph), ph);
+      HBig coef = inv_mod(sq[1 - h], m2);
+      if (oi.is_zero() || coef.is_zero()) return 0;
+      const uint32_t mp1 = mont_prime(ph, LB);
+      uint32_t *dph, *dck, *dhR, *dpm1, *done, *dprog, *dr2, *dcoef, *dpe;
+      if ((rc = upload(c, ph.limbs(sa, LB), &dph)) ||
+          (rc = upload(c, split(mul_pow2_mod(HBig(1), RA * (kp + 1), m2), ph), &dck)) ||
+          (rc = upload(c, mul_pow2_mod(sub(ph, oi), RA, ph).limbs(sa, LB), &dhR)) ||
+          (rc = upload(c, sub(ph, HBig(1)).limbs(sa, LB), &dpm1)) || (rc = upload(c, one, &done)) ||
+          (rc = upload(c, pd, &dprog)) || (rc = upload(c, split(mul_pow2_mod(HBig(1), 2 * RA, m2), ph), &dr2)) ||
+          (rc = upload(c, split(coef, ph), &dcoef)) || (rc = upload(c, pe, &dpe)))
+        return rc;
+      dp[h] = DecPairHalf{dph, dck, dhR, dpm1, mp1, 0u};
+      pw[h] = CrtHalf{dph, nullptr, done, dprog, (int)pd.size(), mp1};
+      pbh[h] = CrtHalf{dph, dr2, dcoef, dpe, (int)pe.size(), mp1};
+    }
+    std::vector<DecPairHalf> dpv(dp, dp + 2);
+    std::vector<CrtHalf> pwv(pw, pw + 2), pbv(pbh, pbh + 2);
+    HBig maxint = sub(div_small(c->n, 3), HBig(1));
+    if ((rc = upload(c, dpv, &c->d_decp_halves)) || (rc = upload(c, pwv, &c->d_decp_pow)) ||
+        (rc = upload(c, pbv, &c->d_crtp_b)) || (rc = upload(c, c->n.limbs(S2, LB), &c->d_decp_nl)) ||
+        (rc = upload(c, maxint.limbs(S2, LB), &c->d_decp_maxint)))
+      return rc;
+    c->decp_kchunks = kp;
+    c->dec_pair_ok = c->dec_lane_ok;   // shares the lane decrypt's p, q, q^-1 R constants
+    c->crt_pair_ok = true;
+  }
   return 0;
 }
 
@@ -850,7 +908,7 @@ int pai_ctx_set_private(pai_ctx* c, const uint8_t* p_le, const uint8_t* q_le, si
     for (void* a : c->priv_allocs) (void)hipFree(a);
     c->priv_allocs.clear();
     (void)hipGetLastError();
-    c->has_priv = c->crt_ok = c->fbg_ok = c->dec_lane_ok = false;
+    c->has_priv = c->crt_ok = c->fbg_ok = c->dec_lane_ok = c->dec_pair_ok = c->crt_pair_ok = false;
     c->fb_state = pai_ctx::FB_UNTRIED;
     g_last_error = msg;
   }
@@ -943,6 +1001,8 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
       return 0;
     case PAI_OPT_FB_WINDOW: *value = c->fb_W_used ? c->fb_W_used : c->fb_W ? c->fb_W : fb_default_window(); return 0;
     case PAI_OPT_FB_READY: *value = c->fb_state == pai_ctx::FB_READY ? 1 : 0; return 0;
+    case PAI_OPT_FB_PAIR: *value = c->fb_state == pai_ctx::FB_READY ? c->fb_pair_s : 0; return 0;
+    case PAI_OPT_PAIR: *value = (c->dec_pair_ok && c->dec_lane_enabled ? 1 : 0) | (c->crt_pair_ok ? 2 : 0); return 0;
   }
   return fail(PAI_ERR_ARG, "pai_ctx_get_option: unknown option");
 }
@@ -1136,6 +1196,8 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
   const long long chunk = std::min(N, CRT_CHUNK);
   int occA = 1, occB = 1;
   if (crt_lane_occupancy(SA, &occA, &occB)) return fail(PAI_ERR_KEY, "CRT encrypt: unsupported size");
+  const bool bpair = c->crt_pair_ok;   // stage B on pairs (kernels_pair.hpp)
+  if (bpair && crt_b_pair_occupancy(SA, &occB)) return fail(PAI_ERR_KEY, "CRT encrypt: unsupported size");
   const long long lanes_blocks = (chunk + LANE_BLOCK - 1) / LANE_BLOCK;
   const int gxA = (int)std::max<long long>(1, std::min<long long>(lanes_blocks, (long long)occA * c->cus / 2));
   const int gxB = (int)std::max<long long>(1, std::min<long long>(lanes_blocks, (long long)occB * c->cus / 2));
@@ -1168,13 +1230,14 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
     stage_mark(c, 1, st);
     HIPCHK(hipGetLastError());
     CrtParams pb{};
-    pb.halves = c->d_crt_b;
+    pb.halves = bpair ? c->d_crtp_b : c->d_crt_b;
     pb.n = n;
     pb.yin = y;
     pb.out = u;
     pb.scratch = (uint32_t*)c->d_scratch;
     const int gB = (int)std::min<long long>(gxB, (n + LANE_BLOCK - 1) / LANE_BLOCK);
-    HIPCHK(crt_launch_b(SA, pb, gB, st));
+    if (bpair) HIPCHK(crt_b_pair_launch(SA, pb, gB, st));
+    else HIPCHK(crt_launch_b(SA, pb, gB, st));
     HIPCHK(hipGetLastError());
     stage_mark(c, 2, st);
     CrtFinParams f{};
@@ -1338,6 +1401,49 @@ static int launch_decrypt(pai_ctx* c, DecParams& p, hipStream_t st) {
   return 0;
 }
 
+// pair decryption (kernels_pair.hpp, engine_pair.hip), in chunks of CRT_CHUNK elements
+static int launch_dec_pair(pai_ctx* c, const DecParams& d, hipStream_t st) {
+  const long long N = d.n;
+  const long long chunk = std::min(N, CRT_CHUNK);
+  const int S = c->crt_sa;
+  DecLaneGeom g;
+  if (dec_pair_geometry(S, c->cus, chunk, &g)) return fail(PAI_ERR_KEY, "pair decrypt: unsupported size");
+  int rc = ensure_scratch(c, g.scratch_bytes);
+  if (rc) return rc;
+  if ((rc = ensure_work(c, (size_t)4 * S * chunk * 4))) return rc;
+  for (long long off = 0; off < N; off += chunk) {
+    const long long n = std::min(chunk, N - off);
+    hipEvent_t* ev = stage_chunk(c);
+    if (ev) c->nev = 4;
+    uint32_t* xw = (uint32_t*)c->d_work;   // [2][2S][n]: c~, then x_h in place
+    DecPairPreParams pre{c->d_decp_halves, n, d.ct + (size_t)off * c->ct_words, c->ct_words, c->decp_kchunks, xw};
+    CrtParams pw{};
+    pw.halves = c->d_decp_pow;
+    pw.n = n;
+    pw.yin = xw;
+    pw.out = xw;
+    pw.scratch = (uint32_t*)c->d_scratch;
+    DecPairFinParams f{};
+    f.halves = c->d_decp_halves;
+    f.n = n;
+    f.xh = xw;
+    f.exp = d.exp + off;
+    f.p = c->d_dec_p;
+    f.q = c->d_dec_q;
+    f.qinvR = c->d_dec_qinvR;
+    f.pprime = c->dec_pprime;
+    f.nlimb = c->d_decp_nl;
+    f.maxint = c->d_decp_maxint;
+    f.val = d.val + off;
+    f.mant = d.mant ? d.mant + off : nullptr;
+    f.status = d.status + off;
+    f.raw = d.raw ? d.raw + (size_t)off * c->pt_words : nullptr;
+    f.pt_words = c->pt_words;
+    HIPCHK(dec_pair_launch(S, pre, pw, f, g, st, ev));
+  }
+  return 0;
+}
+
 // lane-engine decryption (kernels_dec.hpp, engine_dec.hip), in chunks of CRT_CHUNK elements
 static int launch_dec_lane(pai_ctx* c, const DecParams& d, hipStream_t st) {
   const long long N = d.n;
@@ -1408,6 +1514,7 @@ int pai_decrypt_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size
   p.pt_words = c->pt_words;
   p.n_limbs = c->n_limbs;
   hipStream_t st = (hipStream_t)stream;
+  if (c->dec_pair_ok && c->dec_lane_enabled) return launch_dec_pair(c, p, st);
   if (c->dec_lane_ok && c->dec_lane_enabled) return launch_dec_lane(c, p, st);
   switch (c->tpi_d) {
     case 1: return launch_decrypt<1>(c, p, st);

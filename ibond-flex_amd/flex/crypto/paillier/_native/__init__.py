@@ -22,7 +22,7 @@ PAI_EXP_AUTO, PAI_EXP_FIXED = 0, 1
 EL_OK, EL_INT, EL_INT_BIG, EL_OVERFLOW, EL_FLOAT_OVF, EL_ENC_RANGE = 0, 1, 2, 3, 4, 5
 
 PAI_OPT_CRT_ENCRYPT, PAI_OPT_CRT_AVAILABLE, PAI_OPT_STAGE_TIMING, PAI_OPT_LANE_DECRYPT = 1, 2, 3, 4
-PAI_OPT_FIXED_BASE, PAI_OPT_FB_WINDOW, PAI_OPT_FB_READY = 5, 6, 7
+PAI_OPT_FIXED_BASE, PAI_OPT_FB_WINDOW, PAI_OPT_FB_READY, PAI_OPT_FB_PAIR, PAI_OPT_PAIR = 5, 6, 7, 8, 9
 
 EXPORTED = ("pai_device_count", "pai_device_mem_info", "pai_ctx_create", "pai_ctx_set_private", "pai_ctx_destroy", "pai_ctx_info", "pai_last_error",
             "pai_ctx_set_option", "pai_ctx_get_option", "pai_ctx_stage_times", "pai_ctx_fixed_base_info",
@@ -257,6 +257,16 @@ class Context:
     def fb_ready(self) -> bool:
         """True when the fixed-base tables are resident on the device."""
         return bool(self._get_option(PAI_OPT_FB_READY))
+
+    @property
+    def fb_pair(self) -> int:
+        """Limbs of p_h of the resident pair tables (kernels_fbp.hpp: k_fbp), 0 for k_fb tables or none."""
+        return int(self._get_option(PAI_OPT_FB_PAIR))
+
+    @property
+    def pair_paths(self) -> int:
+        """Bit 0: decryption, bit 1: CRT encryption stage B on p-adic pairs (kernels_pair.hpp)."""
+        return int(self._get_option(PAI_OPT_PAIR))
 
     def prepare_fixed_base(self):
         """Build the fixed-base tables now (NativeError with the reason when unavailable)."""

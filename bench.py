@@ -415,7 +415,8 @@ def main():
                 "k_dec_pow": {"kernel_ms": dst[1], "work_mac_per_elem": wd,
                               "achieved_tmac_s": N * wd / (dst[1] * 1e-3) / 1e12},
                 "k_dec_fin": {"kernel_ms": dst[2]}}
-        extra["decrypt_path"] = ("lane-pair" if dec_pair else "lane") if ctx.lane_decrypt else "group"
+        extra["decrypt_path"] = (("lane-pair" if dec_pair else "lane") if ctx.lane_decrypt
+                                 else "split-pair (kernels_dec4.hpp)" if dec_pair else "group")
         ok = bool(torch.equal(val[:n_real], x[:n_real].double())) and int((stt[:n_real] > 1).sum().item()) == 0
         extra["decrypt_per_s_per_gpu"] = N / (dec_ms * 1e-3)
         extra["decrypt_kernel_ms"] = dec_ms

@@ -19,6 +19,7 @@
 #include "engine_fb.hpp"
 #include "engine_fbp.hpp"
 #include "engine_pair.hpp"
+#include "engine_dec4.hpp"
 #include "engine_grp.hpp"
 #include "engine_mul.hpp"
 
@@ -78,6 +79,10 @@ struct pai_ctx {
   CrtHalf* d_crtp_b = nullptr;
   uint32_t *d_decp_nl = nullptr, *d_decp_maxint = nullptr;
   int decp_kchunks = 0;
+  // 4096-bit keys: decryption on split pairs (kernels_dec4.hpp), the default; the group k_decrypt otherwise
+  bool dec4_ok = false;
+  Dec4Half* d_dec4_halves = nullptr;
+  int dec4_kchunks = 0;
   CrtHalf* d_dec_pow = nullptr;   // [2] exponentiation halves: p_h^2, op list for p_h - 1
   uint32_t *d_dec_p = nullptr, *d_dec_q = nullptr, *d_dec_qinvR = nullptr, *d_dec_nl = nullptr, *d_dec_maxint = nullptr;
   uint32_t dec_pprime = 0;
@@ -730,12 +735,52 @@ static int setup_fbg(pai_ctx* c, const HBig& p, const HBig& q) {
   c->fb_p = p;
   c->fb_q = q;
   c->fbg_ok = true;
+  // split-pair decryption (kernels_dec4.hpp): p_h of at most 28 * 74 - 24 bits (R >= 2^24 p_h), the ciphertext
+  // in at most 4 chunks of 74 limbs; $FLEXPAI_PAIR=0 keeps the group engine's k_decrypt
+  bool pair = true;
+  if (const char* e = getenv("FLEXPAI_PAIR")) pair = atoi(e) != 0;
+  const size_t RS = (size_t)LB * D4_S;
+  const int kp = (int)((32 * (size_t)c->ct_words + RS - 1) / RS);
+  if (pair && pb + 24 <= RS && kp <= 4 && c->tpi_d == 4) {
+    const HBig primes[2] = {p, q};
+    Dec4Half dh[2];
+    for (int h = 0; h < 2; ++h) {
+      const HBig& ph = primes[h];
+      const HBig m2 = mul(ph, ph);
+      auto split = [&](const HBig& v) {
+        const HBig qt = div_big(v, ph), rm = sub(v, mul(qt, ph));
+        std::vector<uint32_t> out = rm.limbs(D4_S, LB), b = qt.limbs(D4_S, LB);
+        out.insert(out.end(), b.begin(), b.end());
+        return out;
+      };
+      auto one_minus = [&](const HBig& r) {   // (1 - r) mod p_h for 0 < r < p_h
+        return mod(sub(add(ph, HBig(1)), r), ph);
+      };
+      std::vector<uint32_t> pd;
+      if (!build_lane_program(sub(ph, HBig(1)), pd)) return 0;
+      HBig oi = inv_mod(mod(primes[1 - h], ph), ph);
+      if (oi.is_zero()) return 0;
+      const HBig hh = sub(ph, oi);
+      uint32_t *dp, *dx1, *dxk, *dck, *dhr, *dprog;
+      if ((rc = upload(c, ph.limbs(D4_S, LB), &dp)) ||
+          (rc = upload(c, one_minus(mul_pow2_mod(HBig(1), RS, ph)).limbs(D4_S, LB), &dx1)) ||
+          (rc = upload(c, one_minus(mul_pow2_mod(HBig(1), RS * kp, ph)).limbs(D4_S, LB), &dxk)) ||
+          (rc = upload(c, split(mul_pow2_mod(HBig(1), RS * (kp + 1), m2)), &dck)) ||
+          (rc = upload(c, mul_pow2_mod(hh, RS, ph).limbs(D4_S, LB), &dhr)) || (rc = upload(c, pd, &dprog)))
+        return rc;
+      dh[h] = Dec4Half{dp, dx1, dxk, dck, dhr, dprog, (int)pd.size(), mont_prime(ph, LB)};
+    }
+    std::vector<Dec4Half> dv(dh, dh + 2);
+    if ((rc = upload(c, dv, &c->d_dec4_halves))) return rc;
+    c->dec4_kchunks = kp;
+    c->dec4_ok = true;
+  }
   return 0;
 }
 
 // CRT encryption constants (kernels_crt.hpp). p < q here (sorted like keypair.py:57-62).
 static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
-  c->crt_ok = c->fbg_ok = c->dec_pair_ok = c->crt_pair_ok = false;
+  c->crt_ok = c->fbg_ok = c->dec_pair_ok = c->crt_pair_ok = c->dec4_ok = false;
   const size_t pb = std::max(p.bits(), q.bits());
   int sa = 0, sb = 0;
   for (auto cand : {std::pair<int, int>{19, 37}, std::pair<int, int>{37, 74}}) {
@@ -908,7 +953,7 @@ int pai_ctx_set_private(pai_ctx* c, const uint8_t* p_le, const uint8_t* q_le, si
     for (void* a : c->priv_allocs) (void)hipFree(a);
     c->priv_allocs.clear();
     (void)hipGetLastError();
-    c->has_priv = c->crt_ok = c->fbg_ok = c->dec_lane_ok = c->dec_pair_ok = c->crt_pair_ok = false;
+    c->has_priv = c->crt_ok = c->fbg_ok = c->dec_lane_ok = c->dec_pair_ok = c->crt_pair_ok = c->dec4_ok = false;
     c->fb_state = pai_ctx::FB_UNTRIED;
     g_last_error = msg;
   }
@@ -1002,7 +1047,9 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
     case PAI_OPT_FB_WINDOW: *value = c->fb_W_used ? c->fb_W_used : c->fb_W ? c->fb_W : fb_default_window(); return 0;
     case PAI_OPT_FB_READY: *value = c->fb_state == pai_ctx::FB_READY ? 1 : 0; return 0;
     case PAI_OPT_FB_PAIR: *value = c->fb_state == pai_ctx::FB_READY ? c->fb_pair_s : 0; return 0;
-    case PAI_OPT_PAIR: *value = (c->dec_pair_ok && c->dec_lane_enabled ? 1 : 0) | (c->crt_pair_ok ? 2 : 0); return 0;
+    case PAI_OPT_PAIR:
+      *value = ((c->dec_pair_ok || c->dec4_ok) && c->dec_lane_enabled ? 1 : 0) | (c->crt_pair_ok ? 2 : 0);
+      return 0;
   }
   return fail(PAI_ERR_ARG, "pai_ctx_get_option: unknown option");
 }
@@ -1444,6 +1491,42 @@ static int launch_dec_pair(pai_ctx* c, const DecParams& d, hipStream_t st) {
   return 0;
 }
 
+// 4096-bit split-pair decryption (kernels_dec4.hpp, engine_dec4.hip), in chunks of CRT_CHUNK elements
+static int launch_dec4(pai_ctx* c, const DecParams& d, hipStream_t st) {
+  const long long N = d.n;
+  const long long chunk = std::min(N, CRT_CHUNK);
+  Dec4Geom g;
+  dec4_geometry(c->cus, chunk, &g);
+  int rc = ensure_scratch(c, g.scratch_bytes);
+  if (rc) return rc;
+  const size_t xbytes = (size_t)2 * 2 * D4_S * 4, mbytes = (size_t)2 * D4_S * 4;   // per element
+  if ((rc = ensure_work(c, (xbytes + mbytes) * chunk))) return rc;
+  for (long long off = 0; off < N; off += chunk) {
+    const long long n = std::min(chunk, N - off);
+    hipEvent_t* ev = stage_chunk(c);
+    if (ev) c->nev = 4;
+    Dec4Params p{};
+    p.halves = c->d_dec4_halves;
+    p.n = n;
+    p.ct = d.ct + (size_t)off * c->ct_words;
+    p.ct_words = c->ct_words;
+    p.kchunks = c->dec4_kchunks;
+    p.x = (uint32_t*)c->d_work;
+    p.mh = (uint32_t*)((char*)c->d_work + xbytes * chunk);
+    p.scratch = (uint32_t*)c->d_scratch;
+    DecParams f = d;
+    f.ct += (size_t)off * c->ct_words;
+    f.exp += off;
+    f.n = n;
+    f.val += off;
+    if (f.mant) f.mant += off;
+    f.status += off;
+    if (f.raw) f.raw += (size_t)off * c->pt_words;
+    HIPCHK(dec4_launch(p, f, g, st, ev));
+  }
+  return 0;
+}
+
 // lane-engine decryption (kernels_dec.hpp, engine_dec.hip), in chunks of CRT_CHUNK elements
 static int launch_dec_lane(pai_ctx* c, const DecParams& d, hipStream_t st) {
   const long long N = d.n;
@@ -1515,6 +1598,7 @@ int pai_decrypt_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size
   p.n_limbs = c->n_limbs;
   hipStream_t st = (hipStream_t)stream;
   if (c->dec_pair_ok && c->dec_lane_enabled) return launch_dec_pair(c, p, st);
+  if (c->dec4_ok && c->dec_lane_enabled) return launch_dec4(c, p, st);
   if (c->dec_lane_ok && c->dec_lane_enabled) return launch_dec_lane(c, p, st);
   switch (c->tpi_d) {
     case 1: return launch_decrypt<1>(c, p, st);

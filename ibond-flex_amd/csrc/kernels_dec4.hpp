@@ -1,0 +1,379 @@
+// CRT decryption for 4096-bit keys on p-adic pairs split over a lane pair (bn_pair.hpp's algebra).
+//
+// p_h has 2048 bits, S = 74 limbs: a pair (A, B) with v = A + p_h B (mod p_h^2) and its two CIOS rows
+// (2 x 74 64-bit accumulators) do not fit one lane next to the operand, so the rows go to the two lanes of a
+// lane pair (element-half e: lanes 2e, 2e+1). Both lanes hold the same register operand and run the same
+// instruction stream; they differ only in the digits they stream from LDS and in one DPP step:
+//   even lane: P += a y_j + q1 p           (U = REDC(A1 A2), the A row)
+//   odd lane : P += a y_j + (LMASK - q1) + q2 p, P started at X = (1 - R) mod p_h   (the B row:
+//              REDC(a y - m) with m the even lane's reduction digits q1_j, received by DPP each digit;
+//              the LMASK - q1_j digits and X keep every accumulator non-negative, bn_pair.hpp)
+// A square (A, B)^2 streams A's digits to the even lane and 2B's to the odd one: the pair square costs
+// 2 x 2 S^2 lane-MACs, against 2 (2S)^2 for the Montgomery square over the 148 limbs of p_h^2 that the TPI = 4
+// group engine runs (k_decrypt). A product x t needs A_x B_t + B_x A_t in the B row: a second pass REDC(B_x A_t)
+// (the even lane's copy is discarded) is added to the first (< 4p, a valid operand: R >= 2^24 p_h).
+//
+//   k_dec4_pre  per element-half: c R as a pair (one split CIOS over the ciphertext's limbs against the
+//               constant pair of R^(K+1))
+//   k_dec4_pow  per element-half: c^(p_h - 1) by the lane machine's op list (kernels_crt.hpp) on split
+//               pairs, left in plain form by a product with (1, 0)              (decryptor.py:55-61)
+//   k_dec4_L    per element-half: L_h = B of the canonical pair (A = 1; A = 0 for c == 0 mod p_h, L = B - 1),
+//               m_h = L_h h_h mod p_h
+//   k_dec4_fin  per element (lane group of 4, the bn_group engine): CRT (gmpy_math.py:31-40) and
+//               FixedPointNumber.decode, as k_decrypt's last steps
+#pragma once
+#include "kernels_fb.hpp"   // opaque_uniform
+
+namespace fpai {
+
+constexpr int D4_S = 74;                     // limbs of p_h
+constexpr int D4_PAIRS = LANE_BLOCK / 2;     // element-halves per block
+constexpr int D4_SLOT = 4 * D4_S;            // LDS words per element-half: x [A][B], t [A][B]
+
+struct Dec4Half {
+  const uint32_t* p;       // p_h, S limbs
+  const uint32_t* X1;      // (1 - R) mod p_h
+  const uint32_t* XK;      // (1 - R^K) mod p_h, K = ciphertext chunks of S limbs
+  const uint32_t* cK;      // pair of R^(K+1) mod p_h^2 ([A: S][B: S])
+  const uint32_t* hR;      // h_h R mod p_h
+  const uint32_t* prog;    // lane-machine op list for c^(p_h - 1) (kernels_crt.hpp)
+  int nprog;
+  uint32_t mprime;
+};
+
+struct Dec4Params {
+  const Dec4Half* halves;  // [2]
+  long long n;
+  const uint32_t* ct;
+  int ct_words;
+  int kchunks;
+  uint32_t* x;             // [2][2S][n]: pairs (A: limbs 0..S-1, B: S..2S-1)
+  uint32_t* mh;            // [2][S][n]
+  uint32_t* scratch;       // per-lane tiles (LaneScratch, tile_quads<S> quads per tile)
+};
+
+template <int S, int J>
+__device__ __forceinline__ void d4_step(uint64_t (&P)[S], const uint32_t (&a)[S], const uint32_t* __restrict__ dig,
+                                        uint32_t& cur, int sh, const uint32_t (&m)[S], uint32_t mprime, bool subq) {
+  const uint32_t y = cur << sh;
+  if constexpr (J + 1 < S) cur = dig[J + 1];
+#pragma unroll
+  for (int i = 0; i < S; ++i) P[(i + J) % S] += (uint64_t)a[i] * y;
+  const uint32_t q0 = ((uint32_t)P[J] * mprime) & lane::LMASK;
+  const uint32_t q1 = __builtin_amdgcn_update_dpp(0u, q0, 0xA0, 0xF, 0xF, false);   // quad_perm [0,0,2,2]: even lane's q
+  P[J] += subq ? (uint64_t)(lane::LMASK - q1) : 0ull;
+  const uint32_t q = ((uint32_t)P[J] * mprime) & lane::LMASK;
+#pragma unroll
+  for (int i = 0; i < S; ++i) P[(i + J) % S] += (uint64_t)q * m[i];
+  P[(J + 1) % S] += P[J] >> lane::LB;
+  P[J] = 0;
+  lane::pin<S>(P);
+  __builtin_amdgcn_sched_barrier(0);
+}
+// S digits dig[0..S) (shifted left by sh) against the register operand a; subq: this lane is the B row of a
+// pair pass (it takes LMASK - q1 of its even neighbour at each digit)
+template <int S, int... Js>
+__device__ __forceinline__ void d4_pass(uint64_t (&P)[S], const uint32_t (&a)[S], const uint32_t* __restrict__ dig, int sh,
+                                        const uint32_t (&m)[S], uint32_t mprime, bool subq, std::integer_sequence<int, Js...>) {
+  uint32_t cur = dig[0];
+  (d4_step<S, Js>(P, a, dig, cur, sh, m, mprime, subq), ...);
+}
+
+__device__ __forceinline__ void d4_fence() { wave_lds_fence(); }
+
+// ---------------------------------------------------------------- c~ = c R mod p_h^2 as a pair
+// The constant pair of R^(K+1) (A in the even lane, B in the odd) times the ciphertext's K S digits (staged
+// in LDS), R^-K: one split CIOS, the odd row started at (1 - R^K) mod p_h.
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK, 1) void k_dec4_pre(Dec4Params p) {
+  __shared__ uint32_t lds[D4_PAIRS * D4_SLOT];
+  const int half = blockIdx.y;
+  const Dec4Half* H = p.halves + half;
+  uint32_t m[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) m[j] = H->p[j];
+  const uint32_t mprime = H->mprime;
+  const int tig = threadIdx.x & 1;
+  const bool odd = tig != 0;
+  const int pib = threadIdx.x >> 1;
+  uint32_t* sx = lds + pib * D4_SLOT;
+  for (long long base = (long long)blockIdx.x * D4_PAIRS; base < p.n; base += (long long)gridDim.x * D4_PAIRS) {
+    const long long e = base + pib;
+    const bool valid = e < p.n;
+    const long long ee = valid ? e : p.n - 1;
+    {
+      const uint32_t* cw = p.ct + ee * p.ct_words;
+      const int nw = p.ct_words;
+      d4_fence();
+      for (int k = tig; k < p.kchunks * S; k += 2) {
+        const int bit = k * lane::LB, wi = bit >> 5, sh = bit & 31;
+        const uint64_t lo = wi < nw ? (uint64_t)cw[wi] : 0ull;
+        const uint64_t hi = wi + 1 < nw ? (uint64_t)cw[wi + 1] : 0ull;
+        sx[k] = (uint32_t)(((hi << 32) | lo) >> sh) & lane::LMASK;
+      }
+      d4_fence();
+    }
+    uint32_t a[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) a[i] = H->cK[tig * S + i];
+    uint64_t P[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) P[i] = odd ? (uint64_t)H->XK[i] : 0ull;
+#pragma unroll 1
+    for (int k = 0; k < p.kchunks; ++k)
+      d4_pass<S>(P, a, sx + k * S, 0, m, mprime, odd, std::make_integer_sequence<int, S>{});
+    uint32_t y[S];
+    lane::normalize<S>(P, y);
+    if (valid) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) p.x[((size_t)half * 2 * S + tig * S + i) * p.n + e] = y[i];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- x_h = c~^(p_h - 1), plain pair
+// The lane machine of kernels_crt.hpp (same op list: SQR, MUL with the multiplier from a tile, the constant,
+// or as set, A_FROM_T, STORE, B_SET) on split pairs. Each lane keeps its own component of every tile (the
+// even lane A, the odd lane B). A square is one split pass; a product two (pass 2 adds REDC(B_x A_t) to the
+// B row). Every pass goes through ONE d4_pass call site.
+template <int S, int... Gs>
+__device__ __forceinline__ void d4_tile_store(const LaneScratch& t, int k, const uint32_t* src, std::integer_sequence<int, Gs...>) {
+  constexpr int TQ = tile_quads<S>();
+  ((t.quad(k * TQ + Gs) = make_uint4(4 * Gs < S ? src[4 * Gs] : 0u, 4 * Gs + 1 < S ? src[4 * Gs + 1] : 0u,
+                                     4 * Gs + 2 < S ? src[4 * Gs + 2] : 0u, 4 * Gs + 3 < S ? src[4 * Gs + 3] : 0u)),
+   ...);
+}
+template <int S, int... Gs>
+__device__ __forceinline__ void d4_tile_load(const LaneScratch& t, int k, uint32_t* dst, std::integer_sequence<int, Gs...>) {
+  constexpr int TQ = tile_quads<S>();
+  uint4 v[sizeof...(Gs)];
+  ((v[Gs] = t.quad(k * TQ + Gs)), ...);
+  d4_fence();
+  (((4 * Gs < S ? (dst[4 * Gs] = v[Gs].x) : 0u), (4 * Gs + 1 < S ? (dst[4 * Gs + 1] = v[Gs].y) : 0u),
+    (4 * Gs + 2 < S ? (dst[4 * Gs + 2] = v[Gs].z) : 0u), (4 * Gs + 3 < S ? (dst[4 * Gs + 3] = v[Gs].w) : 0u)),
+   ...);
+  d4_fence();
+}
+
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK, 1) void k_dec4_pow(Dec4Params p) {
+  constexpr int TQ = tile_quads<S>();
+  using Q = std::make_integer_sequence<int, TQ>;
+  __shared__ uint32_t lds[D4_PAIRS * D4_SLOT + S];
+  const int half = blockIdx.y;
+  const Dec4Half* H = p.halves + half;
+  uint32_t m[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) m[j] = H->p[j];
+  const uint32_t mprime = H->mprime;
+  const int nprog = H->nprog;
+  const uint32_t* prog = H->prog;
+  uint32_t* x1 = lds + D4_PAIRS * D4_SLOT;   // (1 - R) mod p_h: the odd row's start (LDS: no SGPRs)
+  for (int i = threadIdx.x; i < S; i += blockDim.x) x1[i] = H->X1[i];
+  __syncthreads();
+  const int tig = threadIdx.x & 1;
+  const bool odd = tig != 0;
+  const int pib = threadIdx.x >> 1;
+  uint32_t* sx = lds + pib * D4_SLOT;
+  uint32_t* st = sx + 2 * S;
+  const LaneScratch tl = lane_scratch(p.scratch);
+  for (long long base = (long long)blockIdx.x * D4_PAIRS; base < p.n; base += (long long)gridDim.x * D4_PAIRS) {
+    const long long e = base + pib;
+    const bool valid = e < p.n;
+    const long long ee = valid ? e : p.n - 1;
+    uint32_t a[S];
+    {
+      d4_fence();
+#pragma unroll
+      for (int i = 0; i < S; ++i) sx[tig * S + i] = p.x[((size_t)half * 2 * S + tig * S + i) * p.n + ee];
+      d4_fence();
+      d4_tile_store<S>(tl, 0, sx + tig * S, Q{});
+#pragma unroll
+      for (int i = 0; i < S; ++i) a[i] = sx[i];
+    }
+    for (int i = 0; i <= nprog; ++i) {
+      const uint32_t op = (i < nprog) ? lane_op(prog, i) : LOP_B_CONST;
+      if (op & LOP_A_FROM_T) {
+        d4_tile_load<S>(tl, (op >> 16) & 0xFF, sx + tig * S, Q{});
+#pragma unroll
+        for (int j = 0; j < S; ++j) a[j] = sx[j];
+      }
+      const bool sqr = (op & LOP_SQR) != 0;
+      if (sqr && (op & LOP_PREFETCH)) d4_tile_load<S>(tl, (op >> 8) & 0xFF, st + tig * S, Q{});   // next MUL's (B_READY)
+      if (!sqr) {   // the multiplier -> st
+        if (op & LOP_B_CONST) {
+          d4_fence();
+#pragma unroll
+          for (int j = 0; j < S; ++j) st[tig * S + j] = (tig == 0 && j == 0) ? 1u : 0u;   // (1, 0): leave Montgomery form
+          d4_fence();
+        } else if (!(op & LOP_B_READY)) {
+          d4_tile_load<S>(tl, (op >> 8) & 0xFF, st + tig * S, Q{});
+        }
+      }
+      for (int ps = 0; ps < (sqr ? 1 : 2); ++ps) {
+        const bool second = ps == 1;
+        uint64_t P[S];
+#pragma unroll
+        for (int j = 0; j < S; ++j) P[j] = (odd && !second) ? (uint64_t)x1[j] : 0ull;
+        const uint32_t* dig = sqr ? sx + tig * S : second ? st : st + tig * S;
+        d4_pass<S>(P, a, dig, sqr ? tig : 0, m, mprime, odd && !second, std::make_integer_sequence<int, S>{});
+        uint32_t y[S];
+        lane::normalize<S>(P, y);
+        if (!second) {
+          d4_fence();
+          if (!sqr) {
+#pragma unroll
+            for (int j = 0; j < S; ++j) a[j] = sx[S + j];   // B_x: pass 2's operand
+          }
+          d4_fence();
+#pragma unroll
+          for (int j = 0; j < S; ++j) sx[tig * S + j] = y[j];
+          d4_fence();
+        } else {
+          uint32_t c = 0;
+#pragma unroll
+          for (int j = 0; j < S; ++j) {   // B row += B_x A_t (< 4p)
+            const uint32_t v = sx[S + j] + y[j] + c;
+            y[j] = v & lane::LMASK;
+            c = v >> lane::LB;
+          }
+          d4_fence();
+          if (odd) {
+#pragma unroll
+            for (int j = 0; j < S; ++j) sx[S + j] = y[j];
+          }
+          d4_fence();
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < S; ++j) a[j] = sx[j];
+      if (op & LOP_STORE) d4_tile_store<S>(tl, op >> 24, sx + tig * S, Q{});
+      if (op & LOP_B_SET) {
+        d4_fence();
+#pragma unroll
+        for (int j = 0; j < S; ++j) st[tig * S + j] = sx[tig * S + j];
+        d4_fence();
+      }
+    }
+    if (valid) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) p.x[((size_t)half * 2 * S + tig * S + i) * p.n + e] = sx[tig * S + i];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- m_h = L_h h_h mod p_h
+// one lane per element-half: the canonical pair of x_h (A < 2p, B < 4p on entry) gives L_h = B (A = 1), or
+// B - 1 (A = 0: c == 0 mod p_h, the reference's floor division); then REDC(L_h h_h R) with h_h R's digits
+// broadcast from LDS.
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK) void k_dec4_L(Dec4Params p) {
+  __shared__ uint32_t hr[S];
+  const int half = blockIdx.y;
+  const Dec4Half* H = p.halves + half;
+  for (int i = threadIdx.x; i < S; i += blockDim.x) hr[i] = H->hR[i];
+  __syncthreads();
+  uint32_t m[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) m[j] = H->p[j];
+  for (long long e = (long long)blockIdx.x * LANE_BLOCK + threadIdx.x; e < p.n; e += (long long)gridDim.x * LANE_BLOCK) {
+    uint32_t a[S], b[S], d[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      a[i] = p.x[((size_t)half * 2 * S + i) * p.n + e];
+      b[i] = p.x[((size_t)half * 2 * S + S + i) * p.n + e];
+    }
+    const bool lt = lane::sub<S>(a, m, d);
+    uint32_t c = lt ? 0u : 1u;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      a[i] = lt ? a[i] : d[i];
+      const uint32_t v = b[i] + c;
+      b[i] = v & lane::LMASK;
+      c = v >> lane::LB;
+    }
+#pragma unroll 1
+    for (int r = 0; r < 4; ++r) lane::cond_sub<S>(b, m);
+    uint32_t nz = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) nz |= a[i];
+    if (nz == 0) {
+      uint32_t one[S];
+#pragma unroll
+      for (int i = 0; i < S; ++i) one[i] = i == 0 ? 1u : 0u;
+      const bool neg = lane::sub<S>(b, one, d);
+#pragma unroll
+      for (int i = 0; i < S; ++i) b[i] = neg ? m[i] - (i == 0 ? 1u : 0u) : d[i];
+    }
+    uint64_t P[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) P[i] = 0;
+    d4_pass<S>(P, b, hr, 0, m, H->mprime, false, std::make_integer_sequence<int, S>{});
+    lane::normalize<S>(P, b);
+    lane::cond_sub<S>(b, m);
+#pragma unroll
+    for (int i = 0; i < S; ++i) p.mh[((size_t)half * S + i) * p.n + e] = b[i];
+  }
+}
+
+// CRT + decode from m_p, m_q ([2][74][n]) on a lane group of TPI = 4 (S = 148), k_decrypt's steps 8-9
+template <int TPI>
+__global__ __launch_bounds__(BLOCK) void k_dec4_fin(DecParams p, const uint32_t* __restrict__ mh) {
+  constexpr int S = TPI * L;
+  constexpr int GPB = BLOCK / TPI;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int tig = threadIdx.x % TPI;
+  const int gib = threadIdx.x / TPI;
+  uint32_t* eslot = smem + gib * S;
+  const DecHalf* H0 = p.halves;
+  for (long long base = (long long)blockIdx.x * GPB; base < p.n; base += (long long)gridDim.x * GPB) {
+    const long long inst = base + gib;
+    const bool valid = inst < p.n;
+    const long long ii = valid ? inst : p.n - 1;
+    uint32_t mp[L], mq[L];
+    {
+      int t = tig;
+      asm volatile("" : "+v"(t));
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+        const int limb = t * L + i;
+        mp[i] = limb < D4_S ? mh[(size_t)limb * p.n + ii] : 0u;
+        mq[i] = limb < D4_S ? mh[((size_t)D4_S + limb) * p.n + ii] : 0u;
+      }
+    }
+    uint32_t p0[L], a1[L], a2[L], u[L];
+    load_limbs_g<TPI>(H0->ph, p0, tig);
+    copy_g_to_lds<TPI>(eslot, p.qinvR, tig);
+    montmul<TPI>(a1, mp, eslot, TPI, p0, H0->pprime, lane, tig);
+    cond_sub<TPI>(a1, p0, lane, tig);
+    montmul<TPI>(a2, mq, eslot, TPI, p0, H0->pprime, lane, tig);
+    cond_sub<TPI>(a2, p0, lane, tig);
+    {
+      const bool neg = sub_limbs<TPI>(a1, a2, u, lane, tig);
+      uint64_t P[L];
+#pragma unroll
+      for (int i = 0; i < L; ++i) P[i] = (uint64_t)u[i] + (neg ? p0[i] : 0u);
+      normalize<TPI>(P, u, lane, tig);
+    }
+    uint32_t nlm[L], uq[L], x[L];
+    load_limbs_g<TPI>(p.nlimb, nlm, tig);
+    copy_g_to_lds<TPI>(eslot, p.qRn, tig);
+    montmul<TPI>(uq, u, eslot, TPI, nlm, p.nprime, lane, tig);
+    cond_sub<TPI>(uq, nlm, lane, tig);
+    {
+      uint64_t P[L];
+#pragma unroll
+      for (int i = 0; i < L; ++i) P[i] = (uint64_t)uq[i] + mq[i];
+      normalize<TPI>(P, x, lane, tig);
+    }
+    write_limbs_lds<TPI>(eslot, x, tig);
+    if (valid && p.raw) {
+      for (int j = tig; j < p.pt_words; j += TPI) p.raw[ii * p.pt_words + j] = limbs_word(eslot, S, j);
+    }
+    if (valid && tig == 0) decode_element(eslot, p, ii);
+    wave_lds_fence();
+  }
+}
+
+}  // namespace fpai

@@ -116,6 +116,14 @@ def work_fbg(nb: int, digits: int) -> dict:
     return {"k_fb_digits": 0.0, "k_fbg": float(2 * digits * _M(s)), "k_fbg_fin": float(_M(s) + _M(nb // 16))}
 
 
+def work_fbgp(nb: int, digits: int) -> dict:
+    """The 4096-bit sampler on pair groups (kernels_grp_pair.hpp): K pair products per half over the nb/64
+    32-bit limbs of p_h; the fin stage adds k_fbgp_w's product mod p_h^2 per half to the Garner work."""
+    s = nb // 64
+    return {"k_fb_digits": 0.0, "k_fbgp": float(2 * digits * _Mp(s)),
+            "k_fbg_fin": float(2 * _M(nb // 32) + _M(nb // 32) + _M(nb // 16))}
+
+
 def work_dec(nb: int) -> float:
     return float(2 * (_P(nb // 2) + 2) * _M(nb // 32))
 
@@ -591,7 +599,9 @@ def main():
         achieved = N * dom_work / (dom_ms * 1e-3)
         extra["k_add_ms"] = add_ms
     else:
-        if grp_fb:
+        if grp_fb and fb_pair:
+            names, works = ["k_fb_digits", "k_fbgp", "k_fbg_fin"], work_fbgp(nb, fb_info[2])
+        elif grp_fb:
             names, works = ["k_fb_digits", "k_fbg", "k_fbg_fin"], work_fbg(nb, fb_info[2])
         elif use_crt and use_fb and fb_pair:
             names, works = ["k_fb_digits", "k_fbp", "k_fb_fin"], work_fbp(nb, fb_info[2])
@@ -692,11 +702,11 @@ def main():
                    "elements_per_gpu": N, "parallelism": f"dp{world}"},
         "roofline": {"bound": "valu-int-mac", "achieved": achieved / 1e12, "peak": INT_MAC_PEAK / 1e12,
                      "unit": "TMAC/s", "frac": achieved / INT_MAC_PEAK,
-                     "traffic": load_traffic(dom, N, nb, fb_info[3] if (use_fb and dom in ("k_fb", "k_fbp", "k_fbg")) else None),
+                     "traffic": load_traffic(dom, N, nb, fb_info[3] if (use_fb and dom in ("k_fb", "k_fbp", "k_fbg", "k_fbgp")) else None),
                      "kernel": dom, "kernel_ms": dom_ms,
                      "work_per_unit": (f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} pair "
                                        f"products mod p_h^2 per half, 5 s^2 + 2 s each over s = nb/64 32-bit limbs of p_h, "
-                                       f"kernels_fbp.hpp), not SURVEY.md §8d's W_enc" if dom == "k_fbp" else
+                                       f"kernels_fbp.hpp), not SURVEY.md §8d's W_enc" if dom in ("k_fbp", "k_fbgp") else
                                        f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} table "
                                        f"products per half, 32-bit limbs, kernels_fb.hpp), not SURVEY.md §8d's W_enc"
                                        if dom in ("k_fb", "k_fbg") else f"{dom_work:.4g} canonical 32x32->64 MAC per element (SURVEY.md §8d)")},

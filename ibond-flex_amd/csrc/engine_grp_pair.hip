@@ -1,0 +1,39 @@
+// Pair-group fixed-base kernels for 4096-bit keys (kernels_grp_pair.hpp): instantiations and launches.
+#include "engine_grp_pair.hpp"
+
+namespace fpai {
+
+static size_t pg_lds() { return ((size_t)(BLOCK / FBGP_TPI) * 2 * FBGP_S + FBGP_S) * 4; }
+static size_t w_lds() { return (size_t)(BLOCK / 4) * 4 * L * 4; }
+
+int fbgp_occupancy(int* occ) {
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, k_fbgp<FBGP_TPI, FBGP_LL>, BLOCK, pg_lds()) != hipSuccess ||
+      *occ < 1)
+    *occ = 1;
+  return 0;
+}
+
+hipError_t fbgp_launch(const FbgpParams& p, int gx, hipStream_t st) {
+  hipLaunchKernelGGL((k_fbgp<FBGP_TPI, FBGP_LL>), dim3(gx, 2), dim3(BLOCK), pg_lds(), st, p);
+  return hipGetLastError();
+}
+
+hipError_t fbgp_launch_w(const FbgpParams& p, int gx, hipStream_t st) {
+  hipLaunchKernelGGL(k_fbgp_w<4>, dim3(gx, 2), dim3(BLOCK), w_lds(), st, p);
+  return hipGetLastError();
+}
+
+hipError_t fbgp_build_tables(const FbgpHalf* d_halves, uint32_t* t0, uint32_t* t1, int K, int W, hipStream_t st) {
+  constexpr int GPB = BLOCK / FBGP_TPI;
+  const int LO = W / 2, HI = W - LO;
+  const int nent = (1 << LO) + (1 << HI);
+  hipLaunchKernelGGL((k_fbgp_lohi<FBGP_TPI, FBGP_LL>), dim3((nent + GPB - 1) / GPB, K, 2), dim3(BLOCK), pg_lds(), st,
+                     d_halves, K, W);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_fbgp_fill<FBGP_TPI, FBGP_LL>), dim3(((1 << W) + GPB - 1) / GPB, K, 2), dim3(BLOCK), pg_lds(), st,
+                     d_halves, K, W, t0, t1);
+  return hipGetLastError();
+}
+
+}  // namespace fpai

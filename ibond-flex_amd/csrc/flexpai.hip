@@ -20,6 +20,7 @@
 #include "engine_fbp.hpp"
 #include "engine_pair.hpp"
 #include "engine_dec4.hpp"
+#include "engine_grp_pair.hpp"
 #include "engine_grp.hpp"
 #include "engine_mul.hpp"
 
@@ -100,6 +101,8 @@ struct pai_ctx {
   FbHalf* d_fb_halves = nullptr;
   FbpHalf* d_fbp_halves = nullptr;  // pair tables (kernels_fbp.hpp): the default for 1024/2048-bit keys
   int fb_pair_s = 0;            // limbs of p_h of the resident pair tables; 0 = k_fb tables
+  FbgpHalf* d_fbgp_halves = nullptr;  // 4096-bit keys: pair-group tables (kernels_grp_pair.hpp)
+  bool fb_gpair = false;
   FbRed* d_fb_red = nullptr;
   uint32_t *d_fb_m8 = nullptr, *d_fb_coefR = nullptr, *d_fb_q2 = nullptr, *d_fb_m0 = nullptr;
   uint32_t* d_fb_q2Rn = nullptr;  // 4096-bit keys: q^2 R mod n^2 (k_fbg_fin)
@@ -535,6 +538,8 @@ static void fb_release(pai_ctx* c) {
   c->d_fb_halves = nullptr;
   c->d_fbp_halves = nullptr;
   c->fb_pair_s = 0;
+  c->d_fbgp_halves = nullptr;
+  c->fb_gpair = false;
   c->d_fb_red = nullptr;
 }
 
@@ -589,7 +594,13 @@ static int ensure_fb(pai_ctx* c) {
   if (const char* e = getenv("FLEXPAI_FB_PAIR")) pair_ok = pair_ok && atoi(e) != 0;
   for (int h = 0; h < 2 && pair_ok; ++h)
     pair_ok = primes[h].bits() <= (size_t)32 * pw && primes[h].bits() + FBP_PB + 1 <= (size_t)LB * ps;
-  const int lohi_limbs = pair_ok ? std::max(sb, 2 * ps) : sb;
+  // 4096-bit keys: pair products on lane groups of 4 x 19 limbs (kernels_grp_pair.hpp), R = 2^(28 76) >= 2^24 p_h
+  bool gpair_ok = grp;
+  if (const char* e = getenv("FLEXPAI_FB_PAIR")) gpair_ok = gpair_ok && atoi(e) != 0;
+  for (int h = 0; h < 2 && gpair_ok; ++h)
+    gpair_ok = primes[h].bits() + 24 <= (size_t)LB * FBGP_S && primes[h].bits() <= (size_t)LB * FBGP_SP;
+  const int lohi_limbs = pair_ok ? std::max(sb, 2 * ps) : gpair_ok ? std::max(sb, 2 * FBGP_S) : sb;
+  FbgpHalf gv[2];
   FbpHalf pv[2];
   FbHalf hv[2];
   FbRed red[2];
@@ -668,6 +679,42 @@ static int ensure_fb(pai_ctx* c) {
         return fb_unavailable(c, pai_last_error());
       pv[h] = FbpHalf{(const uint4*)t[h], pp, pone, pbases, dlohi, pnm, ppbig, mont_prime(P, LB)};
     }
+    if (gpair_ok) {
+      // pair-group constants: S = 76 limbs of p_h, R = 2^(28 S); pairs as [A: S][B: S]
+      const HBig& P = primes[h];
+      const size_t RS = (size_t)LB * FBGP_S;
+      auto split = [&](const HBig& v, std::vector<uint32_t>& out) {
+        const HBig qt = div_big(v, P), rm = sub(v, mul(qt, P));
+        const std::vector<uint32_t> a = rm.limbs(FBGP_S, LB), b = qt.limbs(FBGP_S, LB);
+        out.insert(out.end(), a.begin(), a.end());
+        out.insert(out.end(), b.begin(), b.end());
+      };
+      std::vector<uint32_t> one_p, bases_p, nm_p;
+      split(mul_pow2_mod(HBig(1), RS, m2), one_p);
+      const int LOb = W / 2;
+      HBig y = M2.to(M2.pow(HBig(c->fb_g[h]), c->n));
+      for (int k = 0; k < K; ++k) {
+        HBig z = y;
+        split(mul_pow2_mod(M2.from(z), RS, m2), bases_p);
+        for (int q = 0; q < LOb; ++q) z = M2.mul(z, z);
+        split(mul_pow2_mod(M2.from(z), RS, m2), bases_p);
+        for (int q = 0; q < W; ++q) y = M2.mul(y, y);
+      }
+      for (int k = 0; k < 4; ++k) {
+        const std::vector<uint32_t> v = mul_pow2_mod(mod(primes[1 - h], P), (size_t)16 * k, P).limbs(FBGP_S, LB);
+        nm_p.insert(nm_p.end(), v.begin(), v.end());
+      }
+      const HBig r = mul_pow2_mod(HBig(1), RS, P);
+      const HBig X = mod(sub(add(P, HBig(1)), r), P);   // (1 - R) mod p_h
+      uint32_t *gp, *gx, *gone, *gbases, *gnm, *gpbig, *gp2, *gpr2;
+      if ((rc = upload_fb(c, P.limbs(FBGP_S, LB), &gp)) || (rc = upload_fb(c, X.limbs(FBGP_S, LB), &gx)) ||
+          (rc = upload_fb(c, one_p, &gone)) || (rc = upload_fb(c, bases_p, &gbases)) || (rc = upload_fb(c, nm_p, &gnm)) ||
+          (rc = upload_fb(c, mul(P, pow2(20)).limbs(FBGP_S, LB), &gpbig)) || (rc = upload_fb(c, m2.limbs(sb, LB), &gp2)) ||
+          (rc = upload_fb(c, mul_pow2_mod(P, RB, m2).limbs(sb, LB), &gpr2)))
+        return fb_unavailable(c, pai_last_error());
+      gv[h] = FbgpHalf{(const uint32_t*)t[h], gp, gx, gone, gbases, dlohi, gnm, gpbig, gp2, gpr2, mont_prime(P, LB),
+                       mont_prime(m2, LB)};
+    }
     if (h == 0) {
       c->d_fb_m0 = dm;
       c->fb_mprime0 = mont_prime(m2, LB);
@@ -697,7 +744,12 @@ static int ensure_fb(pai_ctx* c) {
     std::vector<FbpHalf> pvv(pv, pv + 2);
     if ((rc = upload_fb(c, pvv, &c->d_fbp_halves))) return fb_unavailable(c, pai_last_error());
   }
-  const hipError_t be = grp       ? grp_build_tables(c->d_fb_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
+  if (gpair_ok) {
+    std::vector<FbgpHalf> gvv(gv, gv + 2);
+    if ((rc = upload_fb(c, gvv, &c->d_fbgp_halves))) return fb_unavailable(c, pai_last_error());
+  }
+  const hipError_t be = gpair_ok  ? fbgp_build_tables(c->d_fbgp_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
+                        : grp     ? grp_build_tables(c->d_fb_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
                         : pair_ok ? fbp_build_tables(ps, c->d_fbp_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr)
                                   : fb_build_tables(sb, c->d_fb_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
   if (be != hipSuccess || hipDeviceSynchronize() != hipSuccess)
@@ -712,6 +764,7 @@ static int ensure_fb(pai_ctx* c) {
   c->fb_table_bytes = fb_bytes(c, W);
   c->fb_K = K;
   c->fb_pair_s = pair_ok ? ps : 0;
+  c->fb_gpair = gpair_ok;
   c->fb_W_used = W;
   c->fb_raw_bits = raw_bits;
   c->fb_state = pai_ctx::FB_READY;
@@ -1046,7 +1099,9 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
       return 0;
     case PAI_OPT_FB_WINDOW: *value = c->fb_W_used ? c->fb_W_used : c->fb_W ? c->fb_W : fb_default_window(); return 0;
     case PAI_OPT_FB_READY: *value = c->fb_state == pai_ctx::FB_READY ? 1 : 0; return 0;
-    case PAI_OPT_FB_PAIR: *value = c->fb_state == pai_ctx::FB_READY ? c->fb_pair_s : 0; return 0;
+    case PAI_OPT_FB_PAIR:
+      *value = c->fb_state == pai_ctx::FB_READY ? (c->fb_gpair ? FBGP_S : c->fb_pair_s) : 0;
+      return 0;
     case PAI_OPT_PAIR:
       *value = ((c->dec_pair_ok || c->dec4_ok) && c->dec_lane_enabled ? 1 : 0) | (c->crt_pair_ok ? 2 : 0);
       return 0;
@@ -1152,7 +1207,10 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
   const long long N = e.n;
   const long long chunk = std::min(N, CRT_CHUNK);
   int occF = 1, occG = 1;
-  if (grp) grp_occupancy(&occF);
+  if (grp) {
+    if (c->fb_gpair) fbgp_occupancy(&occF);
+    else grp_occupancy(&occF);
+  }
   else if (fb_occupancy(SB, &occF, &occG)) return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
   if (c->fb_pair_s && fbp_occupancy(c->fb_pair_s, &occF)) return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
   // elements per block: one per lane, or one per lane group (grp)
@@ -1198,6 +1256,13 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     if (c->fb_pair_s) {
       const FbpParams pp{c->d_fbp_halves, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
       HIPCHK(fbp_launch(c->fb_pair_s, pp, gF, st));
+    } else if (grp && c->fb_gpair) {
+      const FbgpParams pg{c->d_fbgp_halves, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
+      HIPCHK(fbgp_launch(pg, gF, st));
+      int occW = 1;
+      grp_fin_occupancy(&occW, &occG);
+      const long long gb4 = (n + BLOCK / 4 - 1) / (BLOCK / 4);
+      HIPCHK(fbgp_launch_w(pg, (int)std::max<long long>(1, std::min<long long>(gb4, (long long)occW * c->cus / 2)), st));
     } else {
       HIPCHK(grp ? grp_launch_fb(pf, gF, st) : fb_launch(SB, pf, gF, st));
     }

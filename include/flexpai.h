@@ -97,9 +97,10 @@ typedef struct pai_comm pai_comm;
                                     requested window whose 2 K 2^W rows fit $FLEXPAI_FB_MAX_BYTES (default:
                                     free device memory less 4 GiB)                                        */
 #define PAI_OPT_FB_READY 7       /* read-only: 1 when the fixed-base tables are resident                    */
-#define PAI_OPT_FB_PAIR 8        /* read-only: limbs of p_h (19 or 37) when the resident tables are pair tables
-                                    (kernels_fbp.hpp, the default for 1024/2048-bit keys; $FLEXPAI_FB_PAIR=0
-                                    selects k_fb), else 0                                                      */
+#define PAI_OPT_FB_PAIR 8        /* read-only: limbs of p_h (19, 37; 76 for the 4096-bit pair-group tables)
+                                    when the resident tables are pair tables (kernels_fbp.hpp,
+                                    kernels_grp_pair.hpp: the default; $FLEXPAI_FB_PAIR=0 selects k_fb / k_fbg),
+                                    else 0                                                                     */
 #define PAI_OPT_PAIR 9           /* read-only: bit 0 = decryption, bit 1 = CRT encryption (stage B) run on p-adic
                                     pairs (kernels_pair.hpp: the default for 1024/2048-bit keys; $FLEXPAI_PAIR=0
                                     selects the 2S-limb lane kernels)                                         */

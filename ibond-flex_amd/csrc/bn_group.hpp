@@ -44,10 +44,10 @@ __device__ __forceinline__ uint32_t bcast0(uint32_t v) {
   static_assert(TPI == 1 || TPI == 2 || TPI == 4 || TPI == 8 || TPI == 16, "TPI");
   if constexpr (TPI == 1) {
     return v;
-  } else if constexpr (TPI == 2) {
-    return __builtin_amdgcn_update_dpp(0u, v, 0xA0, 0xF, 0xF, false);   // quad_perm [0,0,2,2]
+  } else if constexpr (TPI == 2) {   // every lane is written: no old value (saves a v_mov per broadcast)
+    return __builtin_amdgcn_mov_dpp(v, 0xA0, 0xF, 0xF, false);          // quad_perm [0,0,2,2]
   } else if constexpr (TPI == 4) {
-    return __builtin_amdgcn_update_dpp(0u, v, 0x00, 0xF, 0xF, false);   // quad_perm [0,0,0,0]
+    return __builtin_amdgcn_mov_dpp(v, 0x00, 0xF, 0xF, false);          // quad_perm [0,0,0,0]
   } else if constexpr (TPI == 8) {
     uint32_t t = __builtin_amdgcn_update_dpp(0u, v, 0x00, 0xF, 0xF, false);
     return __builtin_amdgcn_update_dpp(t, t, 0x114, 0xF, 0xA, false);   // row_shr:4 into banks 1,3

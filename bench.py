@@ -476,15 +476,21 @@ def main():
         ctx.set_crt(False)
         ctx.set_fixed_base(False)
         encrypt(x, ct2, ex2, index_base_chk, npub)
-        pub_ms = ctx.stage_times()[0]
+        pub_st = ctx.stage_times()          # k_encrypt: one stage; split pairs: k_pe_pre, k_pe_pow, k_pe_fin
+        pub_ms = float(sum(pub_st))
+        pe = bool(ctx.pair_paths & 4) and len(pub_st) == 3
         ctx.set_crt(True)
         ctx.set_fixed_base(use_fb)
         torch.cuda.synchronize()
         ncmp = npub if use_crt else min(npub, S_chk)
         same = bool(torch.equal(ct2[:ncmp], ct_ref[:ncmp]))
+        wpe = float((_P(nb) + 1) * _Mp(nb // 32))   # W_enc with pair products over the nb/32 limbs of n
         extra["public_key_path"] = {"value": npub / (pub_ms * 1e-3), "unit": "encrypts/s per GPU", "elements": npub,
-                                    "kernel": "k_encrypt", "kernel_ms": pub_ms,
-                                    "int_mac_frac": npub * work_enc_public(nb) / (pub_ms * 1e-3) / INT_MAC_PEAK,
+                                    "kernel": "k_pe_pre + k_pe_pow + k_pe_fin (split pairs)" if pe else "k_encrypt",
+                                    "kernel_ms": pub_ms,
+                                    "stages_ms": dict(zip(["k_pe_pre", "k_pe_pow", "k_pe_fin"], pub_st)) if pe else None,
+                                    "int_mac_frac": npub * (wpe if pe else work_enc_public(nb)) / (pub_ms * 1e-3) / INT_MAC_PEAK,
+                                    "w_enc_equivalent_frac": npub * work_enc_public(nb) / (pub_ms * 1e-3) / INT_MAC_PEAK,
                                     "bit_identical_to_crt": same}
         del ct2, ex2
         if not same:

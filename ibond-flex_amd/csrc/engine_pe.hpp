@@ -1,0 +1,11 @@
+// Host interface of the public-key split-pair encryption unit (engine_pe.hip, kernels_pe.hpp).
+#pragma once
+#include "engine_dec4.hpp"
+#include "kernels_pe.hpp"
+
+namespace fpai {
+
+int pe_geometry(int cus, long long chunk, Dec4Geom* g);   // gx_pre, gx_pow, gx_L (= k_pe_fin), scratch_bytes
+hipError_t pe_launch(const PeParams& p, const Dec4Geom& g, hipStream_t st, hipEvent_t* ev);
+
+}  // namespace fpai

@@ -21,6 +21,7 @@
 #include "engine_pair.hpp"
 #include "engine_dec4.hpp"
 #include "engine_grp_pair.hpp"
+#include "engine_pe.hpp"
 #include "engine_grp.hpp"
 #include "engine_mul.hpp"
 
@@ -84,6 +85,9 @@ struct pai_ctx {
   bool dec4_ok = false;
   Dec4Half* d_dec4_halves = nullptr;
   int dec4_kchunks = 0;
+  // public-key encryption on split pairs (kernels_pe.hpp): 2048-bit n, the default ($FLEXPAI_PAIR=0: k_encrypt)
+  bool pe_ok = false;
+  PeConst* d_pe = nullptr;
   CrtHalf* d_dec_pow = nullptr;   // [2] exponentiation halves: p_h^2, op list for p_h - 1
   uint32_t *d_dec_p = nullptr, *d_dec_q = nullptr, *d_dec_qinvR = nullptr, *d_dec_nl = nullptr, *d_dec_maxint = nullptr;
   uint32_t dec_pprime = 0;
@@ -386,6 +390,8 @@ int pai_device_count(int* count) {
   return 0;
 }
 
+static int setup_pe(pai_ctx* c, const HBig& n);
+
 int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** out) {
   if (!n_le || !out || n_bytes == 0) return fail(PAI_ERR_ARG, "pai_ctx_create: null argument");
   HBig n = HBig::from_le_bytes(n_le, n_bytes);
@@ -439,7 +445,7 @@ int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** ou
   if ((rc = upload(c, rs, &c->d_RS)) || (rc = upload(c, c->N.limbs(c->S_e, LB), &c->d_N)) ||
       (rc = upload(c, R2.limbs(c->S_e, LB), &c->d_R2)) ||
       (rc = upload(c, n.limbs(c->S_e, LB), &c->d_nl)) || (rc = upload(c, prog, &c->d_prog)) ||
-      (rc = upload(c, oneR.limbs(c->S_e, LB), &c->d_oneR))) {
+      (rc = upload(c, oneR.limbs(c->S_e, LB), &c->d_oneR)) || (rc = setup_pe(c, n))) {
     delete c;
     return rc;
   }
@@ -488,6 +494,34 @@ static HBig div_big(const HBig& a, const HBig& m) {
   }
   q.trim();
   return q;
+}
+
+// Public-key encryption on split pairs (kernels_pe.hpp) for n of 1537..2048 bits: S = 74 limbs of n, R =
+// 2^(28 S) >= 2^24 n. Constants: n, (1 - R) and (1 - R^2) mod n, the pair of R^3 mod n^2, the op list for n.
+static int setup_pe(pai_ctx* c, const HBig& n) {
+  bool pair = true;
+  if (const char* e = getenv("FLEXPAI_PAIR")) pair = atoi(e) != 0;
+  const size_t RS = (size_t)LB * D4_S;
+  if (!pair || n.bits() + 24 > RS || n.bits() <= 1536) return 0;
+  std::vector<uint32_t> prog;
+  if (!build_lane_program(n, prog)) return 0;
+  const HBig n2 = mul(n, n);
+  auto one_minus = [&](const HBig& r) { return mod(sub(add(n, HBig(1)), r), n); };   // (1 - r) mod n, 0 < r < n
+  const HBig r3 = mul_pow2_mod(HBig(1), 3 * RS, n2);
+  const HBig qt = div_big(r3, n), rm = sub(r3, mul(qt, n));
+  std::vector<uint32_t> ck = rm.limbs(D4_S, LB), b = qt.limbs(D4_S, LB);
+  ck.insert(ck.end(), b.begin(), b.end());
+  uint32_t *dn, *dx1, *dxk, *dck, *dprog;
+  int rc;
+  if ((rc = upload(c, n.limbs(D4_S, LB), &dn)) ||
+      (rc = upload(c, one_minus(mul_pow2_mod(HBig(1), RS, n)).limbs(D4_S, LB), &dx1)) ||
+      (rc = upload(c, one_minus(mul_pow2_mod(HBig(1), 2 * RS, n)).limbs(D4_S, LB), &dxk)) ||
+      (rc = upload(c, ck, &dck)) || (rc = upload(c, prog, &dprog)))
+    return rc;
+  std::vector<PeConst> pc{PeConst{dn, dx1, dxk, dck, dprog, (int)prog.size(), mont_prime(n, LB)}};
+  if ((rc = upload(c, pc, &c->d_pe))) return rc;
+  c->pe_ok = true;
+  return 0;
 }
 
 template <typename T>
@@ -1103,7 +1137,8 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
       *value = c->fb_state == pai_ctx::FB_READY ? (c->fb_gpair ? FBGP_S : c->fb_pair_s) : 0;
       return 0;
     case PAI_OPT_PAIR:
-      *value = ((c->dec_pair_ok || c->dec4_ok) && c->dec_lane_enabled ? 1 : 0) | (c->crt_pair_ok ? 2 : 0);
+      *value = ((c->dec_pair_ok || c->dec4_ok) && c->dec_lane_enabled ? 1 : 0) | (c->crt_pair_ok ? 2 : 0) |
+               (c->pe_ok ? 4 : 0);
       return 0;
   }
   return fail(PAI_ERR_ARG, "pai_ctx_get_option: unknown option");
@@ -1296,6 +1331,47 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
   return 0;
 }
 
+// public-key encryption on split pairs (kernels_pe.hpp, engine_pe.hip), in chunks of CRT_CHUNK elements
+static int launch_pe(pai_ctx* c, const EncParams& e, hipStream_t st) {
+  const long long N = e.n;
+  const long long chunk = std::min(N, CRT_CHUNK);
+  Dec4Geom g;
+  pe_geometry(c->cus, chunk, &g);
+  int rc = ensure_scratch(c, g.scratch_bytes);
+  if (rc) return rc;
+  const size_t xbytes = (size_t)2 * D4_S * 4;   // per element, + 8 for M
+  if ((rc = ensure_work(c, (xbytes + 8) * chunk))) return rc;
+  const size_t esz = e.dtype == PAI_F32 ? 4 : 8;
+  for (long long off = 0; off < N; off += chunk) {
+    const long long n = std::min(chunk, N - off);
+    hipEvent_t* ev = stage_chunk(c);
+    if (ev) c->nev = 4;
+    PeParams p{};
+    p.k = c->d_pe;
+    p.x = (const char*)e.x + (size_t)off * esz;
+    p.dtype = e.dtype;
+    p.exp_mode = e.exp_mode;
+    p.fexp = e.fexp;
+    p.obf = e.obf;
+    p.r = e.r ? e.r + (size_t)off * e.r_stride : nullptr;
+    p.r_stride = e.r_stride;
+    p.r_words = e.r_words;
+    p.rng_words = e.rng_words;
+    std::memcpy(p.rng_key, e.rng_key, sizeof(p.rng_key));
+    p.index_base = e.index_base + (unsigned long long)off;
+    p.n = n;
+    p.xw = (uint32_t*)c->d_work;
+    p.M = (int64_t*)((char*)c->d_work + xbytes * chunk);
+    p.scratch = (uint32_t*)c->d_scratch;
+    p.ct = e.ct + (size_t)off * c->ct_words;
+    p.ct_words = c->ct_words;
+    p.exp = e.exp + off;
+    p.status = e.status ? e.status + off : nullptr;
+    HIPCHK(pe_launch(p, g, st, ev));
+  }
+  return 0;
+}
+
 template <int SA, int SB>
 static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
   static_assert(SB == 2 * SA || SB == 2 * SA - 1, "stage sizes");
@@ -1423,6 +1499,7 @@ int pai_encrypt_dev(pai_ctx* c, int dtype, const void* d_x, size_t N, int exp_mo
     if (c->crt_sa == 19) return launch_crt<19, 37>(c, p, st);
     if (c->crt_sa == 37) return launch_crt<37, 74>(c, p, st);
   }
+  if (obf_mode != PAI_OBF_NONE && c->pe_ok && c->ct_words == 2 * 64) return launch_pe(c, p, st);
   switch (c->tpi_e) {
     case 2: return launch_encrypt<2>(c, p, st);
     case 4: return launch_encrypt<4>(c, p, st);

@@ -155,6 +155,81 @@ __device__ __forceinline__ void d4_tile_load(const LaneScratch& t, int k, uint32
   d4_fence();
 }
 
+// The op list on split pairs: x = (a = A in registers, sx = [A][B] in LDS, each lane's component in its
+// tiles); st = the multiplier. final_b(st + tig S) writes this lane's component of the final multiplier
+// (LOP_B_CONST). Every pass goes through ONE d4_pass call site.
+template <int S, class FinalB>
+__device__ __forceinline__ void d4_run(uint32_t (&a)[S], uint32_t* sx, uint32_t* st, const LaneScratch& tl,
+                                       const uint32_t* __restrict__ prog, int nprog, const uint32_t* x1,
+                                       const uint32_t (&m)[S], uint32_t mprime, int tig, FinalB&& final_b) {
+  constexpr int TQ = tile_quads<S>();
+  using Q = std::make_integer_sequence<int, TQ>;
+  const bool odd = tig != 0;
+  for (int i = 0; i <= nprog; ++i) {
+    const uint32_t op = (i < nprog) ? lane_op(prog, i) : LOP_B_CONST;
+    if (op & LOP_A_FROM_T) {
+      d4_tile_load<S>(tl, (op >> 16) & 0xFF, sx + tig * S, Q{});
+#pragma unroll
+      for (int j = 0; j < S; ++j) a[j] = sx[j];
+    }
+    const bool sqr = (op & LOP_SQR) != 0;
+    if (sqr && (op & LOP_PREFETCH)) d4_tile_load<S>(tl, (op >> 8) & 0xFF, st + tig * S, Q{});   // next MUL's (B_READY)
+    if (!sqr) {   // the multiplier -> st
+      if (op & LOP_B_CONST) {
+        d4_fence();
+        final_b(st + tig * S);
+        d4_fence();
+      } else if (!(op & LOP_B_READY)) {
+        d4_tile_load<S>(tl, (op >> 8) & 0xFF, st + tig * S, Q{});
+      }
+    }
+    for (int ps = 0; ps < (sqr ? 1 : 2); ++ps) {
+      const bool second = ps == 1;
+      uint64_t P[S];
+#pragma unroll
+      for (int j = 0; j < S; ++j) P[j] = (odd && !second) ? (uint64_t)x1[j] : 0ull;
+      const uint32_t* dig = sqr ? sx + tig * S : second ? st : st + tig * S;
+      d4_pass<S>(P, a, dig, sqr ? tig : 0, m, mprime, odd && !second, std::make_integer_sequence<int, S>{});
+      uint32_t y[S];
+      lane::normalize<S>(P, y);
+      if (!second) {
+        d4_fence();
+        if (!sqr) {
+#pragma unroll
+          for (int j = 0; j < S; ++j) a[j] = sx[S + j];   // B_x: pass 2's operand
+        }
+        d4_fence();
+#pragma unroll
+        for (int j = 0; j < S; ++j) sx[tig * S + j] = y[j];
+        d4_fence();
+      } else {
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < S; ++j) {   // B row += B_x A_t (< 4p)
+          const uint32_t v = sx[S + j] + y[j] + c;
+          y[j] = v & lane::LMASK;
+          c = v >> lane::LB;
+        }
+        d4_fence();
+        if (odd) {
+#pragma unroll
+          for (int j = 0; j < S; ++j) sx[S + j] = y[j];
+        }
+        d4_fence();
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < S; ++j) a[j] = sx[j];
+    if (op & LOP_STORE) d4_tile_store<S>(tl, op >> 24, sx + tig * S, Q{});
+    if (op & LOP_B_SET) {
+      d4_fence();
+#pragma unroll
+      for (int j = 0; j < S; ++j) st[tig * S + j] = sx[tig * S + j];
+      d4_fence();
+    }
+  }
+}
+
 template <int S>
 __global__ __launch_bounds__(LANE_BLOCK, 1) void k_dec4_pow(Dec4Params p) {
   constexpr int TQ = tile_quads<S>();
@@ -172,7 +247,6 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_dec4_pow(Dec4Params p) {
   for (int i = threadIdx.x; i < S; i += blockDim.x) x1[i] = H->X1[i];
   __syncthreads();
   const int tig = threadIdx.x & 1;
-  const bool odd = tig != 0;
   const int pib = threadIdx.x >> 1;
   uint32_t* sx = lds + pib * D4_SLOT;
   uint32_t* st = sx + 2 * S;
@@ -191,70 +265,10 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_dec4_pow(Dec4Params p) {
 #pragma unroll
       for (int i = 0; i < S; ++i) a[i] = sx[i];
     }
-    for (int i = 0; i <= nprog; ++i) {
-      const uint32_t op = (i < nprog) ? lane_op(prog, i) : LOP_B_CONST;
-      if (op & LOP_A_FROM_T) {
-        d4_tile_load<S>(tl, (op >> 16) & 0xFF, sx + tig * S, Q{});
+    d4_run<S>(a, sx, st, tl, prog, nprog, x1, m, mprime, tig, [&](uint32_t* dst) {   // (1, 0): leave Montgomery form
 #pragma unroll
-        for (int j = 0; j < S; ++j) a[j] = sx[j];
-      }
-      const bool sqr = (op & LOP_SQR) != 0;
-      if (sqr && (op & LOP_PREFETCH)) d4_tile_load<S>(tl, (op >> 8) & 0xFF, st + tig * S, Q{});   // next MUL's (B_READY)
-      if (!sqr) {   // the multiplier -> st
-        if (op & LOP_B_CONST) {
-          d4_fence();
-#pragma unroll
-          for (int j = 0; j < S; ++j) st[tig * S + j] = (tig == 0 && j == 0) ? 1u : 0u;   // (1, 0): leave Montgomery form
-          d4_fence();
-        } else if (!(op & LOP_B_READY)) {
-          d4_tile_load<S>(tl, (op >> 8) & 0xFF, st + tig * S, Q{});
-        }
-      }
-      for (int ps = 0; ps < (sqr ? 1 : 2); ++ps) {
-        const bool second = ps == 1;
-        uint64_t P[S];
-#pragma unroll
-        for (int j = 0; j < S; ++j) P[j] = (odd && !second) ? (uint64_t)x1[j] : 0ull;
-        const uint32_t* dig = sqr ? sx + tig * S : second ? st : st + tig * S;
-        d4_pass<S>(P, a, dig, sqr ? tig : 0, m, mprime, odd && !second, std::make_integer_sequence<int, S>{});
-        uint32_t y[S];
-        lane::normalize<S>(P, y);
-        if (!second) {
-          d4_fence();
-          if (!sqr) {
-#pragma unroll
-            for (int j = 0; j < S; ++j) a[j] = sx[S + j];   // B_x: pass 2's operand
-          }
-          d4_fence();
-#pragma unroll
-          for (int j = 0; j < S; ++j) sx[tig * S + j] = y[j];
-          d4_fence();
-        } else {
-          uint32_t c = 0;
-#pragma unroll
-          for (int j = 0; j < S; ++j) {   // B row += B_x A_t (< 4p)
-            const uint32_t v = sx[S + j] + y[j] + c;
-            y[j] = v & lane::LMASK;
-            c = v >> lane::LB;
-          }
-          d4_fence();
-          if (odd) {
-#pragma unroll
-            for (int j = 0; j < S; ++j) sx[S + j] = y[j];
-          }
-          d4_fence();
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < S; ++j) a[j] = sx[j];
-      if (op & LOP_STORE) d4_tile_store<S>(tl, op >> 24, sx + tig * S, Q{});
-      if (op & LOP_B_SET) {
-        d4_fence();
-#pragma unroll
-        for (int j = 0; j < S; ++j) st[tig * S + j] = sx[tig * S + j];
-        d4_fence();
-      }
-    }
+      for (int j = 0; j < S; ++j) dst[j] = (tig == 0 && j == 0) ? 1u : 0u;
+    });
     if (valid) {
 #pragma unroll
       for (int i = 0; i < S; ++i) p.x[((size_t)half * 2 * S + tig * S + i) * p.n + e] = sx[tig * S + i];

@@ -101,9 +101,10 @@ typedef struct pai_comm pai_comm;
                                     when the resident tables are pair tables (kernels_fbp.hpp,
                                     kernels_grp_pair.hpp: the default; $FLEXPAI_FB_PAIR=0 selects k_fb / k_fbg),
                                     else 0                                                                     */
-#define PAI_OPT_PAIR 9           /* read-only: bit 0 = decryption, bit 1 = CRT encryption (stage B) run on p-adic
-                                    pairs (kernels_pair.hpp: the default for 1024/2048-bit keys; $FLEXPAI_PAIR=0
-                                    selects the 2S-limb lane kernels)                                         */
+#define PAI_OPT_PAIR 9           /* read-only: bit 0 = decryption, bit 1 = CRT encryption (stage B), bit 2 =
+                                    public-key encryption (2048-bit n) run on p-adic pairs (kernels_pair.hpp,
+                                    kernels_dec4.hpp, kernels_pe.hpp: the default; $FLEXPAI_PAIR=0 at context
+                                    creation selects the kernels they replace)                                */
 
 /* Number of visible GPUs (0 when there is none or the runtime cannot start). */
 int pai_device_count(int* count);

@@ -1,0 +1,77 @@
+"""GPU parity of the public-key encryption on split pairs (kernels_pe.hpp: k_pe_pre / k_pe_pow / k_pe_fin, the
+path of every party that holds only the public key, 2048-bit n) against the reference golden vectors
+(explicit r: encryptor.py:48-69 with random_value), the CPU oracle (device ChaCha20 obfuscators) and the
+group-engine kernel it replaces (k_encrypt, $FLEXPAI_PAIR=0): bit-identical ciphertexts, exponents, statuses."""
+import numpy as np
+import pytest
+
+from oracle import paillier_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _native():
+    from flex.crypto.paillier import _native
+    return _native
+
+
+@pytest.fixture(scope="module")
+def key2048(golden):
+    k = golden["keys"]["2048"]
+    return O.Key(int(k["n"], 16), int(k["p"], 16), int(k["q"], 16))
+
+
+def _pub(monkeypatch, key, pair):
+    monkeypatch.setenv("FLEXPAI_PAIR", "1" if pair else "0")
+    ctx = _native().Context(key.n, 0)
+    assert bool(ctx.pair_paths & 4) == pair
+    return ctx
+
+
+def test_pe_given_r_matches_reference_goldens(golden, key2048, monkeypatch):
+    N = _native()
+    ctx = _pub(monkeypatch, key2048, True)
+    recs = golden["encrypt"]["2048"]
+    x = np.array([r["bits"] for r in recs], dtype=np.uint32).view(np.float32)
+    rs = [int(r["r"], 16) for r in recs]
+    ct, ex, st = ctx.encrypt(x, obf_mode=N.PAI_OBF_GIVEN, r=rs)
+    got = N.words_to_ints(ct)
+    for i, rec in enumerate(recs):
+        assert st[i] == 0
+        assert (hex(got[i]), int(ex[i])) == (rec["c"], rec["e"]), f"element {i}"
+
+
+@pytest.mark.parametrize("n", [1, 127, 129, 300])
+def test_pe_matches_k_encrypt_and_oracle(key2048, monkeypatch, n):
+    N = _native()
+    a = _pub(monkeypatch, key2048, True)
+    b = _pub(monkeypatch, key2048, False)
+    rng = np.random.default_rng(n)
+    x = (rng.standard_normal(n) * 10.0 ** rng.integers(-30, 30, n)).astype(np.float32)
+    x[::7] = 0.0
+    x[1::9] = -x[1::9]
+    kw = dict(obf_mode=N.PAI_OBF_RNG, rng_key=bytes(range(32)), index_base=77)
+    ca, ea, sa = a.encrypt(x, **kw)
+    cb, eb, sb = b.encrypt(x, **kw)
+    assert np.array_equal(ca, cb) and np.array_equal(ea, eb) and np.array_equal(sa, sb)
+    got = N.words_to_ints(ca[: min(n, 6)])
+    rb = ((2048 + 64 + 31) // 32) * 4       # bytes of the ChaCha20 stream k_encrypt and k_pe_pre draw
+    for i in range(min(n, 6)):
+        c, e = O.encrypt_value(x[i], key2048, O.device_r(bytes(range(32)), 77 + i, rb))
+        assert (got[i], int(ea[i])) == (c, e), f"element {i}"
+
+
+def test_pe_edge_obfuscators(key2048, monkeypatch):
+    """r = 0, 1, n - 1, n, n + 1, a multiple of p, r >= n^2 (explicit, like random_value)."""
+    N = _native()
+    a = _pub(monkeypatch, key2048, True)
+    b = _pub(monkeypatch, key2048, False)
+    k = key2048
+    rs = [0, 1, 2, k.n - 1, k.n, k.n + 1, 5 * k.p, k.nsquare - 1, (1 << (32 * a.ct_words)) - 1]
+    x = np.array([0.0, 1.0, -1.0, 3.5, -2.25, 1e-30, -1e30, 7.0, -0.0], dtype=np.float32)
+    ca, ea, _ = a.encrypt(x, obf_mode=N.PAI_OBF_GIVEN, r=rs)
+    cb, eb, _ = b.encrypt(x, obf_mode=N.PAI_OBF_GIVEN, r=rs)
+    assert np.array_equal(ca, cb) and np.array_equal(ea, eb)
+    got = N.words_to_ints(ca)
+    for i, r in enumerate(rs):
+        assert got[i] == O.encrypt_value(x[i], k, r)[0], f"r #{i}"

@@ -180,11 +180,11 @@ def main():
     ap.add_argument("--path", choices=("crt", "public"), default="crt")
     ap.add_argument("--obf", choices=("fixedbase", "generic"), default="fixedbase",
                     help="device-RNG sampler of r^n on the CRT path (kernels_fb.hpp vs r from ChaCha20)")
-    ap.add_argument("--fb-window", type=int, default=22, choices=(8, 12, 16, 20, 21, 22, 23, 24),
+    ap.add_argument("--fb-window", type=int, default=23, choices=(8, 12, 16, 20, 21, 22, 23, 24),
                     help="largest digit window of the fixed-base tables; the library takes the largest one <= this "
-                         "whose tables fit the free HBM (nb = 2048: W = 22, 47 products per half, 2 x 50.5 GB; "
-                         "nb = 4096: W = 20, 103 products per half, 2 x 63.9 GB). W = 23 (2 x 96.6 GB) measured "
-                         "only 0.8 %% faster than 22 at nb = 2048 (TLB reach), so 22 is the default")
+                         "whose tables fit the free HBM (nb = 2048: W = 23, 45 pair products per half, 2 x 96.6 GB; "
+                         "nb = 4096: W = 21, 98 products per half, 2 x 121.7 GB). With the pair sampler W = 23 "
+                         "measured 1.8 %% faster than 22 (profiles/r02_window_sweep_pair.txt)")
     ap.add_argument("--cpu-sample", type=int, default=16384)
     ap.add_argument("--cpu-threads", type=int, default=os.cpu_count() or 1,
                     help="threads of the GMP CPU baseline (default os.cpu_count(), like the reference's Pool)")

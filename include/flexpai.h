@@ -118,7 +118,8 @@ void pai_ctx_destroy(pai_ctx* ctx);
 int pai_ctx_set_option(pai_ctx* ctx, int option, int value);
 int pai_ctx_get_option(const pai_ctx* ctx, int option, int* value);
 /* With PAI_OPT_STAGE_TIMING on: kernel durations (ms) of the last encrypt call's final chunk, in launch
- * order (CRT: stage A, stage B, finish; public key: the one encrypt kernel). Waits for them. */
+ * order (CRT: stage A, stage B, finish; public key on pairs: k_pe_pre, k_pe_pow, k_pe_fin; other public-key
+ * paths: the one encrypt kernel). Waits for them. */
 int pai_ctx_stage_times(pai_ctx* ctx, float* ms_out, int max_out, int* count);
 /* key bits, 32-bit words per ciphertext (2*key_bits/32), words per plaintext (key_bits/32) */
 int pai_ctx_info(const pai_ctx* ctx, int* key_bits, int* ct_words, int* pt_words);

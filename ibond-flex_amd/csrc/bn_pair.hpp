@@ -28,10 +28,13 @@ namespace pair {
 using lane::LB;
 using lane::LMASK;
 
-template <int S>
+// pins every accumulator but position Z, which was just cleared: the compiler then sees the zero and starts
+// that position's next sum with a product instead of moving 0 into it first
+template <int S, int Z>
 __device__ __forceinline__ void pin2(uint64_t (&P1)[S], uint64_t (&P2)[S]) {
 #pragma unroll
-  for (int i = 0; i < S; ++i) asm volatile("" : "+v"(P1[i]), "+v"(P2[i]));
+  for (int i = 0; i < S; ++i)
+    if (i != Z) asm volatile("" : "+v"(P1[i]), "+v"(P2[i]));
 }
 
 // reductions of digit J: P1 by q1 (its own digit), P2 by q2 after subtracting q1 at position J
@@ -49,7 +52,7 @@ __device__ __forceinline__ void red2(uint64_t (&P1)[S], uint64_t (&P2)[S], const
   P2[(J + 1) % S] += (uint64_t)((int64_t)P2[J] >> LB);
   P1[J] = 0;
   P2[J] = 0;
-  pin2<S>(P1, P2);
+  pin2<S, J>(P1, P2);
   __builtin_amdgcn_sched_barrier(0);
 }
 

@@ -103,9 +103,10 @@ def _Mp(s: int) -> int:
 
 def work_fbp(nb: int, digits: int) -> dict:
     """Per-element MACs of the pair fixed-base path (kernels_fbp.hpp): k_fbp = K pair products per half
-    (s = nb/64 limbs of p_h) + the c0 chunk sum and w = A + p B (s^2); Garner as work_fb."""
+    (s = nb/64 limbs of p_h) + the c0 chunk sum (s^2); k_fbp_fin = Garner on pairs: q B_q (4 s^2, B row zero),
+    h (5 s^2), c = A_q + q B_q + q^2 H_A + p q^2 H_B (6 s^2)."""
     s = nb // 64
-    return {"k_fb_digits": 0.0, "k_fbp": float(2 * (digits * _Mp(s) + s * s)), "k_fb_fin": float(_M(2 * s) + 4 * s * s)}
+    return {"k_fb_digits": 0.0, "k_fbp": float(2 * (digits * _Mp(s) + s * s)), "k_fbp_fin": float(15 * s * s)}
 
 
 def work_fbg(nb: int, digits: int) -> dict:
@@ -610,7 +611,7 @@ def main():
         elif grp_fb:
             names, works = ["k_fb_digits", "k_fbg", "k_fbg_fin"], work_fbg(nb, fb_info[2])
         elif use_crt and use_fb and fb_pair:
-            names, works = ["k_fb_digits", "k_fbp", "k_fb_fin"], work_fbp(nb, fb_info[2])
+            names, works = ["k_fb_digits", "k_fbp", "k_fbp_fin"], work_fbp(nb, fb_info[2])
         elif use_crt and use_fb:
             names, works = ["k_fb_digits", "k_fb", "k_fb_fin"], work_fb(nb, fb_info[2])
         elif use_crt:

@@ -19,6 +19,22 @@ hipError_t fbp_launch(int s, const FbpParams& p, int gx, hipStream_t st) {
   return hipGetLastError();
 }
 
+int fbp_fin_occupancy(int s, int* occ) {
+  hipError_t e;
+  if (s == 19) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, k_fbp_fin<19>, LANE_BLOCK, 0);
+  else if (s == 37) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, k_fbp_fin<37>, LANE_BLOCK, 0);
+  else return -1;
+  if (e != hipSuccess || *occ < 1) *occ = 1;
+  return 0;
+}
+
+hipError_t fbp_launch_fin(int s, const FbpFinParams& p, int gx, hipStream_t st) {
+  if (s == 19) hipLaunchKernelGGL(k_fbp_fin<19>, dim3(gx), dim3(LANE_BLOCK), 0, st, p);
+  else if (s == 37) hipLaunchKernelGGL(k_fbp_fin<37>, dim3(gx), dim3(LANE_BLOCK), 0, st, p);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 hipError_t fbp_build_tables(int s, const FbpHalf* d_halves, uint4* t0, uint4* t1, int K, int W, hipStream_t st) {
   const int per = ((1 << W) + LANE_BLOCK - 1) / LANE_BLOCK;
   if (s == 19) {

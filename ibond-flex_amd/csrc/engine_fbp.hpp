@@ -7,6 +7,9 @@ namespace fpai {
 // blocks per CU of k_fbp<s>; -1 if s is unsupported (19: 1024-bit keys, 37: 2048-bit keys)
 int fbp_occupancy(int s, int* occ);
 hipError_t fbp_launch(int s, const FbpParams& p, int gx, hipStream_t st);
+// blocks per CU of k_fbp_fin<s>, and its launch
+int fbp_fin_occupancy(int s, int* occ);
+hipError_t fbp_launch_fin(int s, const FbpFinParams& p, int gx, hipStream_t st);
 // builds both halves' pair tables (K digit positions of W bits) on `st`
 hipError_t fbp_build_tables(int s, const FbpHalf* d_halves, uint4* t0, uint4* t1, int K, int W, hipStream_t st);
 

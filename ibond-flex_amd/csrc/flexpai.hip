@@ -104,6 +104,8 @@ struct pai_ctx {
   int fb_raw_bits = 0;
   FbHalf* d_fb_halves = nullptr;
   FbpHalf* d_fbp_halves = nullptr;  // pair tables (kernels_fbp.hpp): the default for 1024/2048-bit keys
+  uint32_t *d_fbp_fin_cs = nullptr, *d_fbp_fin_p = nullptr;   // k_fbp_fin: its 12 S constant words, p
+  uint32_t fbp_fin_mprime = 0;
   int fb_pair_s = 0;            // limbs of p_h of the resident pair tables; 0 = k_fb tables
   FbgpHalf* d_fbgp_halves = nullptr;  // 4096-bit keys: pair-group tables (kernels_grp_pair.hpp)
   bool fb_gpair = false;
@@ -571,6 +573,7 @@ static void fb_release(pai_ctx* c) {
   c->fb_mem.clear();
   c->d_fb_halves = nullptr;
   c->d_fbp_halves = nullptr;
+  c->d_fbp_fin_cs = c->d_fbp_fin_p = nullptr;
   c->fb_pair_s = 0;
   c->d_fbgp_halves = nullptr;
   c->fb_gpair = false;
@@ -620,6 +623,9 @@ static int ensure_fb(pai_ctx* c) {
   const int K = fb_digit_count(c, W);
   const size_t RB = (size_t)LB * sb;
   const HBig primes[2] = {c->fb_p, c->fb_q};
+  // both Garner kernels take w_q < q^2 as an operand mod p^2 (k_fb_fin: w_p + 8 p^2 - w_q > 0; k_fbp_fin:
+  // A_q, B_q < 2p): keys with q >= 2p encrypt on the generic CRT path
+  if (cmp(primes[1], shl1(primes[0])) >= 0) return fb_unavailable(c, "q >= 2p: fixed-base Garner bounds");
   // pair products (kernels_fbp.hpp) over the S limbs of p_h: needs p_h < 2^(32 PW) and R = 2^(28 S) >=
   // 2^12 p_h (bounds of the first product, kernels_fbp.hpp); $FLEXPAI_FB_PAIR=0 selects k_fb
   const int ps = sb == 37 ? 19 : sb == 74 ? 37 : 0;
@@ -777,6 +783,29 @@ static int ensure_fb(pai_ctx* c) {
   if (pair_ok) {
     std::vector<FbpHalf> pvv(pv, pv + 2);
     if ((rc = upload_fb(c, pvv, &c->d_fbp_halves))) return fb_unavailable(c, pai_last_error());
+    // k_fbp_fin (kernels_fbp.hpp): (q R)^, (q^-2 R)^ as pairs over p, then q, q^2, p q^2, 4p, 3p
+    const HBig &P = primes[0], &Q = primes[1];
+    const size_t RS = (size_t)LB * ps;
+    std::vector<uint32_t> cs;
+    auto put = [&](const HBig& v, int limbs) {
+      const std::vector<uint32_t> l = v.limbs(limbs, LB);
+      cs.insert(cs.end(), l.begin(), l.end());
+    };
+    auto put_pair = [&](const HBig& v) {   // v mod p^2 -> (v mod p, v div p)
+      const HBig qt = div_big(v, P);
+      put(sub(v, mul(qt, P)), ps);
+      put(qt, ps);
+    };
+    put_pair(mul_pow2_mod(mod(Q, sq[0]), RS, sq[0]));
+    put_pair(mul_pow2_mod(coef, RS, sq[0]));
+    put(Q, ps);
+    put(sq[1], 2 * ps);
+    put(mul(P, sq[1]), 3 * ps);
+    put(mul(P, HBig(4)), ps);
+    put(mul(P, HBig(3)), ps);
+    if ((rc = upload_fb(c, cs, &c->d_fbp_fin_cs))) return fb_unavailable(c, pai_last_error());
+    c->d_fbp_fin_p = const_cast<uint32_t*>(pv[0].p);
+    c->fbp_fin_mprime = pv[0].mprime;
   }
   if (gpair_ok) {
     std::vector<FbgpHalf> gvv(gv, gv + 2);
@@ -1253,7 +1282,7 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
   const long long lane_blocks = (chunk + EPB - 1) / EPB;
   const int gxF = (int)std::max<long long>(1, std::min<long long>(lane_blocks, (long long)occF * c->cus / 2));
   const int gxG = (int)std::max<long long>(1, std::min<long long>(lane_blocks, (long long)occG * c->cus));
-  const size_t dbytes = (size_t)2 * c->fb_K * 4, wbytes = (size_t)2 * SB * 4;   // per element
+  const size_t dbytes = (size_t)2 * c->fb_K * 4, wbytes = (size_t)2 * std::max(SB, 2 * c->fb_pair_s) * 4;   // per element
   int rc;
   if ((rc = ensure_work(c, (dbytes + wbytes) * chunk))) return rc;
   uint32_t* digits = (uint32_t*)c->d_work;
@@ -1312,6 +1341,16 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
       HIPCHK(grp_launch_garner(gh, (int)std::max<long long>(1, std::min<long long>(gb4, (long long)occH * c->cus)), st));
       FbgFinParams gf{w, SB, n, c->d_N, c->d_fb_q2Rn, c->mprime_N, e.ct + (size_t)off * c->ct_words, c->ct_words};
       HIPCHK(grp_launch_fin(gf, (int)std::max<long long>(1, std::min<long long>(gb8, (long long)occC * c->cus)), st));
+      stage_mark(c, 3, st);
+      continue;
+    }
+    if (c->fb_pair_s) {   // Garner on pairs (kernels_fbp.hpp)
+      int occP = 1;
+      fbp_fin_occupancy(c->fb_pair_s, &occP);
+      const FbpFinParams pp{w, n, c->d_fbp_fin_p, c->d_fbp_fin_cs, c->fbp_fin_mprime, e.ct + (size_t)off * c->ct_words,
+                            c->ct_words};
+      const long long nb = (n + LANE_BLOCK - 1) / LANE_BLOCK;
+      HIPCHK(fbp_launch_fin(c->fb_pair_s, pp, (int)std::max<long long>(1, std::min<long long>(nb, (long long)occP * c->cus)), st));
       stage_mark(c, 3, st);
       continue;
     }
@@ -2391,16 +2430,18 @@ int pai_decrypt(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, do
 }
 
 // ------------------------------------------------------------------ debugging hook (tests / tools only)
-// Copies the per-half k_fb outputs (c0 G_h^a_h mod h^2, limbs [2][SB][n]) of the last fixed-base chunk.
+// Copies the per-half sampler outputs (c0 G_h^a_h mod h^2) of the last fixed-base chunk: limbs [2][SB][n]
+// (k_fb, k_fbg), or canonical pairs [2][2S][n] with *sb = 2S when the pair tables are resident (k_fbp).
 extern "C" int pai_debug_fb_w(pai_ctx* c, uint32_t* out, size_t max_words, long long* n, int* sb) {
   if (!c || !c->fb_last_w) return fail(PAI_ERR_ARG, "no fixed-base output");
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipDeviceSynchronize());
-  const size_t words = (size_t)2 * c->crt_sb * c->fb_last_n;
+  const int rows = c->fb_pair_s ? 2 * c->fb_pair_s : c->crt_sb;
+  const size_t words = (size_t)2 * rows * c->fb_last_n;
   if (words > max_words) return fail(PAI_ERR_ARG, "buffer too small");
   HIPCHK(hipMemcpy(out, c->fb_last_w, words * 4, hipMemcpyDeviceToHost));
   *n = c->fb_last_n;
-  *sb = c->crt_sb;
+  *sb = rows;
   return 0;
 }
 

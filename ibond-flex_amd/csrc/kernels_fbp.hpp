@@ -7,8 +7,8 @@
 // 1 + n M = 1 + p_h (n / p_h) M, i.e. the pair (1, (n / p_h) M mod p_h), with the second component an
 // unreduced sum of 8-bit chunks of |M| (< 2^PB p_h; the first product keeps B < 2 p_h while R >= 2^(PB+1) p_h).
 // Every product multiplies a plain pair by a Montgomery-form row, so the result stays plain: after the
-// K products the pair is c0 G_h^(a_h) mod p_h^2, written as w = A + p_h B (< 2 p_h^2, SB limbs) for
-// k_fb_fin's Garner recombination (unchanged).
+// K products the pair is c0 G_h^(a_h) mod p_h^2, written as its canonical pair for k_fbp_fin's Garner
+// recombination (below).
 #pragma once
 #include "bn_pair.hpp"
 #include "kernels_fb.hpp"
@@ -43,7 +43,7 @@ struct FbpParams {
   long long n;
   int K, W;
   const uint32_t* digits;  // [2][K][n]
-  uint32_t* out;           // w [2][SB][n]
+  uint32_t* out;           // canonical pairs [2][2S][n] (A limbs, then B) for k_fbp_fin
   const void* x;
   int dtype, exp_mode, fexp;
   int32_t* exp;
@@ -193,8 +193,136 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp(FbpParams p) {
     }
     if (i < p.n) {
       pair::canon<S>(A, B, m);
-      fbp_store_w<S, SB>(A, B, m, p.out + (size_t)half * SB * p.n + i, p.n, std::make_integer_sequence<int, SB>{});
+      uint32_t* o = p.out + (size_t)half * 2 * S * p.n + i;
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        o[(size_t)j * p.n] = A[j];
+        o[(size_t)(S + j) * p.n] = B[j];
+      }
     }
+  }
+}
+
+// ---------------------------------------------------------------- Garner on pairs -> ciphertext words
+// c = w_q + q^2 h, h = (w_p - w_q) q^-2 mod p^2 (k_fb_fin's recombination) from the canonical pairs
+// (A_p, B_p), (A_q, B_q) that k_fbp leaves (w_h = A_h + h B_h), with every product mod p^2 a pair product
+// over the S limbs of p (bn_pair.hpp) and so in half the registers of k_fb_fin's 2S-limb products:
+//   X = (B_q, 0) (q R)^ R^-1            = q B_q mod p^2                          4 S^2 MACs (B row zero)
+//   D = (A_p + 4p - A_q - X_A,  B_p + 3p - X_B - 4)    == w_p - w_q, A < 5p, B < 4p (needs q < 2p)
+//   H = D (q^-2 R)^ R^-1, canonical     = h = H_A + p H_B < p^2                  5 S^2
+//   c = A_q + q B_q + q^2 H_A + p q^2 H_B (product scanning, words out)          6 S^2
+// (u^ = the pair of u mod p^2.) Bounds: an operand below 5p (4p) keeps REDC's outputs below 2p while
+// R > 10 p^2 / p; every column of the last sum takes at most 3S products < 2^56.
+struct FbpFinParams {
+  const uint32_t* pr;      // [2][2S][n] canonical pairs from k_fbp (half 0: p, half 1: q)
+  long long n;
+  const uint32_t* p;       // S limbs of p
+  const uint32_t* cs;      // 12 S words: (qR)^ [2S], (q^-2 R)^ [2S], q [S], q^2 [2S], p q^2 [3S], 4p [S], 3p [S]
+  uint32_t mprime;         // -p^-1 mod 2^28
+  uint32_t* ct;
+  int ct_words;
+};
+
+template <int S>
+struct FbpFinDigits {   // multiplier digit pairs of a pair constant in LDS (A limbs, then B)
+  const uint32_t* d;
+  template <int J>
+  __device__ __forceinline__ uint2 operator()(std::integral_constant<int, J>) const { return make_uint2(d[J], d[S + J]); }
+};
+
+// limb K of A_q + q B_q + q^2 H_A + p q^2 H_B (constants q, q^2, p q^2 at cq, cq + S, cq + 3S in LDS)
+template <int S, int K>
+__device__ __forceinline__ uint64_t fbpf_col(const uint32_t (&a1)[S], const uint32_t (&b1)[S], const uint32_t (&ha)[S],
+                                             const uint32_t (&hb)[S], const uint32_t* __restrict__ cq) {
+  uint64_t s = K < S ? (uint64_t)a1[K] : 0ull;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    if (K - i >= 0 && K - i < S) s += (uint64_t)b1[i] * cq[K - i];
+    if (K - i >= 0 && K - i < 2 * S) s += (uint64_t)ha[i] * cq[S + K - i];
+    if (K - i >= 0 && K - i < 3 * S) s += (uint64_t)hb[i] * cq[3 * S + K - i];
+  }
+  return s;
+}
+template <int S, int CW, int K>
+__device__ __forceinline__ void fbpf_out_step(uint64_t& acc, uint64_t& buf, uint32_t (&o4)[4], const uint32_t (&a1)[S],
+                                              const uint32_t (&b1)[S], const uint32_t (&ha)[S], const uint32_t (&hb)[S],
+                                              const uint32_t* __restrict__ cq, uint4* dst, bool valid) {
+  acc += fbpf_col<S, K>(a1, b1, ha, hb, cq);
+  const uint32_t limb = (uint32_t)acc & lane::LMASK;
+  acc >>= lane::LB;
+  constexpr int NB = (28 * K) % 32;           // bits held in buf before this limb
+  buf |= (uint64_t)limb << NB;
+  if constexpr (NB + 28 >= 32) {
+    constexpr int w = (28 * K) / 32;          // word completed by this limb
+    o4[w % 4] = (uint32_t)buf;
+    buf >>= 32;
+    if constexpr (w % 4 == 3 && w < CW) {
+      if (valid) dst[w / 4] = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+    }
+  }
+}
+template <int S, int CW, int... Ks>
+__device__ __forceinline__ void fbpf_out_all(const uint32_t (&a1)[S], const uint32_t (&b1)[S], const uint32_t (&ha)[S],
+                                             const uint32_t (&hb)[S], const uint32_t* __restrict__ cq, uint4* dst, bool valid,
+                                             std::integer_sequence<int, Ks...>) {
+  uint64_t acc = 0, buf = 0;
+  uint32_t o4[4] = {0u, 0u, 0u, 0u};
+  (fbpf_out_step<S, CW, Ks>(acc, buf, o4, a1, b1, ha, hb, cq, dst, valid), ...);
+}
+
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
+  constexpr int CW = 2 * FbGeom<FbpGeom<S>::SB>::TW;   // ciphertext words
+  constexpr int NL = (32 * CW + 27) / 28;             // limbs that cover them
+  static_assert(NL <= 4 * S, "c < n^2 fits 4 S limbs");
+  __shared__ uint32_t cs[12 * S];
+  for (int j = threadIdx.x; j < 12 * S; j += blockDim.x) cs[j] = p.cs[j];
+  __syncthreads();
+  uint32_t m[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) m[j] = p.p[j];
+  const uint32_t mprime = p.mprime;
+  const uint32_t* p4 = cs + 10 * S;
+  const uint32_t* p3 = cs + 11 * S;
+  for (long long base = (long long)blockIdx.x * LANE_BLOCK; base < p.n; base += (long long)gridDim.x * LANE_BLOCK) {
+    const long long i = base + threadIdx.x;
+    const bool valid = i < p.n;
+    const long long ii = valid ? i : p.n - 1;
+    const uint32_t* pr = p.pr + ii;
+    // X = q B_q mod p^2
+    uint32_t xa[S], xb[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      xa[j] = pr[(size_t)(3 * S + j) * p.n];
+      xb[j] = 0u;
+    }
+    pair::mont_mul<S>(xa, xb, FbpFinDigits<S>{cs}, m, mprime);
+    // D = w_p - w_q as a pair with non-negative parts
+    {
+      int64_t ca = 0, cb = 0;
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        const int64_t va = (int64_t)pr[(size_t)j * p.n] + (int64_t)p4[j] - (int64_t)pr[(size_t)(2 * S + j) * p.n] -
+                           (int64_t)xa[j] + ca;
+        const int64_t vb = (int64_t)pr[(size_t)(S + j) * p.n] + (int64_t)p3[j] - (int64_t)xb[j] - (j == 0 ? 4 : 0) + cb;
+        xa[j] = (uint32_t)va & lane::LMASK;
+        xb[j] = (uint32_t)vb & lane::LMASK;
+        ca = va >> lane::LB;
+        cb = vb >> lane::LB;
+      }
+    }
+    // h = D q^-2 mod p^2, canonical
+    pair::mont_mul<S>(xa, xb, FbpFinDigits<S>{cs + 2 * S}, m, mprime);
+    pair::canon<S>(xa, xb, m);
+    // c = w_q + q^2 h
+    uint32_t a1[S], b1[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      a1[j] = pr[(size_t)(2 * S + j) * p.n];
+      b1[j] = pr[(size_t)(3 * S + j) * p.n];
+    }
+    fbpf_out_all<S, CW>(a1, b1, xa, xb, cs + 4 * S, reinterpret_cast<uint4*>(p.ct + ii * p.ct_words), valid,
+                        std::make_integer_sequence<int, NL>{});
   }
 }
 

@@ -59,3 +59,49 @@ def test_pair_kernels_match_the_kernels_they_replace(golden, monkeypatch, nb):
     for u, v in zip(da, db):
         assert np.array_equal(np.asarray(u).view(np.uint8), np.asarray(v).view(np.uint8))
     assert np.array_equal(da[0], x.astype(np.float64))
+
+
+def _prime(bits, rng):
+    """A random prime of exactly `bits` bits (Miller-Rabin, 24 random bases)."""
+    def probable(n):
+        d, s = n - 1, 0
+        while d % 2 == 0:
+            d, s = d // 2, s + 1
+        for _ in range(24):
+            x = pow(int(rng.integers(2, 1 << 62)) % (n - 3) + 2, d, n)
+            if x in (1, n - 1):
+                continue
+            for _ in range(s - 1):
+                x = x * x % n
+                if x == n - 1:
+                    break
+            else:
+                return False
+        return True
+    while True:
+        c = int.from_bytes(rng.bytes((bits + 7) // 8), "little") % (1 << bits) | (1 << (bits - 1)) | 1
+        if all(c % sp for sp in (3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37)) and probable(c):
+            return c
+
+
+def test_unbalanced_key_takes_the_generic_path():
+    """Both fixed-base Garner kernels take w_q < q^2 as an operand mod p^2 (k_fbp_fin: A_q, B_q < 2p;
+    k_fb_fin: w_p + 8 p^2 - w_q > 0), so a key with q > 2p (p of 1020 bits, q of 1024) gets no tables and
+    encrypts on the generic CRT path with the ChaCha20 r, bit-exact against the oracle, and decrypts."""
+    N = _native()
+    rng = np.random.default_rng(2044)
+    p, q = _prime(1020, rng), _prime(1024, rng)
+    assert q > 2 * p
+    key = O.Key(p * q, p, q)
+    ctx = N.Context(key.n, 0, key.p, key.q)
+    x = (rng.standard_normal(200) * 50).astype(np.float32)
+    rk = bytes(range(100, 132))
+    ct, ex, _ = ctx.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=9)
+    assert not ctx.fixed_base and not ctx.fb_ready
+    got = N.words_to_ints(ct)
+    rbytes = ((key.n.bit_length() + 64 + 31) // 32) * 4
+    for i in (0, 77, 199):
+        r = O.device_r(rk, 9 + i, rbytes) % key.n
+        c, e = O.encrypt_value(x[i], key, r)
+        assert got[i] == c and int(ex[i]) == e, f"element {i}"
+    assert np.array_equal(ctx.decrypt(ct, ex)[0], x.astype(np.float64))

@@ -224,10 +224,18 @@ struct FbpFinParams {
 };
 
 template <int S>
-struct FbpFinDigits {   // multiplier digit pairs of a pair constant in LDS (A limbs, then B)
-  const uint32_t* d;
+struct FbpFinDigits {   // multiplier digit pairs of a pair constant in LDS (A limbs, then B), read one digit ahead
+  const uint32_t* d;    // (the read for digit J+1 is issued in digit J's region, past its sched_barrier)
+  uint32_t na = 0, nb = 0;
   template <int J>
-  __device__ __forceinline__ uint2 operator()(std::integral_constant<int, J>) const { return make_uint2(d[J], d[S + J]); }
+  __device__ __forceinline__ uint2 operator()(std::integral_constant<int, J>) {
+    const uint2 r = J == 0 ? make_uint2(d[0], d[S]) : make_uint2(na, nb);
+    if constexpr (J + 1 < S) {
+      na = d[J + 1];
+      nb = d[S + J + 1];
+    }
+    return r;
+  }
 };
 
 // limb K of A_q + q B_q + q^2 H_A + p q^2 H_B (constants q, q^2, p q^2 at cq, cq + S, cq + 3S in LDS)

@@ -193,11 +193,14 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp(FbpParams p) {
     }
     if (i < p.n) {
       pair::canon<S>(A, B, m);
+      // (opaque base and stride: their 2S addresses must not be hoisted into registers live across the k loop)
       uint32_t* o = p.out + (size_t)half * 2 * S * p.n + i;
+      long long nn = p.n;
+      asm volatile("" : "+v"(o), "+s"(nn));
 #pragma unroll
-      for (int j = 0; j < S; ++j) {
-        o[(size_t)j * p.n] = A[j];
-        o[(size_t)(S + j) * p.n] = B[j];
+      for (int j = 0; j < 2 * S; ++j) {
+        *o = j < S ? A[j] : B[j - S];
+        o += nn;
       }
     }
   }

@@ -24,7 +24,7 @@ done
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $O/pmcsq -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-public --no-host --no-add8 > $O/pmcsq.log 2>&1 || { echo "pmc sq failed rc=$?"; tail -20 $O/pmcsq.log; exit 1; }
 cd $R
 python3 tools/pmc_traffic.py $O/pmc_FETCH_SIZE/run_counter_collection.csv $O/pmc_WRITE_SIZE/run_counter_collection.csv --kernel k_fbp --n 1048576 --nb 2048 --window 23 -o $O/pmc_k_fbp_latest.json || exit 1
-for k in k_fb_fin k_fb_digits; do
+for k in k_fbp_fin k_fb_digits; do
   python3 tools/pmc_traffic.py $O/pmc_FETCH_SIZE/run_counter_collection.csv $O/pmc_WRITE_SIZE/run_counter_collection.csv --kernel $k --n 1048576 --nb 2048 -o $O/pmc_${k}_latest.json || exit 1
 done
 python3 tools/pmc_traffic.py $O/pmc2_FETCH_SIZE/run_counter_collection.csv $O/pmc2_WRITE_SIZE/run_counter_collection.csv --kernel k_add --n 1048576 --nb 2048 -o $O/pmc_k_add_latest.json || exit 1

@@ -120,6 +120,9 @@ struct pai_ctx {
   uint32_t* fb_last_w = nullptr;  // debugging: k_fb output of the last chunk ([2][SB][fb_last_n])
   long long fb_last_n = 0;
   uint64_t fb_table_bytes = 0;
+  long long fb_seen = 0;        // device-RNG elements encrypted under this key before the tables exist
+  int fb_call = 0;              // host-buffer call in progress: its one fixed-base decision (+1 / -1), else 0
+  bool stage_keep = false;      // host-buffer calls: stage timing spans all chunks of the call
   std::vector<void*> allocs;
   std::vector<void*> priv_allocs;   // private-key constants: all freed together if set_private fails
   bool in_priv = false;             // upload() targets priv_allocs
@@ -338,6 +341,7 @@ static int ensure_work(pai_ctx* c, size_t bytes) {
 }
 
 static void stage_reset(pai_ctx* c) {
+  if (c->stage_keep) return;   // inside a host-buffer call: its entry point reset once for all chunks
   c->nev = 0;
   c->nchunk_ev = 0;
 }
@@ -559,14 +563,34 @@ static uint64_t fb_bytes(const pai_ctx* c, int W) {
   return 2ull * (uint64_t)fb_digit_count(c, W) * (1ull << W) * (uint64_t)fb_row_words(c->crt_sb) * 4ull;
 }
 
-// Budget for the two tables: $FLEXPAI_FB_MAX_BYTES, else the free device memory less a 4 GiB reserve.
+// Budget for the two tables: $FLEXPAI_FB_MAX_BYTES, else the free device memory less a reserve of
+// max(4 GiB, 1/12 of the device) -- 24 GB on a 288 GB MI355X -- kept for what the context (and others in
+// the process) allocate after the tables: host-pipeline buffers for larger calls, decryption work and
+// scratch, k_add's schedule, a configs[3] shard with its all-gather receive buffers.
 static uint64_t fb_budget(const pai_ctx* c) {
+  (void)c;
   if (const char* e = getenv("FLEXPAI_FB_MAX_BYTES")) return (uint64_t)strtod(e, nullptr);
   size_t fr = 0, tot = 0;
   if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 0;
-  const uint64_t reserve = 4ull << 30;
+  const uint64_t reserve = std::max<uint64_t>(4ull << 30, (uint64_t)tot / 12);
   return fr > reserve ? fr - reserve : 0;
 }
+
+// Fixed-base break-even: the tables cost a one-time build (host bases + k_fb*_lohi/fill over 2 K 2^W rows,
+// ~2.1 ns per 256-B row on one MI355X, profiles/r02_bench_v13.log setup) and save, per element, the
+// difference between the generic path and the sampler (nb = 2048: 1/1.63 M - 1/40 M s = 0.59 us; nb = 4096
+// against the public-key kernel: 1/37 k - 1/4.2 M s = 27 us; nb = 1024: ~0.08 us). A fresh key builds them
+// only once the device-RNG elements of this context (this call included) reach the break-even count --
+// a re-keying caller (HE_SA_FT, he_sa_ft/train.py:39-40) encrypting a few hundred elements per key never
+// pays the build. $FLEXPAI_FB_MIN_ELEMS overrides the count; pai_ctx_fixed_base_prepare builds at once.
+static long long fb_break_even(const pai_ctx* c, int W, int K, int row_bytes) {
+  if (const char* e = getenv("FLEXPAI_FB_MIN_ELEMS")) return atoll(e);
+  const double build_s = 0.05 + 2.0 * K * (double)(1ull << W) * 2.1e-9 * (row_bytes / 256.0);
+  const double save_s = c->nb > 2048 ? 27e-6 : c->nb > 1024 ? 0.59e-6 : 0.08e-6;
+  return (long long)(build_s / save_s) + 1;
+}
+
+static bool fb_wanted(pai_ctx* c, long long n);
 
 static void fb_release(pai_ctx* c) {
   for (void* p : c->fb_mem) (void)hipFree(p);
@@ -1214,6 +1238,33 @@ int pai_ctx_fixed_base_prepare(pai_ctx* c) {
   return 0;
 }
 
+// The window ensure_fb would choose and its break-even element count (0 when the tables are resident or
+// the path is unavailable: nothing left to decide).
+static long long fb_threshold(pai_ctx* c) {
+  if (c->fb_state != pai_ctx::FB_UNTRIED || (!c->crt_ok && !c->fbg_ok)) return 0;
+  const int TW = fb_row_words(c->crt_sb);
+  if (!TW) return 0;
+  if (!c->fb_W) c->fb_W = fb_default_window();
+  const uint64_t budget = fb_budget(c);
+  for (int w : {24, 23, 22, 21, 20, 16, 12, 8})
+    if (w <= c->fb_W && fb_bytes(c, w) <= budget) return fb_break_even(c, w, fb_digit_count(c, w), 4 * TW);
+  return 0;
+}
+
+static bool fb_wanted(pai_ctx* c, long long n) {
+  if (c->fb_state != pai_ctx::FB_UNTRIED) return true;   // resident, or known unavailable (ensure_fb says)
+  if (c->fb_call) return c->fb_call > 0;                 // a host-buffer call decided once for all chunks
+  c->fb_seen += n;
+  return c->fb_seen >= fb_threshold(c);
+}
+
+int pai_ctx_fixed_base_policy(pai_ctx* c, long long* seen, long long* threshold) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (seen) *seen = c->fb_seen;
+  if (threshold) *threshold = fb_threshold(c);
+  return 0;
+}
+
 int pai_ctx_fixed_base_setup(const pai_ctx* c, float* host_ms, float* device_ms, uint64_t* table_bytes) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
   if (c->fb_state != pai_ctx::FB_READY) return fail(PAI_ERR_KEY, "fixed-base tables are not resident");
@@ -1414,7 +1465,7 @@ static int launch_pe(pai_ctx* c, const EncParams& e, hipStream_t st) {
 template <int SA, int SB>
 static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
   static_assert(SB == 2 * SA || SB == 2 * SA - 1, "stage sizes");
-  if (e.obf == PAI_OBF_RNG && c->fb_enabled && ensure_fb(c)) return launch_fb(c, e, st);
+  if (e.obf == PAI_OBF_RNG && c->fb_enabled && fb_wanted(c, e.n) && ensure_fb(c)) return launch_fb(c, e, st);
   const long long N = e.n;
   const int r_words = e.obf == PAI_OBF_GIVEN ? e.r_words : e.rng_words;
   const int kchunks = (32 * r_words + LB * SA - 1) / (LB * SA);
@@ -1532,7 +1583,7 @@ int pai_encrypt_dev(pai_ctx* c, int dtype, const void* d_x, size_t N, int exp_mo
   p.nprog = c->nprog;
   p.ct_words = c->ct_words;
   hipStream_t st = (hipStream_t)stream;
-  if (obf_mode == PAI_OBF_RNG && c->fbg_ok && c->crt_enabled && c->fb_enabled && ensure_fb(c))
+  if (obf_mode == PAI_OBF_RNG && c->fbg_ok && c->crt_enabled && c->fb_enabled && fb_wanted(c, p.n) && ensure_fb(c))
     return launch_fb(c, p, st);
   if (obf_mode != PAI_OBF_NONE && c->crt_ok && c->crt_enabled) {
     if (c->crt_sa == 19) return launch_crt<19, 37>(c, p, st);
@@ -2277,6 +2328,20 @@ static size_t carve_bytes(std::initializer_list<size_t> sizes) {
   return t;
 }
 
+// Scope of one host-buffer call (pai_encrypt / pai_add / pai_decrypt): the stage timing is reset once and
+// then spans every chunk's *_dev call; the fixed-base decision of the call is dropped at exit.
+struct HostCall {
+  pai_ctx* c;
+  explicit HostCall(pai_ctx* ctx) : c(ctx) {
+    stage_reset(c);
+    c->stage_keep = true;
+  }
+  ~HostCall() {
+    c->stage_keep = false;
+    c->fb_call = 0;
+  }
+};
+
 int pai_encrypt(pai_ctx* c, int dtype, const void* x, size_t N, int exp_mode, int32_t fixed_exp, int obf_mode,
                 const uint8_t* r_le, size_t r_stride_bytes, size_t r_bytes, const uint8_t* rng_key32,
                 uint64_t index_base, uint32_t* ct_out, int32_t* exp_out, int32_t* status_out) {
@@ -2307,6 +2372,10 @@ int pai_encrypt(pai_ctx* c, int dtype, const void* x, size_t N, int exp_mode, in
     HIPCHK(hipStreamSynchronize(sc));   // hr is released at the end of this scope
   }
   const size_t r_stride_words = r_stride_bytes ? r_words : 0;
+  // one fixed-base decision and one stage-timing record for the whole call: the ciphertexts of a call do
+  // not depend on how it is chunked
+  HostCall hc(c);
+  if (obf_mode == PAI_OBF_RNG) c->fb_call = fb_wanted(c, (long long)N) ? 1 : -1;
   // every chunk's kernels are queued first; the copy stream then drains chunk i while i+1.. compute
   for (int i = 0; i < nch; ++i) {
     const size_t off = (size_t)i * CH, n = std::min(CH, N - off);
@@ -2363,6 +2432,7 @@ int pai_add(pai_ctx* c, const uint32_t* const* cts, const int32_t* const* exps, 
   uint32_t* dout = cv.take<uint32_t>(N * W);
   int32_t* dexp = cv.take<int32_t>(N);
   hipStream_t sc = c->s_comp, sy = c->s_copy;
+  HostCall hc(c);
   for (int i = 0; i < nch; ++i) {
     const size_t off = (size_t)i * CH, n = std::min(CH, N - off);
     uint32_t* cc = dcts + (size_t)k * off * W;
@@ -2407,6 +2477,7 @@ int pai_decrypt(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, do
   int32_t* dst = cv.take<int32_t>(N);
   uint32_t* draw = cv.take<uint32_t>(N * P);
   hipStream_t sc = c->s_comp, sy = c->s_copy;
+  HostCall hc(c);
   for (int i = 0; i < nch; ++i) {
     const size_t off = (size_t)i * CH, n = std::min(CH, N - off);
     if (i >= 2) HIPCHK(hipEventSynchronize(c->hev[i - 2]));   // the slot's previous upload is done

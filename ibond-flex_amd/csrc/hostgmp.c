@@ -13,7 +13,15 @@
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
+#if PY_VERSION_HEX >= 0x030C0000
+/* 3.12 moved the sign of a PyLong into lv_tag: the digit-level conversions below read ob_digit with the
+ * sign in Py_SIZE (the layout of 3.6 - 3.11). Refuse to build rather than build wrong ints. */
+#error "hostgmp.c reads the PyLong digit layout of CPython <= 3.11"
+#elif PY_VERSION_HEX >= 0x030B0000
+#include <cpython/longintrepr.h>
+#else
 #include <longintrepr.h>
+#endif
 #include <structmember.h>
 #include <pthread.h>
 #include <unistd.h>
@@ -408,7 +416,9 @@ static PyObject* g_make_numbers(PyObject* self, PyObject* const* args, Py_ssize_
     *(PyObject**)((char*)obj + o_ct) = it[i];
     *(PyObject**)((char*)obj + o_ob) = flag;
     /* the slots hold two ints, a bool and the public key: no cycle can pass through the number, so it
-     * stays out of the collector (which otherwise rescans every survivor as the list grows) */
+     * stays out of the collector (which otherwise rescans every survivor as the list grows). Objects built
+     * here are therefore NOT tracked by the cyclic GC: a caller that later stores a container in one of
+     * their slots (nothing in the package or the reference does) would have to re-track it. */
     if (PyObject_IS_GC(obj)) PyObject_GC_UnTrack(obj);
     PyList_SET_ITEM(out, i, obj);
   }
@@ -419,7 +429,68 @@ done:
   return out;
 }
 
+/* packed_valid(cls, objs, ints, exps) -> bool: every objs[i] is a `cls` whose ciphertext slot IS ints[i]
+ * (object identity) and whose exponent equals exps[i] (int64 buffer) -- the check that a PaillierArray's
+ * cached device words still describe its elements (cipher_array.PaillierArray._valid_packed). Elements can
+ * change in place (apply_obfuscation replaces the ciphertext, callers may assign .exponent), so the check
+ * is per element, done here at a few ns per element instead of two Python attribute reads. */
+static PyObject* g_packed_valid(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  (void)self;
+  if (nargs != 4 || !PyType_Check(args[0])) {
+    PyErr_SetString(PyExc_TypeError, "packed_valid(cls, objs, ints, exps)");
+    return NULL;
+  }
+  PyTypeObject* cls = (PyTypeObject*)args[0];
+  const char* cname = cls->tp_name;
+  const char* dot = strrchr(cname, '.');
+  if (dot) cname = dot + 1;
+  char nct[256];
+  snprintf(nct, sizeof nct, "_%s__ciphertext", cname);
+  Py_ssize_t o_ex, o_ct;
+  if ((o_ex = slot_offset(args[0], "exponent")) < 0 || (o_ct = slot_offset(args[0], nct)) < 0) return NULL;
+  PyObject* objs = PySequence_Fast(args[1], "packed_valid: objs must be a sequence");
+  if (!objs) return NULL;
+  PyObject* ints = PySequence_Fast(args[2], "packed_valid: ints must be a sequence");
+  if (!ints) {
+    Py_DECREF(objs);
+    return NULL;
+  }
+  Py_buffer ev;
+  if (PyObject_GetBuffer(args[3], &ev, PyBUF_C_CONTIGUOUS) < 0) {
+    Py_DECREF(objs);
+    Py_DECREF(ints);
+    return NULL;
+  }
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(objs);
+  int ok = n == PySequence_Fast_GET_SIZE(ints) && ev.len == n * 8;
+  PyObject** it = PySequence_Fast_ITEMS(objs);
+  PyObject** iv = PySequence_Fast_ITEMS(ints);
+  const int64_t* e = (const int64_t*)ev.buf;
+  for (Py_ssize_t i = 0; ok && i < n; ++i) {
+    PyObject* o = it[i];
+    if (Py_TYPE(o) != cls) {
+      ok = 0;
+      break;
+    }
+    PyObject* ct = *(PyObject**)((char*)o + o_ct);
+    PyObject* ex = *(PyObject**)((char*)o + o_ex);
+    if (ct != iv[i] || !ex || !PyLong_CheckExact(ex)) {
+      ok = 0;
+      break;
+    }
+    int over = 0;
+    const long long v = PyLong_AsLongLongAndOverflow(ex, &over);
+    if (over || v != e[i]) ok = 0;
+  }
+  PyBuffer_Release(&ev);
+  Py_DECREF(objs);
+  Py_DECREF(ints);
+  if (PyErr_Occurred()) return NULL;
+  return PyBool_FromLong(ok);
+}
+
 static PyMethodDef methods[] = {
+    {"packed_valid", (PyCFunction)(void (*)(void))g_packed_valid, METH_FASTCALL, "cached words still match"},
     {"make_numbers", (PyCFunction)(void (*)(void))g_make_numbers, METH_FASTCALL, "bulk slot construction"},
     {"words_to_ints", (PyCFunction)(void (*)(void))g_words_to_ints, METH_FASTCALL, "rows of LE 32-bit words -> ints"},
     {"ints_to_words", (PyCFunction)(void (*)(void))g_ints_to_words, METH_FASTCALL, "ints -> rows of LE 32-bit words"},

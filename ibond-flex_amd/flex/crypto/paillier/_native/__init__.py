@@ -26,7 +26,7 @@ PAI_OPT_FIXED_BASE, PAI_OPT_FB_WINDOW, PAI_OPT_FB_READY, PAI_OPT_FB_PAIR, PAI_OP
 
 EXPORTED = ("pai_device_count", "pai_device_mem_info", "pai_ctx_create", "pai_ctx_set_private", "pai_ctx_destroy", "pai_ctx_info", "pai_last_error",
             "pai_ctx_set_option", "pai_ctx_get_option", "pai_ctx_stage_times", "pai_ctx_fixed_base_info",
-            "pai_ctx_fixed_base_prepare", "pai_ctx_fixed_base_setup",
+            "pai_ctx_fixed_base_prepare", "pai_ctx_fixed_base_setup", "pai_ctx_fixed_base_policy",
             "pai_encrypt", "pai_add", "pai_decrypt", "pai_encrypt_dev", "pai_add_dev", "pai_decrypt_dev",
             "pai_mul", "pai_mul_dev", "pai_matmul", "pai_matmul_dev", "pai_add_plain", "pai_add_plain_dev",
             "pai_segment_add", "pai_segment_add_dev", "pai_comm_unique_id", "pai_comm_create", "pai_comm_destroy",
@@ -66,6 +66,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.pai_ctx_fixed_base_info.argtypes = [P, P, P, P, P]
         lib.pai_ctx_fixed_base_prepare.argtypes = [P]
         lib.pai_ctx_fixed_base_setup.argtypes = [P, P, P, P]
+        lib.pai_ctx_fixed_base_policy.argtypes = [P, P, P]
         lib.pai_encrypt.argtypes = [P, I, P, S, I, ctypes.c_int32, I, P, S, S, P, U64, P, P, P]
         lib.pai_add.argtypes = [P, P, P, I, S, P, P]
         lib.pai_decrypt.argtypes = [P, P, P, S, P, P, P, P]
@@ -277,6 +278,13 @@ class Context:
         hm, dm, tb = ctypes.c_float(), ctypes.c_float(), ctypes.c_uint64()
         _check(self.lib.pai_ctx_fixed_base_setup(self._h, ctypes.byref(hm), ctypes.byref(dm), ctypes.byref(tb)))
         return float(hm.value), float(dm.value), int(tb.value)
+
+    def fixed_base_policy(self):
+        """(seen, threshold): device-RNG elements encrypted under this key so far, and the count at which
+        the fixed-base tables get built (0 once resident or unavailable); include/flexpai.h."""
+        seen, thr = ctypes.c_longlong(), ctypes.c_longlong()
+        _check(self.lib.pai_ctx_fixed_base_policy(self._h, ctypes.byref(seen), ctypes.byref(thr)))
+        return int(seen.value), int(thr.value)
 
     def close(self):
         if getattr(self, "_h", None):

@@ -12,14 +12,17 @@ the registry is process-local and never pickled. $FLEXPAI_CRT=0 disables CRT enc
 
 Contexts live in a bounded LRU ($FLEXPAI_MAX_CONTEXTS, default 4): a process that cycles through
 keys (a new keypair per round, or several simulated parties) drops the least recently used context,
-whose device memory (constants, fixed-base tables) is released when the last reference goes.
+whose device memory (constants, fixed-base tables) is released when the last reference goes, and the
+registered private key of that public key with it; the private-key registry is bounded by the same
+limit. A PaillierDecryptor always passes its own key, so eviction only costs a later encryption under an
+evicted key the CRT path (it then runs the public-key kernels, same ciphertext distribution).
 """
 from __future__ import annotations
 
 import collections
 import os
 import threading
-from typing import Dict, Optional, Tuple
+from typing import Optional, Tuple
 
 import numpy as np
 
@@ -27,7 +30,7 @@ from . import _native
 
 _lock = threading.Lock()
 _ctxs: "collections.OrderedDict[Tuple[int, int, int], _native.Context]" = collections.OrderedDict()
-_private: Dict[int, object] = {}
+_private: "collections.OrderedDict[int, object]" = collections.OrderedDict()
 _gpus: Optional[Tuple[int, int]] = None     # (pid, device count)
 
 
@@ -53,6 +56,18 @@ def register_private(public_key, private_key) -> None:
     """Remember this process's private key for `public_key` (enables CRT encryption)."""
     with _lock:
         _private[public_key.n] = private_key
+        _private.move_to_end(public_key.n)
+        while len(_private) > max_contexts():    # bounded like the contexts (HE_SA_FT re-keys per exchange)
+            _private.popitem(last=False)
+
+
+def _evict_lru() -> None:
+    """Drop the least recently used contexts beyond max_contexts(), and with each the private key of its
+    public key unless another cached context (another device) still uses it. Caller holds _lock."""
+    while len(_ctxs) > max_contexts():
+        (n_old, _, _), _ = _ctxs.popitem(last=False)        # freed once no caller holds it any more
+        if not any(k[0] == n_old for k in _ctxs):
+            _private.pop(n_old, None)
 
 
 def device_index() -> int:
@@ -75,10 +90,11 @@ def context(public_key, private_key=None) -> "_native.Context":
         if ctx is None:
             ctx = _native.Context(public_key.n, dev)
             _ctxs[k] = ctx
-            while len(_ctxs) > max_contexts():
-                _ctxs.popitem(last=False)        # freed once no caller holds it any more
+            _evict_lru()
         else:
             _ctxs.move_to_end(k)
+        if public_key.n in _private:
+            _private.move_to_end(public_key.n)
         if private_key is not None and not ctx.has_private:
             ctx.set_private(private_key.p, private_key.q)
     return ctx

@@ -17,13 +17,15 @@ indexes, reshapes or pickles the result keep working unchanged. Two additions:
   GPU launch (negative scalars: one batch inversion for the whole array), and ``a.dot(x)`` /
   ``a @ x`` with a plain matrix (he_otp_lr_ft1/train.py:160) as one launch plus a reduction tree.
 
-Pickling (ionic_bond ships pickles, ion.py:150-178) writes the bulk wire format below and unpickles
-into a PaillierArray again, with its packed words cached: an array received from a flexpai peer goes
-straight back to the GPU for the receiver's ``+``, ``sum``, ``.dot`` and ``*`` (HE_SA_FT coordinator
-he_sa_ft/train.py:66-69, HE_OTP_LR he_otp_lr_ft1/train.py:158-160, HE_LINEAR he_linear_ft/train.py:64-65).
-With ``FLEXPAI_PICKLE_PLAIN=1`` it pickles as a plain object ndarray instead, for deployments that mix in
-unmodified FLEX peers (they cannot import this module). Plain object ndarrays received from such peers
-run the reference's per-element operators on the package's GMP binding (_bigint.py).
+Pickling (ionic_bond ships pickles, ion.py:150-178) writes, by default, exactly what the reference
+writes: a plain object ndarray of PaillierEncryptedNumber (same class path and slot state), which an
+unmodified FLEX peer's ``pickle.load`` (ion.py:201) reads. Deployments where every party runs this
+package opt in to the bulk wire format below with ``FLEXPAI_PICKLE_BULK=1`` on the senders: the pickle
+then unpickles into a PaillierArray with its packed words cached, so an array received from a flexpai
+peer goes straight back to the GPU for the receiver's ``+``, ``sum``, ``.dot`` and ``*`` (HE_SA_FT
+coordinator he_sa_ft/train.py:66-69, HE_OTP_LR he_otp_lr_ft1/train.py:158-160, HE_LINEAR
+he_linear_ft/train.py:64-65). Plain object ndarrays (the default, and what unmodified peers send) run
+the reference's per-element operators on the package's GMP binding (_bigint.py).
 
 On a host without a GPU (e.g. a CPU-only protocol coordinator) the operators on existing ciphertext
 arrays fall back to numpy's per-element loop over PaillierEncryptedNumber, i.e. exactly the reference's
@@ -43,10 +45,10 @@ from .encrypted_number import PaillierEncryptedNumber
 
 _CT = "_PaillierEncryptedNumber__ciphertext"
 
-try:                                        # bulk slot construction (csrc/hostgmp.c), when built
-    from ._gmp import make_numbers as _make_numbers
+try:                                        # bulk slot construction and checks (csrc/hostgmp.c), when built
+    from ._gmp import make_numbers as _make_numbers, packed_valid as _packed_valid
 except ImportError:                         # pragma: no cover - build() always builds it
-    _make_numbers = None
+    _make_numbers = _packed_valid = None
 
 
 class _Packed:
@@ -54,6 +56,12 @@ class _Packed:
 
     def __init__(self, n: int, words: np.ndarray, exps: np.ndarray, ints: list):
         self.n, self.words, self.exps, self.ints = n, words, exps, ints
+
+
+def bulk_pickle_enabled() -> bool:
+    """FLEXPAI_PICKLE_BULK=1: pickle PaillierArray through the bulk wire format (all peers run flexpai).
+    Default: the reference's plain object-ndarray pickle."""
+    return os.environ.get("FLEXPAI_PICKLE_BULK", "0").strip() not in ("", "0")
 
 
 class PaillierArray(np.ndarray):
@@ -67,7 +75,7 @@ class PaillierArray(np.ndarray):
 
     def __reduce__(self):
         plain = np.asarray(self).view(np.ndarray).__reduce__
-        if os.environ.get("FLEXPAI_PICKLE_PLAIN", "0").strip() not in ("", "0"):
+        if not bulk_pickle_enabled():
             return plain()
         try:
             return (_from_pickle, (to_wire(self),))
@@ -86,6 +94,8 @@ class PaillierArray(np.ndarray):
         flat = np.asarray(self).reshape(-1)
         if flat.size != pk.exps.size:
             return None
+        if _packed_valid is not None:            # the same identity check in C (csrc/hostgmp.c), ~ns/element
+            return pk if _packed_valid(PaillierEncryptedNumber, flat, pk.ints, pk.exps) else None
         try:
             cur = [getattr(e, _CT) for e in flat]
             exps = [e.exponent for e in flat]
@@ -430,8 +440,8 @@ def add_plain(a, y):
 #   magic "FPAW1\0" | u32 ndim | i64 shape[ndim] | u32 n_bytes | n (little-endian) | u32 W |
 #   i32 exponents[N] | u8 obfuscated[N] | u32 words[N][W]
 # i.e. 4 W + 5 bytes per element plus a header; ciphertext i = int.from_bytes(words[i], "little").
-# PaillierArray pickles through this format (see the module docstring; FLEXPAI_PICKLE_PLAIN=1 for mixed
-# deployments); from_wire(lazy=True) reads it into a CiphertextBuffer without per-element objects.
+# PaillierArray pickles through this format when FLEXPAI_PICKLE_BULK=1 (see the module docstring);
+# from_wire(lazy=True) reads it into a CiphertextBuffer without per-element objects.
 _WIRE_MAGIC = b"FPAW1\0"
 
 

@@ -116,9 +116,18 @@ class CiphertextBuffer(object):
     __radd__ = __add__
 
     def __sub__(self, other):
-        return self._add_plain(_plain(other, self.size) * -1)     # self + (other * -1), encrypted_number.py:74-75
+        # self + (other * -1), encrypted_number.py:74-75: an encrypted operand is scaled by -1 on the GPU
+        # (k_mul with the batch inversion) and added by k_add; a plain one is negated and added as plain
+        if isinstance(other, PaillierEncryptedNumber):
+            other = CiphertextBuffer.from_array(np.full(self.shape, other, dtype=object))
+        b = self._coerce(other)
+        if b is not None:
+            return add_buffers([self, b * -1])
+        return self._add_plain(_plain(other, self.size) * -1)
 
     def __rsub__(self, other):
+        if isinstance(other, PaillierEncryptedNumber):
+            return CiphertextBuffer.from_array(np.full(self.shape, other, dtype=object)) - self
         return (self * -1)._add_plain(other)                    # other + (self * -1), encrypted_number.py:77-78
 
     def _add_plain(self, y):

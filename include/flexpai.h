@@ -117,8 +117,8 @@ void pai_ctx_destroy(pai_ctx* ctx);
  * multiply-accumulates); PAI_OPT_CRT_ENCRYPT = 0 forces the public-key kernel. */
 int pai_ctx_set_option(pai_ctx* ctx, int option, int value);
 int pai_ctx_get_option(const pai_ctx* ctx, int option, int* value);
-/* With PAI_OPT_STAGE_TIMING on: kernel durations (ms) of the last encrypt call's final chunk, in launch
- * order (CRT: stage A, stage B, finish; public key on pairs: k_pe_pre, k_pe_pow, k_pe_fin; other public-key
+/* With PAI_OPT_STAGE_TIMING on: kernel durations (ms) of the last encrypt call, summed over its chunks
+ * (a host-buffer call's chunks included), in launch order (CRT: stage A, stage B, finish; public key on pairs: k_pe_pre, k_pe_pow, k_pe_fin; other public-key
  * paths: the one encrypt kernel). Waits for them. */
 int pai_ctx_stage_times(pai_ctx* ctx, float* ms_out, int max_out, int* count);
 /* key bits, 32-bit words per ciphertext (2*key_bits/32), words per plaintext (key_bits/32) */
@@ -139,6 +139,13 @@ int pai_ctx_fixed_base_prepare(pai_ctx* ctx);
 /* Cost of the last table build: host ms (bases, B_k, constants, hipMalloc), device ms (table kernels),
  * resident table bytes.                                                                            */
 int pai_ctx_fixed_base_setup(const pai_ctx* ctx, float* host_ms, float* device_ms, uint64_t* table_bytes);
+/* Fixed-base break-even: a device-RNG encryption builds the tables only once the device-RNG
+ * elements encrypted under this context (the current call included) reach `threshold` (estimated build
+ * time / per-element saving against the generic path; $FLEXPAI_FB_MIN_ELEMS overrides); smaller calls
+ * take the generic path (same ciphertext distribution). `seen`: elements counted so far. threshold = 0
+ * once the tables are resident or known unavailable. Replaces nothing in the reference (its obfuscator,
+ * obfuscator.py:23-37, has no per-key state); protects re-keying callers (he_sa_ft/train.py:39-40).  */
+int pai_ctx_fixed_base_policy(pai_ctx* ctx, long long* seen, long long* threshold);
 
 /* Encrypt N plaintexts. dtype PAI_F32/F64/I64. obf_mode PAI_OBF_*.
  *   r_le:      PAI_OBF_GIVEN only: r values as little-endian byte strings of r_bytes each, element i

@@ -2,7 +2,7 @@
 engine, recombined by k_crt_fin<8>), SURVEY.md §8 row (f) nb = 4096 / BASELINE configs[4]:
 
 * bit-exact against THE REFERENCE's own 4096-bit ciphertexts under the sampler's obfuscator
-  (tests/golden/paillier_golden_fb.json, made by tests/golden/make_golden_fb.py) at W = 12 and 16;
+  (tests/golden/paillier_golden_fb.json, made by tests/golden/make_golden_fb.py) at W = 12, 16 and 21 (the bench's);
 * bit-exact against the CPU restatement (oracle/paillier_oracle.py fb_encrypt_value) at other index
   bases and ragged sizes, identical across windows, decryptable;
 * with the table memory capped, device-RNG encryption falls back to the public-key path (r = the ChaCha20
@@ -46,8 +46,9 @@ def test_fixed_base_4096_params(ctx4096):
     assert nbytes == 2 * K * (1 << W) * 148 * 4          # rows of 148 canonical 28-bit limbs
 
 
-@pytest.mark.parametrize("window", [12, 16])
+@pytest.mark.parametrize("window", [12, 16, 21])
 def test_fixed_base_4096_matches_reference_goldens(ctx4096, golden_fb, window):
+    """W = 21 is the configs[4] bench window (98 digits per half, the largest whose tables fit one MI355X)."""
     N = _native()
     ctx, key = ctx4096
     g = golden_fb["keys"][str(NB)]

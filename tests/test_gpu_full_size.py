@@ -22,16 +22,24 @@ def ctx2048(golden):
     return _native.Context(key.n, 0, key.p, key.q), key
 
 
-def test_full_size_roundtrip(ctx2048):
+@pytest.mark.parametrize("window", [16, 23])
+def test_full_size_roundtrip(ctx2048, window):
+    """At the library default window and at the bench's timed one (W = 23, 2 x 96.6 GB of tables)."""
     from flex.crypto.paillier import _native as Nn
     ctx, key = ctx2048
     x = np.random.default_rng(0).standard_normal(N, dtype=np.float32)
     rk = bytes(range(200, 232))
-    ct, ex, st = ctx.encrypt(x, obf_mode=Nn.PAI_OBF_RNG, rng_key=rk, index_base=0)
+    try:
+        ctx.set_fb_window(window)
+        ctx.prepare_fixed_base()
+        assert ctx.fixed_base_info()[3] == window
+        ct, ex, st = ctx.encrypt(x, obf_mode=Nn.PAI_OBF_RNG, rng_key=rk, index_base=0)
+        params = ctx.fixed_base_info()
+    finally:
+        ctx.set_fb_window(16)
     assert np.all(st == 0)
     val, _, dst, _ = ctx.decrypt(ct, ex)
     assert np.all(dst == 0) and np.array_equal(val, x.astype(np.float64))
-    params = ctx.fixed_base_info()
     idx = [0, 1, N // 3, N - 1]
     got = Nn.words_to_ints(ct[idx])
     for j, i in enumerate(idx):

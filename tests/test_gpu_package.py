@@ -159,14 +159,15 @@ def test_decrypt_errors(pe_pd, golden):
         pd.decrypt(pe2.encrypt(np.array([1.0], dtype=np.float32)))
 
 
-def test_received_arrays_run_on_the_gpu(pe_pd):
-    """Arrays that arrive over the wire (pickled by the sender, ion.py:150-178) unpickle as PaillierArray
-    and the receiver's unchanged operators reach the device: the HE_SA_FT coordinator's `+`
+def test_received_arrays_run_on_the_gpu(pe_pd, monkeypatch):
+    """Arrays that arrive over the wire from flexpai senders that opted in to the bulk pickle
+    (FLEXPAI_PICKLE_BULK=1; ion.py:150-178) unpickle as PaillierArray and the receiver's unchanged operators reach the device: the HE_SA_FT coordinator's `+`
     (he_sa_ft/train.py:66-69) -> pai_add, HE_LINEAR's `sum(...)` (he_linear_ft/train.py:64-65) ->
     pai_add_plain + pai_add, HE_OTP_LR's `(-1/bs) * enc.dot(features)` (he_otp_lr_ft1/train.py:158-160)
     -> pai_matmul + pai_mul. Bit-exact against the oracle's restatement of encrypted_number.py."""
     from flex.crypto.paillier import _runtime
     from flex.crypto.paillier.cipher_array import PaillierArray
+    monkeypatch.setenv("FLEXPAI_PICKLE_BULK", "1")
     pe, pd = pe_pd
     key = O.Key(pe.pub_key.n, pd.priv_key.p, pd.priv_key.q)
     rng = np.random.default_rng(11)

@@ -1,7 +1,7 @@
 """Bulk ciphertext-array wire format (cipher_array.to_wire / from_wire): round trip of
-ciphertexts, exponents, obfuscation flags and shape; key checks; pickling a PaillierArray goes through the
-wire format (a PaillierArray comes back), and with FLEXPAI_PICKLE_PLAIN=1 it produces the plain object
-ndarray unmodified FLEX peers load. CPU only (no kernel calls)."""
+ciphertexts, exponents, obfuscation flags and shape; key checks; pickling a PaillierArray produces, by default, the plain object
+ndarray unmodified FLEX peers load, and with FLEXPAI_PICKLE_BULK=1 goes through the wire format (a
+PaillierArray comes back). CPU only (no kernel calls)."""
 import pickle
 
 import numpy as np
@@ -55,13 +55,13 @@ def test_wire_errors_and_pickle(golden, monkeypatch):
         from_wire(b"nonsense" + buf)
     with pytest.raises(TypeError):
         to_wire(np.array([1.0, 2.0]))
+    plain = pickle.loads(pickle.dumps(arr))           # default: the reference's object-ndarray pickle
+    assert type(plain) is np.ndarray and plain.dtype == object
+    monkeypatch.setenv("FLEXPAI_PICKLE_BULK", "1")
     back = pickle.loads(pickle.dumps(arr))
     assert type(back) is type(arr) and back._valid_packed() is not None
     assert [(a.ciphertext(False), a.exponent, a._is_obfuscated()) for a in arr] == \
         [(b.ciphertext(False), b.exponent, b._is_obfuscated()) for b in back]
-    monkeypatch.setenv("FLEXPAI_PICKLE_PLAIN", "1")
-    plain = pickle.loads(pickle.dumps(arr))
-    assert type(plain) is np.ndarray and plain.dtype == object
 
 
 def test_lazy_from_wire_buffer_round_trip(golden):

@@ -11,8 +11,8 @@ Workload (nb = 2048 key, seed 1; ciphertexts are uniform residues < n^2 with N(0
     (HE_SA_FT coordinator, he_sa_ft/train.py:66-69) -> pair-adds/s = 7 n / seconds;
   * dot: a pickled (32,) array times a (32, 6) float64 matrix with `.dot` (HE_OTP_LR,
     he_otp_lr_ft1/train.py:158-160) -> dots/s.
-For this package, `--plain` pickles plain object ndarrays (what an unmodified FLEX peer sends);
-otherwise PaillierArray's wire pickle. Prints one JSON line.
+For this package, `--plain` pickles plain object ndarrays (the default pickle, and what an unmodified FLEX
+peer sends); otherwise PaillierArray's bulk wire pickle (FLEXPAI_PICKLE_BULK=1). Prints one JSON line.
 """
 import argparse
 import json
@@ -35,8 +35,8 @@ def main():
     args = ap.parse_args()
     if not args.ref:
         sys.path.insert(0, os.path.join(ROOT, "ibond-flex_amd"))
-        if args.plain:
-            os.environ["FLEXPAI_PICKLE_PLAIN"] = "1"
+        if not args.plain:
+            os.environ["FLEXPAI_PICKLE_BULK"] = "1"
     from flex.crypto.paillier.encrypted_number import PaillierEncryptedNumber
     from flex.crypto.paillier.keypair import generate_paillier_keypair
     pk, _ = generate_paillier_keypair(2048, seed=1)

@@ -655,12 +655,14 @@ def main():
         npub = min(N, 1 << 16) if nb > 2048 else N
         ctx.set_crt(False)
         ctx.set_fixed_base(False)
+        ctx.set_public_fixed_base(False)    # the per-element exponentiation (same r as the CRT path)
         encrypt(x, ct2, ex2, index_base_chk, npub)
         pub_st = ctx.stage_times()          # k_encrypt: one stage; split pairs: k_pe_pre, k_pe_pow, k_pe_fin
         pub_ms = float(sum(pub_st))
         pe = bool(ctx.pair_paths & 4) and len(pub_st) == 3
         ctx.set_crt(True)
         ctx.set_fixed_base(use_fb)
+        ctx.set_public_fixed_base(True)
         torch.cuda.synchronize()
         ncmp = npub if use_crt else min(npub, S_chk)
         same = bool(torch.equal(ct2[:ncmp], ct_ref[:ncmp]))
@@ -675,6 +677,51 @@ def main():
         del ct2, ex2
         if not same:
             raise SystemExit("CRT and public-key ciphertexts differ")
+
+    # ---- a party holding ONLY the public key (HE_OTP_LR / HE_LR_FP hosts): public fixed bases (kernels_pfb.hpp)
+    pfb_check = None
+    if not args.no_public and solo and nb == 2048:
+        cpub = _native.Context(pk.n, local_rank)
+        t1 = time.perf_counter()
+        cpub.prepare_public_fixed_base()
+        pfb_setup_ms = (time.perf_counter() - t1) * 1e3
+        cpub.set_stage_timing(True)
+        ct3 = torch.empty_like(ct)
+        ex3 = torch.empty_like(ex)
+        runs = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            rc = lib.pai_encrypt_dev(cpub.handle, _native.PAI_F32, x.data_ptr(), N, 0, 0, _native.PAI_OBF_RNG, None, 0, 0,
+                                     rng_key, index_base_chk, ct3.data_ptr(), ex3.data_ptr(), st.data_ptr(),
+                                     stream.cuda_stream)
+            if rc != 0:
+                raise RuntimeError(lib.pai_last_error().decode())
+            torch.cuda.synchronize()
+            runs.append((time.perf_counter() - t1, cpub.stage_times()))
+        wall, pst = min(runs, key=lambda r: r[0])
+        bases, Kp, Wp, K0p = cpub.public_fixed_base_info()
+        wpfb = float(Kp * _Mp(nb // 32))            # K pair products mod n^2 over the nb/32 32-bit limbs of n
+        # exact round trip through the key holder's decryption
+        valp = torch.empty(N, dtype=torch.float64, device=dev)
+        stp = torch.empty(N, dtype=torch.int32, device=dev)
+        decrypt(ct3, ex3, valp, stp)
+        torch.cuda.synchronize()
+        okp = bool(torch.equal(valp, x.double())) and int((stp > 1).sum().item()) == 0
+        extra["public_key_fixed_base"] = {
+            "value": N / wall, "unit": "encrypts/s per GPU", "elements": N,
+            "kernel": "k_pfb_digits + k_pfb + k_pe_fin", "stages_ms": dict(zip(["k_pfb_digits", "k_pfb", "k_pe_fin"], pst)),
+            "k_pfb_int_mac_frac": N * wpfb / (pst[1] * 1e-3) / INT_MAC_PEAK if len(pst) > 1 else None,
+            "work_mac_per_elem": wpfb, "digits": Kp, "window": Wp, "e0_digits": K0p,
+            "setup_ms": pfb_setup_ms, "table_bytes": Kp * (1 << Wp) * 512,
+            "roundtrip_exact": okp,
+            "note": "a public-key-only context: r = prod_j g_j^e_j mod n over 33 self-drawn bases (DESIGN.md §3), "
+                    "r^n as K table-row products; ciphertexts are the reference's encryption under that r"}
+        pfb_check = (bases, Wp, ct3[:4].cpu().numpy().view(np.uint32).copy(), ex3[:4].cpu().numpy().copy())
+        del ct3, ex3, valp, stp, cpub
+        torch.cuda.empty_cache()
+        if not okp:
+            raise SystemExit("public fixed-base ciphertexts do not decrypt to the input")
 
     # ---- configs[2] beside configs[1]: encrypt 8 arrays, one 8-way add (k_add), decrypt the sum
     if cfg_id == 1 and solo and not args.no_add8 and not args.no_decrypt:
@@ -849,6 +896,16 @@ def main():
                 cpu["fixed_base_bit_exact_vs_oracle"] = {"elements": idx, "ok": fb_ok}
                 if not fb_ok:
                     raise SystemExit("fixed-base ciphertexts differ from the oracle restatement")
+            if pfb_check is not None:
+                from oracle import paillier_oracle as O
+                bases, Wp, cts, exs = pfb_check
+                okey = O.Key(pk.n, sk.p, sk.q)
+                got = _native.words_to_ints(cts)
+                pok = all(O.pfb_encrypt_value(x_host[i], okey, bases, rng_key, index_base_chk + i, Wp)
+                          == (got[i], int(exs[i])) for i in range(len(got)))
+                cpu["public_fixed_base_bit_exact_vs_oracle"] = {"elements": list(range(len(got))), "ok": pok}
+                if not pok:
+                    raise SystemExit("public fixed-base ciphertexts differ from the oracle restatement")
             # configs[0] timed in full: nb = 1024, 1000 elements, encrypt + decrypt, threads = os.cpu_count()
             pk0, sk0 = generate_paillier_keypair(1024, seed=1)
             x0 = np.random.default_rng(0).standard_normal(1000, dtype=np.float32)

@@ -4,17 +4,18 @@
 namespace fpai {
 
 static size_t pg_lds() { return ((size_t)(BLOCK / FBGP_TPI) * 2 * FBGP_S + FBGP_S) * 4; }
+static size_t main_lds() { return ((size_t)(BLOCK / FBGP_TPI) * (2 * FBGP_S + 2 * FBGP_PW) + FBGP_S) * 4; }   // + row staging
 static size_t w_lds() { return (size_t)(BLOCK / 4) * 4 * L * 4; }
 
 int fbgp_occupancy(int* occ) {
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, k_fbgp<FBGP_TPI, FBGP_LL>, BLOCK, pg_lds()) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, k_fbgp<FBGP_TPI, FBGP_LL>, BLOCK, main_lds()) != hipSuccess ||
       *occ < 1)
     *occ = 1;
   return 0;
 }
 
 hipError_t fbgp_launch(const FbgpParams& p, int gx, hipStream_t st) {
-  hipLaunchKernelGGL((k_fbgp<FBGP_TPI, FBGP_LL>), dim3(gx, 2), dim3(BLOCK), pg_lds(), st, p);
+  hipLaunchKernelGGL((k_fbgp<FBGP_TPI, FBGP_LL>), dim3(gx, 2), dim3(BLOCK), main_lds(), st, p);
   return hipGetLastError();
 }
 

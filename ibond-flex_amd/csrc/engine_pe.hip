@@ -36,4 +36,11 @@ hipError_t pe_launch(const PeParams& p, const Dec4Geom& g, hipStream_t st, hipEv
   return hipSuccess;
 }
 
+hipError_t pe_launch_fin(const PeParams& p, int cus, hipStream_t st) {
+  const long long lb = (p.n + LANE_BLOCK - 1) / LANE_BLOCK;
+  const int gx = (int)std::max<long long>(1, std::min<long long>(lb, (long long)occupancy(k_pe_fin<D4_S>) * cus));
+  hipLaunchKernelGGL(k_pe_fin<D4_S>, dim3(gx), dim3(LANE_BLOCK), 0, st, p);
+  return hipGetLastError();
+}
+
 }  // namespace fpai

@@ -7,5 +7,7 @@ namespace fpai {
 
 int pe_geometry(int cus, long long chunk, Dec4Geom* g);   // gx_pre, gx_pow, gx_L (= k_pe_fin), scratch_bytes
 hipError_t pe_launch(const PeParams& p, const Dec4Geom& g, hipStream_t st, hipEvent_t* ev);
+// k_pe_fin alone: c = A + n B from the pairs in p.xw (the public fixed-base path, engine_pfb.hip)
+hipError_t pe_launch_fin(const PeParams& p, int cus, hipStream_t st);
 
 }  // namespace fpai

@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <sys/random.h>
 #include <thread>
 #include <vector>
 
@@ -22,6 +23,7 @@
 #include "engine_dec4.hpp"
 #include "engine_grp_pair.hpp"
 #include "engine_pe.hpp"
+#include "engine_pfb.hpp"
 #include "engine_grp.hpp"
 #include "engine_mul.hpp"
 
@@ -120,8 +122,21 @@ struct pai_ctx {
   uint32_t* fb_last_w = nullptr;  // debugging: k_fb output of the last chunk ([2][SB][fb_last_n])
   long long fb_last_n = 0;
   uint64_t fb_table_bytes = 0;
+  // public-key fixed-base obfuscators (kernels_pfb.hpp): device-RNG encryption without the private key.
+  // Built lazily past the break-even count (or pai_ctx_public_fb_prepare); never needed for correctness.
+  int pfb_state = FB_UNTRIED;
+  std::string pfb_reason;
+  bool pfb_enabled = true;
+  int pfb_W = 0, pfb_W_used = 0, pfb_K = 0, pfb_K0 = 0, pfb_KS = 0;
+  std::vector<HBig> pfb_bases;  // g_0 .. g_PFB_SHORT (chosen at the first build unless set)
+  PfbConst* d_pfb = nullptr;
+  std::vector<void*> pfb_mem;
+  long long pfb_seen = 0;
+  float pfb_host_ms = 0.f, pfb_dev_ms = 0.f;
+  uint64_t pfb_table_bytes = 0;
   long long fb_seen = 0;        // device-RNG elements encrypted under this key before the tables exist
   int fb_call = 0;              // host-buffer call in progress: its one fixed-base decision (+1 / -1), else 0
+  int pfb_call = 0;             // the same for the public fixed-base sampler
   bool stage_keep = false;      // host-buffer calls: stage timing spans all chunks of the call
   std::vector<void*> allocs;
   std::vector<void*> priv_allocs;   // private-key constants: all freed together if set_private fails
@@ -171,6 +186,7 @@ struct pai_ctx {
     for (void* p : allocs) (void)hipFree(p);
     for (void* p : priv_allocs) (void)hipFree(p);
     for (void* p : fb_mem) (void)hipFree(p);
+    for (void* p : pfb_mem) (void)hipFree(p);
     if (d_scratch) (void)hipFree(d_scratch);
     if (d_work) (void)hipFree(d_work);
     if (d_mul) (void)hipFree(d_mul);
@@ -554,13 +570,27 @@ static int fb_row_words(int sb) {
   return sb == 37 ? FbGeom<37>::TW : sb == 74 ? FbGeom<74>::TW : sb == GRP_TPI * L ? GRP_TPI * L : 0;
 }
 
+// 4096-bit keys: the pair-group sampler (kernels_grp_pair.hpp) runs when both p_h fit its 76 limbs with
+// R >= 2^24 p_h ($FLEXPAI_FB_PAIR=0 selects k_fbg); its rows are the canonical pair as 2 x 64 words
+static bool fb_gpair_possible(const pai_ctx* c) {
+  if (c->crt_sb != GRP_TPI * L) return false;
+  if (const char* e = getenv("FLEXPAI_FB_PAIR"))
+    if (atoi(e) == 0) return false;
+  for (const HBig* h : {&c->fb_p, &c->fb_q})
+    if (h->bits() + 24 > (size_t)LB * FBGP_S || h->bits() > (size_t)LB * FBGP_SP || h->bits() > (size_t)32 * FBGP_PW)
+      return false;
+  return true;
+}
+
+static int fb_row_words(const pai_ctx* c) { return fb_gpair_possible(c) ? 4 * FBGP_ROW4 : fb_row_words(c->crt_sb); }
+
 static int fb_digit_count(const pai_ctx* c, int W) {
   const size_t kb = std::max(sub(c->fb_p, HBig(1)).bits(), sub(c->fb_q, HBig(1)).bits());
   return (int)((kb + W - 1) / W);
 }
 
 static uint64_t fb_bytes(const pai_ctx* c, int W) {
-  return 2ull * (uint64_t)fb_digit_count(c, W) * (1ull << W) * (uint64_t)fb_row_words(c->crt_sb) * 4ull;
+  return 2ull * (uint64_t)fb_digit_count(c, W) * (1ull << W) * (uint64_t)fb_row_words(c) * 4ull;
 }
 
 // Budget for the two tables: $FLEXPAI_FB_MAX_BYTES, else the free device memory less a reserve of
@@ -591,6 +621,8 @@ static long long fb_break_even(const pai_ctx* c, int W, int K, int row_bytes) {
 }
 
 static bool fb_wanted(pai_ctx* c, long long n);
+static bool pfb_supported(const pai_ctx* c);
+static void pfb_release(pai_ctx* c);
 
 static void fb_release(pai_ctx* c) {
   for (void* p : c->fb_mem) (void)hipFree(p);
@@ -625,7 +657,7 @@ static int ensure_fb(pai_ctx* c) {
   if (c->fb_state == pai_ctx::FB_READY) return 1;
   if (c->fb_state == pai_ctx::FB_UNAVAILABLE) return 0;
   if (!c->crt_ok && !c->fbg_ok) return fb_unavailable(c, "needs the private key and the CRT kernels");
-  const int sb = c->crt_sb, TW = fb_row_words(sb);
+  const int sb = c->crt_sb, TW = fb_row_words(c);
   if (!TW) return fb_unavailable(c, "key size not supported by the fixed-base kernels");
   const bool grp = sb == GRP_TPI * L;   // group-engine rows (limbs), recombined by k_crt_fin
   const HBig sq[2] = {mul(c->fb_p, c->fb_p), mul(c->fb_q, c->fb_q)};
@@ -659,10 +691,7 @@ static int ensure_fb(pai_ctx* c) {
   for (int h = 0; h < 2 && pair_ok; ++h)
     pair_ok = primes[h].bits() <= (size_t)32 * pw && primes[h].bits() + FBP_PB + 1 <= (size_t)LB * ps;
   // 4096-bit keys: pair products on lane groups of 4 x 19 limbs (kernels_grp_pair.hpp), R = 2^(28 76) >= 2^24 p_h
-  bool gpair_ok = grp;
-  if (const char* e = getenv("FLEXPAI_FB_PAIR")) gpair_ok = gpair_ok && atoi(e) != 0;
-  for (int h = 0; h < 2 && gpair_ok; ++h)
-    gpair_ok = primes[h].bits() + 24 <= (size_t)LB * FBGP_S && primes[h].bits() <= (size_t)LB * FBGP_SP;
+  const bool gpair_ok = grp && fb_gpair_possible(c);
   const int lohi_limbs = pair_ok ? std::max(sb, 2 * ps) : gpair_ok ? std::max(sb, 2 * FBGP_S) : sb;
   FbgpHalf gv[2];
   FbpHalf pv[2];
@@ -1161,6 +1190,15 @@ int pai_ctx_set_option(pai_ctx* c, int option, int value) {
     case PAI_OPT_STAGE_TIMING: c->timing = value != 0; stage_reset(c); return 0;
     case PAI_OPT_LANE_DECRYPT: c->dec_lane_enabled = value != 0; return 0;
     case PAI_OPT_FIXED_BASE: c->fb_enabled = value != 0; return 0;
+    case PAI_OPT_PUBLIC_FB: c->pfb_enabled = value != 0; return 0;
+    case PAI_OPT_PFB_WINDOW:
+      if (!fb_window_ok(value)) return fail(PAI_ERR_ARG, "fixed-base window must be 8, 12, 16 or 20 .. 24");
+      if (value == c->pfb_W) return 0;
+      c->pfb_W = value;
+      HIPCHK(hipSetDevice(c->device));
+      pfb_release(c);
+      c->pfb_state = pai_ctx::FB_UNTRIED;
+      return 0;
     case PAI_OPT_FB_WINDOW:
       if (!fb_window_ok(value)) return fail(PAI_ERR_ARG, "fixed-base window must be 8, 12, 16 or 20 .. 24");
       if (value == c->fb_W) return 0;
@@ -1186,6 +1224,11 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
       return 0;
     case PAI_OPT_FB_WINDOW: *value = c->fb_W_used ? c->fb_W_used : c->fb_W ? c->fb_W : fb_default_window(); return 0;
     case PAI_OPT_FB_READY: *value = c->fb_state == pai_ctx::FB_READY ? 1 : 0; return 0;
+    case PAI_OPT_PUBLIC_FB:
+      *value = (pfb_supported(c) && c->pfb_enabled && c->pfb_state != pai_ctx::FB_UNAVAILABLE) ? 1 : 0;
+      return 0;
+    case PAI_OPT_PFB_READY: *value = c->pfb_state == pai_ctx::FB_READY ? 1 : 0; return 0;
+    case PAI_OPT_PFB_WINDOW: *value = c->pfb_W_used ? c->pfb_W_used : c->pfb_W ? c->pfb_W : fb_default_window(); return 0;
     case PAI_OPT_FB_PAIR:
       *value = c->fb_state == pai_ctx::FB_READY ? (c->fb_gpair ? FBGP_S : c->fb_pair_s) : 0;
       return 0;
@@ -1242,7 +1285,7 @@ int pai_ctx_fixed_base_prepare(pai_ctx* c) {
 // the path is unavailable: nothing left to decide).
 static long long fb_threshold(pai_ctx* c) {
   if (c->fb_state != pai_ctx::FB_UNTRIED || (!c->crt_ok && !c->fbg_ok)) return 0;
-  const int TW = fb_row_words(c->crt_sb);
+  const int TW = fb_row_words(c);
   if (!TW) return 0;
   if (!c->fb_W) c->fb_W = fb_default_window();
   const uint64_t budget = fb_budget(c);
@@ -1421,6 +1464,303 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
   return 0;
 }
 
+// ------------------------------------------------------------------ public-key fixed bases (kernels_pfb.hpp)
+// A party without the private key samples r = g_0^e_0 g_1^e_1 ... g_32^e_32 mod n from 33 bases it drew itself
+// (g_0 with Jacobi symbol -1) and exponents from the element's ChaCha20 stream (e_0: nb + 64 bits, e_j: 96 bits),
+// and gets r^n mod n^2 as a product of table rows (distribution argument, break-even).
+static bool pfb_supported(const pai_ctx* c) {
+  return c->pe_ok && c->ct_words == 2 * PFB_PW && (size_t)c->nb + 24 <= (size_t)LB * PFB_S;
+}
+
+static void pfb_digit_counts(const pai_ctx* c, int W, int* K0, int* KS) {
+  *K0 = (c->nb + PFB_E0_EXTRA + W - 1) / W;
+  *KS = (PFB_TBITS + W - 1) / W;
+}
+
+static uint64_t pfb_bytes(const pai_ctx* c, int W) {
+  int K0, KS;
+  pfb_digit_counts(c, W, &K0, &KS);
+  return (uint64_t)(K0 + PFB_SHORT * KS) * (1ull << W) * PFB_ROW4 * 16ull;
+}
+
+static int pfb_choose_window(pai_ctx* c) {
+  if (!c->pfb_W) c->pfb_W = fb_default_window();
+  const uint64_t budget = fb_budget(c);
+  for (int w : {24, 23, 22, 21, 20, 16, 12, 8})
+    if (w <= c->pfb_W && pfb_bytes(c, w) <= budget) return w;
+  return 0;
+}
+
+static void pfb_release(pai_ctx* c) {
+  for (void* q : c->pfb_mem) (void)hipFree(q);
+  c->pfb_mem.clear();
+  c->d_pfb = nullptr;
+}
+
+static int pfb_unavailable(pai_ctx* c, const std::string& why) {
+  pfb_release(c);
+  (void)hipGetLastError();
+  c->pfb_state = pai_ctx::FB_UNAVAILABLE;
+  c->pfb_reason = why;
+  return 0;
+}
+
+template <typename T>
+static int upload_pfb(pai_ctx* c, const std::vector<T>& v, T** out) {
+  void* q = nullptr;
+  HIPCHK(hipMalloc(&q, std::max<size_t>(v.size(), 1) * sizeof(T)));
+  c->pfb_mem.push_back(q);
+  if (!v.empty()) HIPCHK(hipMemcpy(q, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  *out = (T*)q;
+  return 0;
+}
+
+// Jacobi symbol (a | n) for odd n > 0: halvings (second supplement), swaps (reciprocity), subtractions
+static int jacobi(HBig a, HBig n) {
+  if (cmp(a, n) >= 0) a = mod(a, n);
+  int t = 1;
+  while (!a.is_zero()) {
+    while (!a.is_odd()) {
+      a = shr1(a);
+      const uint32_t r = n.w[0] & 7u;
+      if (r == 3 || r == 5) t = -t;
+    }
+    if (cmp(a, n) < 0) {
+      std::swap(a, n);
+      if ((a.w[0] & 3u) == 3u && (n.w[0] & 3u) == 3u) t = -t;
+    }
+    a = sub(a, n);
+  }
+  return (n.w.size() == 1 && n.w[0] == 1u) ? t : 0;
+}
+
+// uniform in [2, n) from the OS CSPRNG (rejection sampling on bits(n) bits)
+static bool random_below(const HBig& n, HBig* out) {
+  const size_t nw = n.w.size();
+  const int top = (int)(n.bits() - 32 * (nw - 1));
+  for (int tries = 0; tries < 1000; ++tries) {
+    HBig r;
+    r.w.assign(nw, 0);
+    size_t got = 0;
+    while (got < nw * 4) {
+      const ssize_t k = getrandom((char*)r.w.data() + got, nw * 4 - got, 0);
+      if (k <= 0) return false;
+      got += (size_t)k;
+    }
+    if (top < 32) r.w[nw - 1] &= (1u << top) - 1u;
+    r.trim();
+    if (cmp(r, n) < 0 && r.bits() > 1) {
+      *out = r;
+      return true;
+    }
+  }
+  return false;
+}
+
+static int ensure_pfb(pai_ctx* c) {
+  if (c->pfb_state == pai_ctx::FB_READY) return 1;
+  if (c->pfb_state == pai_ctx::FB_UNAVAILABLE) return 0;
+  if (!pfb_supported(c)) return pfb_unavailable(c, "the public fixed-base kernels need a 1537..2048-bit n");
+  const int W = pfb_choose_window(c);
+  if (!W) return pfb_unavailable(c, "tables do not fit the device memory budget");
+  const auto t0 = std::chrono::steady_clock::now();
+  int K0, KS;
+  pfb_digit_counts(c, W, &K0, &KS);
+  const int K = K0 + PFB_SHORT * KS;
+  const HBig& n = c->n;
+  if (c->pfb_bases.empty()) {
+    HBig g;
+    do {
+      if (!random_below(n, &g)) return pfb_unavailable(c, "no randomness for the bases");
+    } while (jacobi(g, n) != -1);   // g_0: Jacobi symbol -1, so the publicly visible symbol of c mod n is uniform
+    c->pfb_bases.push_back(g);
+    for (int j = 0; j < PFB_SHORT; ++j) {
+      if (!random_below(n, &g)) return pfb_unavailable(c, "no randomness for the bases");
+      c->pfb_bases.push_back(g);
+    }
+  }
+  const HBig& n2 = c->N;
+  const size_t RS = (size_t)LB * PFB_S;
+  auto split = [&](const HBig& v) {   // v < n^2 -> [v mod n: S limbs][v div n: S limbs]
+    const HBig qt = div_big(v, n), rm = sub(v, mul(qt, n));
+    std::vector<uint32_t> out = rm.limbs(PFB_S, LB), b = qt.limbs(PFB_S, LB);
+    out.insert(out.end(), b.begin(), b.end());
+    return out;
+  };
+  const HBig oneR = mul_pow2_mod(HBig(1), RS, n2);
+  const HBig R2 = mul_pow2_mod(oneR, RS, n2);
+  const HBig X = mod(sub(add(n, HBig(1)), mul_pow2_mod(HBig(1), RS, n)), n);   // (1 - R) mod n
+  std::vector<uint32_t> gl;
+  for (const HBig& g : c->pfb_bases) {
+    const std::vector<uint32_t> v = g.limbs(PFB_S, LB);
+    gl.insert(gl.end(), v.begin(), v.end());
+  }
+  pfb_release(c);
+  uint32_t *dn, *dx, *done, *dr2, *dgl, *dnw, *dbases, *dlohi;
+  uint4* dtab;
+  int rc;
+  if ((rc = upload_pfb(c, n.limbs(PFB_S, LB), &dn)) || (rc = upload_pfb(c, X.limbs(PFB_S, LB), &dx)) ||
+      (rc = upload_pfb(c, split(oneR), &done)) || (rc = upload_pfb(c, split(R2), &dr2)) ||
+      (rc = upload_pfb(c, gl, &dgl)) || (rc = upload_pfb(c, n.words(PFB_PW), &dnw)))
+    return pfb_unavailable(c, pai_last_error());
+  void *vb = nullptr, *vl = nullptr, *vt = nullptr;
+  if (hipMalloc(&vb, (size_t)K * 2 * 2 * PFB_S * 4) != hipSuccess) return pfb_unavailable(c, "table allocation failed");
+  c->pfb_mem.push_back(vb);
+  if (hipMalloc(&vl, (size_t)K * 2 * FB_LO * 2 * PFB_S * 4) != hipSuccess) return pfb_unavailable(c, "table allocation failed");
+  c->pfb_mem.push_back(vl);
+  if (hipMalloc(&vt, ((size_t)K << W) * PFB_ROW4 * sizeof(uint4)) != hipSuccess)
+    return pfb_unavailable(c, "table allocation failed");
+  c->pfb_mem.push_back(vt);
+  dbases = (uint32_t*)vb;
+  dlohi = (uint32_t*)vl;
+  dtab = (uint4*)vt;
+  PfbConst pc{};
+  pc.g = FbgpHalf{(const uint32_t*)dtab, dn, dx, done, dbases, dlohi, nullptr, nullptr, nullptr, nullptr,
+                  mont_prime(n, LB), 0u};
+  pc.table = dtab;
+  pc.gl = dgl;
+  pc.r2 = dr2;
+  pc.nw = dnw;
+  pc.nbits = (int)n.bits();
+  pc.nbases = (int)c->pfb_bases.size();
+  pc.K = K;
+  pc.W = W;
+  pc.K0 = K0;
+  pc.KS = KS;
+  std::vector<PfbConst> pv{pc};
+  PfbConst* dpc = nullptr;
+  if ((rc = upload_pfb(c, pv, &dpc))) return pfb_unavailable(c, pai_last_error());
+  const auto t1 = std::chrono::steady_clock::now();
+  if (pfb_build_tables(dpc, pc.nbases, K, W, dtab, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    return pfb_unavailable(c, "table construction failed");
+  for (void* q : {vb, vl}) {   // build scratch
+    c->pfb_mem.erase(std::find(c->pfb_mem.begin(), c->pfb_mem.end(), q));
+    (void)hipFree(q);
+  }
+  const auto t2 = std::chrono::steady_clock::now();
+  c->d_pfb = dpc;
+  c->pfb_host_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
+  c->pfb_dev_ms = std::chrono::duration<float, std::milli>(t2 - t1).count();
+  c->pfb_table_bytes = pfb_bytes(c, W);
+  c->pfb_K = K;
+  c->pfb_K0 = K0;
+  c->pfb_KS = KS;
+  c->pfb_W_used = W;
+  c->pfb_state = pai_ctx::FB_READY;
+  return 1;
+}
+
+// Break-even of the public tables: build ~0.08 s + ~9 ns per row (76-limb pair products, 4x a 37-limb row of the
+// key holder's tables), saving 1/415 k - 1/2.5 M s = 2.0 us per element against k_pe_* 
+static long long pfb_threshold(pai_ctx* c) {
+  if (c->pfb_state != pai_ctx::FB_UNTRIED || !pfb_supported(c)) return 0;
+  if (const char* e = getenv("FLEXPAI_PFB_MIN_ELEMS")) return atoll(e);
+  const int W = pfb_choose_window(c);
+  if (!W) return 0;
+  int K0, KS;
+  pfb_digit_counts(c, W, &K0, &KS);
+  const double build_s = 0.08 + (double)(K0 + PFB_SHORT * KS) * (double)(1ull << W) * 9e-9;
+  return (long long)(build_s / 2.0e-6) + 1;
+}
+
+static bool pfb_wanted(pai_ctx* c, long long n) {
+  if (c->pfb_state != pai_ctx::FB_UNTRIED) return true;
+  if (c->pfb_call) return c->pfb_call > 0;
+  c->pfb_seen += n;
+  return c->pfb_seen >= pfb_threshold(c);
+}
+
+// digits, k_pfb, k_pe_fin per chunk of CRT_CHUNK elements
+static int launch_pfb(pai_ctx* c, const EncParams& e, hipStream_t st) {
+  const long long N = e.n;
+  const long long chunk = std::min(N, CRT_CHUNK);
+  int occ = 1;
+  pfb_occupancy(&occ);
+  constexpr int GPB = BLOCK / PFB_TPI;
+  const int gx = (int)std::max<long long>(1, std::min<long long>((chunk + GPB - 1) / GPB, (long long)occ * c->cus));
+  const size_t dbytes = (size_t)c->pfb_K * 4, xbytes = (size_t)2 * PFB_SP * 4;
+  int rc;
+  if ((rc = ensure_work(c, (dbytes + xbytes) * chunk))) return rc;
+  uint32_t* digits = (uint32_t*)c->d_work;
+  uint32_t* xw = (uint32_t*)((char*)c->d_work + dbytes * chunk);
+  const size_t esz = e.dtype == PAI_F32 ? 4 : 8;
+  for (long long off = 0; off < N; off += chunk) {
+    const long long n = std::min(chunk, N - off);
+    PfbDigitParams pd{};
+    pd.n = n;
+    std::memcpy(pd.rng_key, e.rng_key, sizeof(pd.rng_key));
+    pd.index_base = e.index_base + (unsigned long long)off;
+    pd.K = c->pfb_K;
+    pd.W = c->pfb_W_used;
+    pd.digits = digits;
+    const int gD = (int)std::max<long long>(1, std::min<long long>((long long)8 * c->cus, (n + PFB_DIG_BLOCK - 1) / PFB_DIG_BLOCK));
+    stage_mark(c, 0, st);
+    HIPCHK(pfb_launch_digits(pd, gD, st));
+    stage_mark(c, 1, st);
+    const PfbParams pp{c->d_pfb, n, digits, (const char*)e.x + (size_t)off * esz, e.dtype, e.exp_mode, e.fexp,
+                       e.exp + off, e.status ? e.status + off : nullptr, xw};
+    HIPCHK(pfb_launch(pp, (int)std::min<long long>(gx, (n + GPB - 1) / GPB), st));
+    stage_mark(c, 2, st);
+    PeParams pf{};
+    pf.k = c->d_pe;
+    pf.n = n;
+    pf.xw = xw;
+    pf.ct = e.ct + (size_t)off * c->ct_words;
+    pf.ct_words = c->ct_words;
+    HIPCHK(pe_launch_fin(pf, c->cus, st));
+    stage_mark(c, 3, st);
+  }
+  return 0;
+}
+
+int pai_ctx_public_fb_prepare(pai_ctx* c) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  HIPCHK(hipSetDevice(c->device));
+  if (!ensure_pfb(c)) return fail(PAI_ERR_KEY, "public fixed-base obfuscation not available: " + c->pfb_reason);
+  return 0;
+}
+
+int pai_ctx_public_fb_set_bases(pai_ctx* c, const uint8_t* bases_le, size_t base_bytes, int nbases) {
+  if (!c || !bases_le || base_bytes == 0) return fail(PAI_ERR_ARG, "pai_ctx_public_fb_set_bases: null argument");
+  if (nbases != PFB_NBASES) return fail(PAI_ERR_ARG, "pai_ctx_public_fb_set_bases: wrong number of bases");
+  std::vector<HBig> bs;
+  for (int j = 0; j < nbases; ++j) {
+    HBig g = HBig::from_le_bytes(bases_le + (size_t)j * base_bytes, base_bytes);
+    if (g.bits() < 2 || cmp(g, c->n) >= 0) return fail(PAI_ERR_ARG, "pai_ctx_public_fb_set_bases: need 1 < g < n");
+    bs.push_back(g);
+  }
+  HIPCHK(hipSetDevice(c->device));
+  pfb_release(c);
+  c->pfb_bases = bs;
+  c->pfb_state = pai_ctx::FB_UNTRIED;
+  return 0;
+}
+
+int pai_ctx_public_fb_info(pai_ctx* c, uint8_t* bases_le, size_t base_bytes, int* nbases, int* digits, int* window,
+                           int* e0_digits) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (c->pfb_state != pai_ctx::FB_READY) return fail(PAI_ERR_KEY, "public fixed-base tables are not resident");
+  if (bases_le) {
+    for (size_t j = 0; j < c->pfb_bases.size(); ++j) {
+      const std::vector<uint32_t> w = c->pfb_bases[j].words((base_bytes + 3) / 4);
+      if (c->pfb_bases[j].bits() > 8 * base_bytes) return fail(PAI_ERR_ARG, "pai_ctx_public_fb_info: base_bytes too small");
+      std::memcpy(bases_le + j * base_bytes, w.data(), base_bytes);
+    }
+  }
+  if (nbases) *nbases = (int)c->pfb_bases.size();
+  if (digits) *digits = c->pfb_K;
+  if (window) *window = c->pfb_W_used;
+  if (e0_digits) *e0_digits = c->pfb_K0;
+  return 0;
+}
+
+int pai_ctx_public_fb_policy(pai_ctx* c, long long* seen, long long* threshold) {
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  if (seen) *seen = c->pfb_seen;
+  if (threshold) *threshold = pfb_threshold(c);
+  return 0;
+}
+
 // public-key encryption on split pairs (kernels_pe.hpp, engine_pe.hip), in chunks of CRT_CHUNK elements
 static int launch_pe(pai_ctx* c, const EncParams& e, hipStream_t st) {
   const long long N = e.n;
@@ -1589,6 +1929,8 @@ int pai_encrypt_dev(pai_ctx* c, int dtype, const void* d_x, size_t N, int exp_mo
     if (c->crt_sa == 19) return launch_crt<19, 37>(c, p, st);
     if (c->crt_sa == 37) return launch_crt<37, 74>(c, p, st);
   }
+  if (obf_mode == PAI_OBF_RNG && c->pfb_enabled && pfb_supported(c) && pfb_wanted(c, p.n) && ensure_pfb(c))
+    return launch_pfb(c, p, st);
   if (obf_mode != PAI_OBF_NONE && c->pe_ok && c->ct_words == 2 * 64) return launch_pe(c, p, st);
   switch (c->tpi_e) {
     case 2: return launch_encrypt<2>(c, p, st);
@@ -2339,6 +2681,7 @@ struct HostCall {
   ~HostCall() {
     c->stage_keep = false;
     c->fb_call = 0;
+    c->pfb_call = 0;
   }
 };
 
@@ -2375,7 +2718,10 @@ int pai_encrypt(pai_ctx* c, int dtype, const void* x, size_t N, int exp_mode, in
   // one fixed-base decision and one stage-timing record for the whole call: the ciphertexts of a call do
   // not depend on how it is chunked
   HostCall hc(c);
-  if (obf_mode == PAI_OBF_RNG) c->fb_call = fb_wanted(c, (long long)N) ? 1 : -1;
+  if (obf_mode == PAI_OBF_RNG) {
+    if ((c->crt_ok || c->fbg_ok) && c->crt_enabled) c->fb_call = fb_wanted(c, (long long)N) ? 1 : -1;
+    else if (c->pfb_enabled && pfb_supported(c)) c->pfb_call = pfb_wanted(c, (long long)N) ? 1 : -1;
+  }
   // every chunk's kernels are queued first; the copy stream then drains chunk i while i+1.. compute
   for (int i = 0; i < nch; ++i) {
     const size_t off = (size_t)i * CH, n = std::min(CH, N - off);

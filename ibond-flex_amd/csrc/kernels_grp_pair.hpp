@@ -5,8 +5,8 @@
 //   k_fbgp       w_h = c0 G_h^(a_h) mod p_h^2 as the canonical pair (A, B) (c0 = the pair (1, (n/p_h) M))
 //   k_fbgp_w     w_h = A + p_h B mod p_h^2 (one product mod p_h^2 on the L = 37 group engine, in place), so
 //                k_fbg_garner and k_fbg_fin recombine exactly as after k_fbg
-//   k_fbgp_lohi / k_fbgp_fill   the per-key tables: rows of [A: 74][B: 74] limbs of T_k[d] R mod p_h^2 (the
-//                148-limb row size of k_fbg's tables)
+//   k_fbgp_lohi / k_fbgp_fill   the per-key tables: rows of the canonical pair of T_k[d] R mod p_h^2 as the
+//                32-bit words of A then of B (512 B, below)
 #pragma once
 #include "bn_pgroup.hpp"
 #include "kernels_grp.hpp"
@@ -14,10 +14,12 @@
 namespace fpai {
 
 constexpr int FBGP_TPI = 4, FBGP_LL = 19, FBGP_S = FBGP_TPI * FBGP_LL;   // 76 limbs >= the 74 of a 2048-bit p_h
-constexpr int FBGP_SP = 74;                                               // limbs of A and of B in a table row
+constexpr int FBGP_SP = 74;                                               // limbs of A and of B that can be non-zero
+constexpr int FBGP_PW = 64;                 // 32-bit words of A and of B in a table row (a canonical pair: A, B < 2^2048)
+constexpr int FBGP_ROW4 = 2 * FBGP_PW / 4;  // uint4 per row: 512 B, four aligned 128-B lines
 
 struct FbgpHalf {
-  const uint32_t* table;   // [K][2^W][2 SP] rows: canonical pair of T_k[d] R mod p_h^2
+  const uint32_t* table;   // [K][2^W] rows of FBGP_ROW4 uint4: canonical pair of T_k[d] R mod p_h^2 (words)
   const uint32_t* p;       // p_h, S limbs
   const uint32_t* X;       // (1 - R) mod p_h, S limbs (R = 2^(28 S))
   const uint32_t* oneR;    // pair of R mod p_h^2 ([A: S][B: S])
@@ -81,6 +83,94 @@ __device__ __forceinline__ void fbgp_regs_to_slot(uint32_t* slot, const uint32_t
   wave_lds_fence();
 }
 
+// ---------------------------------------------------------------- table rows as 32-bit words
+// A row is the canonical pair (A, B) of T_k[d] R as the 32-bit words of A then of B (512 B). The limb-row layout
+// of the first version (74 + 74 28-bit limbs, 592 B) straddled 128-B lines and read 1.21x its bytes from HBM.
+
+// canonical pair (registers) -> the group's slot -> lane t stores words [32 t, 32 t + 32) of the row (16-byte
+// stores). Word w of a component = limbs i, i + 1 (i = 32 w / 28, shift 32 w mod 28 = 4 w mod 28 <= 24). row
+// may be null (the group only takes part in the slot traffic).
+template <int TPI, int LL>
+__device__ __forceinline__ void pair_store_row(uint4* row, uint32_t* slot, const uint32_t (&A)[LL], const uint32_t (&B)[LL],
+                                               int tig) {
+  constexpr int S = TPI * LL;
+  static_assert(TPI * 32 == 2 * FBGP_PW, "one lane per 32 row words");
+  fbgp_regs_to_slot<TPI, LL>(slot, A, B, tig);
+  uint32_t wv[32];
+#pragma unroll
+  for (int q = 0; q < 32; ++q) {
+    const int w = tig * 32 + q;
+    const int comp = w / FBGP_PW, ww = w % FBGP_PW;
+    const int i = (32 * ww) / LB, o = (32 * ww) % LB;
+    const uint32_t* cs = slot + comp * S;
+    wv[q] = (cs[i] >> o) | (cs[i + 1] << (LB - o));
+  }
+  if (row) {
+    row += tig * 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) row[q] = make_uint4(wv[4 * q], wv[4 * q + 1], wv[4 * q + 2], wv[4 * q + 3]);
+  }
+  wave_lds_fence();
+}
+
+// The row's words (registers, prefetched) -> the group's staging words -> limbs in the slot [A: S][B: S].
+// Lane t owns limbs [LL t, LL t + LL) of A and of B: limb i = bits [28 i, 28 i + 28) of its component.
+template <int TPI, int LL>
+__device__ __forceinline__ void pair_row_to_slot(uint32_t* slot, uint32_t* stg, const uint4 (&rw)[8], int tig) {
+  constexpr int S = TPI * LL;
+  wave_lds_fence();
+  uint4* s4 = reinterpret_cast<uint4*>(stg) + tig * 8;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) s4[q] = rw[q];
+  wave_lds_fence();
+  int t = tig;
+  asm volatile("" : "+v"(t));
+#pragma unroll
+  for (int comp = 0; comp < 2; ++comp) {
+    const uint32_t* cw = stg + comp * FBGP_PW;
+#pragma unroll
+    for (int r = 0; r < LL; ++r) {
+      const int i = t * LL + r;
+      const int bit = i * LB, w = bit >> 5, o = bit & 31;
+      uint32_t v = 0;
+      if (i < FBGP_SP) {
+        const uint32_t lo = cw[w];
+        const uint32_t hi = (o > 32 - LB && w + 1 < FBGP_PW) ? cw[w + 1] : 0u;
+        v = ((lo >> o) | (o ? hi << (32 - o) : 0u)) & LMASK;
+      }
+      slot[comp * S + i] = v;
+    }
+  }
+  wave_lds_fence();
+}
+
+// (A, B) <- (A, B) prod_k T_k[dg[k stride]] over K word rows of 2^W entries; each row streams one product ahead
+// (its 512 B are in flight in registers while the previous product runs). stg: the group's 2 PW staging words.
+template <int TPI, int LL>
+__device__ __forceinline__ void pair_table_products(uint32_t (&A)[LL], uint32_t (&B)[LL], const uint4* __restrict__ table,
+                                                    const uint32_t* __restrict__ dg, long long stride, int K, int W,
+                                                    uint32_t* slot, uint32_t* stg, const uint32_t* xs, const uint32_t (&m)[LL],
+                                                    uint32_t mprime, int lane, int tig) {
+  uint4 rw[8];
+  uint32_t dnext = dg[0];
+  {
+    const uint4* r0 = table + (size_t)dnext * FBGP_ROW4 + tig * 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) rw[q] = r0[q];
+    dnext = K > 1 ? dg[(size_t)stride] : 0u;
+  }
+  for (int k = 0; k < K; ++k) {
+    pair_row_to_slot<TPI, LL>(slot, stg, rw, tig);
+    if (k + 1 < K) {
+      const uint4* rn = table + (((size_t)(k + 1) << W) + dnext) * FBGP_ROW4 + tig * 8;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) rw[q] = rn[q];
+      dnext = k + 2 < K ? dg[(size_t)(k + 2) * stride] : 0u;
+    }
+    pgrp::montmul<TPI, LL, false>(A, B, slot, xs, m, mprime, lane, tig);
+  }
+}
+
 template <int TPI, int LL>
 __global__ __launch_bounds__(BLOCK, 2) void k_fbgp(FbgpParams p) {
   constexpr int S = TPI * LL;
@@ -92,13 +182,15 @@ __global__ __launch_bounds__(BLOCK, 2) void k_fbgp(FbgpParams p) {
   const int half = blockIdx.y;
   const FbgpHalf* H = p.halves + half;
   uint32_t* slot = smem + gib * 2 * S;
-  uint32_t* xs = smem + GPB * 2 * S;
+  uint32_t* stg = smem + GPB * 2 * S + gib * 2 * FBGP_PW;
+  uint32_t* xs = smem + GPB * (2 * S + 2 * FBGP_PW);
   for (int i = threadIdx.x; i < S; i += BLOCK) xs[i] = H->X[i];
   __syncthreads();
   uint32_t m[LL];
   fbgp_load<TPI, LL>(H->p, m, tig);
   const uint32_t mprime = H->mprime;
   const int K = p.K, W = p.W;
+  const uint4* table = reinterpret_cast<const uint4*>(H->table);
   for (long long base = (long long)blockIdx.x * GPB; base < p.n; base += (long long)gridDim.x * GPB) {
     const long long inst = base + gib;
     const bool valid = inst < p.n;
@@ -140,10 +232,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_fbgp(FbgpParams p) {
         A[i] = (tig == 0 && i == 0) ? 1u : 0u;
       }
     }
-    for (int k = 0; k < K; ++k) {
-      fbgp_pair_to_slot<TPI, LL>(slot, H->table + (((size_t)k << W) + dg[(size_t)k * p.n]) * 2 * FBGP_SP, FBGP_SP, tig);
-      pgrp::montmul<TPI, LL, false>(A, B, slot, xs, m, mprime, lane, tig);
-    }
+    pair_table_products<TPI, LL>(A, B, table, dg, p.n, K, W, slot, stg, xs, m, mprime, lane, tig);
     pgrp::canon<TPI, LL>(A, B, m, lane, tig);
     if (valid) {
 #pragma unroll
@@ -294,17 +383,8 @@ __global__ __launch_bounds__(BLOCK) void k_fbgp_fill(const FbgpHalf* halves, int
   }
   pgrp::montmul<TPI, LL, false>(A, B, slot, xs, m, H->mprime, lane, tig);
   pgrp::canon<TPI, LL>(A, B, m, lane, tig);
-  if (valid) {
-    uint32_t* row = (half ? table1 : table0) + ((size_t)k * ent + d) * 2 * FBGP_SP;
-#pragma unroll
-    for (int i = 0; i < LL; ++i) {
-      const int idx = tig * LL + i;
-      if (idx < FBGP_SP) {
-        row[idx] = A[i];
-        row[FBGP_SP + idx] = B[i];
-      }
-    }
-  }
+  uint4* t = reinterpret_cast<uint4*>(half ? table1 : table0);
+  pair_store_row<TPI, LL>(valid ? t + ((size_t)k * ent + d) * FBGP_ROW4 : nullptr, slot, A, B, tig);
 }
 
 }  // namespace fpai

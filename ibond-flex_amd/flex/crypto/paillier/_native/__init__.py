@@ -23,10 +23,14 @@ EL_OK, EL_INT, EL_INT_BIG, EL_OVERFLOW, EL_FLOAT_OVF, EL_ENC_RANGE = 0, 1, 2, 3,
 
 PAI_OPT_CRT_ENCRYPT, PAI_OPT_CRT_AVAILABLE, PAI_OPT_STAGE_TIMING, PAI_OPT_LANE_DECRYPT = 1, 2, 3, 4
 PAI_OPT_FIXED_BASE, PAI_OPT_FB_WINDOW, PAI_OPT_FB_READY, PAI_OPT_FB_PAIR, PAI_OPT_PAIR = 5, 6, 7, 8, 9
+PAI_OPT_PUBLIC_FB, PAI_OPT_PFB_READY, PAI_OPT_PFB_WINDOW = 10, 11, 12
+PFB_NBASES = 33
 
 EXPORTED = ("pai_device_count", "pai_device_mem_info", "pai_ctx_create", "pai_ctx_set_private", "pai_ctx_destroy", "pai_ctx_info", "pai_last_error",
             "pai_ctx_set_option", "pai_ctx_get_option", "pai_ctx_stage_times", "pai_ctx_fixed_base_info",
             "pai_ctx_fixed_base_prepare", "pai_ctx_fixed_base_setup", "pai_ctx_fixed_base_policy",
+            "pai_ctx_public_fb_prepare", "pai_ctx_public_fb_set_bases", "pai_ctx_public_fb_info",
+            "pai_ctx_public_fb_policy",
             "pai_encrypt", "pai_add", "pai_decrypt", "pai_encrypt_dev", "pai_add_dev", "pai_decrypt_dev",
             "pai_mul", "pai_mul_dev", "pai_matmul", "pai_matmul_dev", "pai_add_plain", "pai_add_plain_dev",
             "pai_segment_add", "pai_segment_add_dev", "pai_comm_unique_id", "pai_comm_create", "pai_comm_destroy",
@@ -67,6 +71,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.pai_ctx_fixed_base_prepare.argtypes = [P]
         lib.pai_ctx_fixed_base_setup.argtypes = [P, P, P, P]
         lib.pai_ctx_fixed_base_policy.argtypes = [P, P, P]
+        lib.pai_ctx_public_fb_prepare.argtypes = [P]
+        lib.pai_ctx_public_fb_set_bases.argtypes = [P, P, S, I]
+        lib.pai_ctx_public_fb_info.argtypes = [P, P, S, P, P, P, P]
+        lib.pai_ctx_public_fb_policy.argtypes = [P, P, P]
         lib.pai_encrypt.argtypes = [P, I, P, S, I, ctypes.c_int32, I, P, S, S, P, U64, P, P, P]
         lib.pai_add.argtypes = [P, P, P, I, S, P, P]
         lib.pai_decrypt.argtypes = [P, P, P, S, P, P, P, P]
@@ -284,6 +292,47 @@ class Context:
         the fixed-base tables get built (0 once resident or unavailable); include/flexpai.h."""
         seen, thr = ctypes.c_longlong(), ctypes.c_longlong()
         _check(self.lib.pai_ctx_fixed_base_policy(self._h, ctypes.byref(seen), ctypes.byref(thr)))
+        return int(seen.value), int(thr.value)
+
+    # ------------------------------------------------------ public-key fixed bases (kernels_pfb.hpp)
+    @property
+    def public_fixed_base(self) -> bool:
+        """True when device-RNG encryption without the private key may use the public fixed bases."""
+        return bool(self._get_option(PAI_OPT_PUBLIC_FB))
+
+    def set_public_fixed_base(self, enabled: bool):
+        _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_PUBLIC_FB, 1 if enabled else 0))
+
+    @property
+    def pfb_ready(self) -> bool:
+        return bool(self._get_option(PAI_OPT_PFB_READY))
+
+    def set_pfb_window(self, bits: int):
+        _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_PFB_WINDOW, int(bits)))
+
+    def prepare_public_fixed_base(self):
+        _check(self.lib.pai_ctx_public_fb_prepare(self._h))
+
+    def set_public_bases(self, bases: Sequence[int]):
+        """Fix the 33 bases g_0..g_32 (each 1 < g < n) instead of drawing them (tests, reproducible runs)."""
+        nb = (self.n.bit_length() + 7) // 8
+        buf = b"".join(int_to_le(g, nb) for g in bases)
+        _check(self.lib.pai_ctx_public_fb_set_bases(self._h, buf, nb, len(bases)))
+
+    def public_fixed_base_info(self):
+        """(bases, K, W, K0) of the resident public tables."""
+        nb = (self.n.bit_length() + 7) // 8
+        buf = (ctypes.c_uint8 * (nb * PFB_NBASES))()
+        nbs, k, w, k0 = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(self.lib.pai_ctx_public_fb_info(self._h, buf, nb, ctypes.byref(nbs), ctypes.byref(k), ctypes.byref(w),
+                                               ctypes.byref(k0)))
+        raw = bytes(buf)
+        bases = [int.from_bytes(raw[j * nb:(j + 1) * nb], "little") for j in range(nbs.value)]
+        return bases, k.value, w.value, k0.value
+
+    def public_fixed_base_policy(self):
+        seen, thr = ctypes.c_longlong(), ctypes.c_longlong()
+        _check(self.lib.pai_ctx_public_fb_policy(self._h, ctypes.byref(seen), ctypes.byref(thr)))
         return int(seen.value), int(thr.value)
 
     def close(self):

@@ -105,6 +105,13 @@ typedef struct pai_comm pai_comm;
                                     public-key encryption (2048-bit n) run on p-adic pairs (kernels_pair.hpp,
                                     kernels_dec4.hpp, kernels_pe.hpp: the default; $FLEXPAI_PAIR=0 at context
                                     creation selects the kernels they replace)                                */
+#define PAI_OPT_PUBLIC_FB 10     /* 1 (default): PAI_OBF_RNG encryption WITHOUT the private key (2048-bit n) samples
+                                  * r^n through the public fixed bases (kernels_pfb.hpp) once the break-even count
+                                  * is reached (pai_ctx_public_fb_policy); get: 1 when the path is enabled and not
+                                  * known unavailable                                                          */
+#define PAI_OPT_PFB_READY 11     /* read-only: 1 when the public fixed-base tables are resident               */
+#define PAI_OPT_PFB_WINDOW 12    /* digit window of the public tables (as PAI_OPT_FB_WINDOW; default 16:
+                                  * 324 rows of 512 B per element, 10.9 GB of tables)                        */
 
 /* Number of visible GPUs (0 when there is none or the runtime cannot start). */
 int pai_device_count(int* count);
@@ -146,6 +153,24 @@ int pai_ctx_fixed_base_setup(const pai_ctx* ctx, float* host_ms, float* device_m
  * once the tables are resident or known unavailable. Replaces nothing in the reference (its obfuscator,
  * obfuscator.py:23-37, has no per-key state); protects re-keying callers (he_sa_ft/train.py:39-40).  */
 int pai_ctx_fixed_base_policy(pai_ctx* ctx, long long* seen, long long* threshold);
+
+/* Public-key fixed bases (DESIGN.md §3 "Fixed bases without the private key"; replaces, for a party holding
+ * only n, the per-element gmpy2.powmod(r, n, n^2) of obfuscator.py:35-36). The context draws 33 bases
+ * g_0..g_32 in [2, n) from the OS CSPRNG (g_0 with Jacobi symbol (g_0 | n) = -1); element i's obfuscator is
+ * r = prod_j g_j^e_j mod n with the exponents read from its ChaCha20 stream (rng_key, counter 0.., nonce =
+ * (index lo, index hi, 0x70666230)) cut into W-bit digits: digits [0, K0) are e_0 (K0 = ceil((nb + 64) / W)),
+ * then 32 runs of KS = ceil(96 / W) digits are e_1..e_32, each little-endian. The ciphertext is the
+ * reference's encryption of x under that r.                                                            */
+int pai_ctx_public_fb_prepare(pai_ctx* ctx);
+/* Use these bases (nbases = 33, each base_bytes little-endian, 1 < g < n) instead of random ones; drops
+ * resident public tables (rebuilt lazily). For reproducible runs and the parity tests.                  */
+int pai_ctx_public_fb_set_bases(pai_ctx* ctx, const uint8_t* bases_le, size_t base_bytes, int nbases);
+/* The resident public tables' bases (nbases x base_bytes, nullable), digit count K, window W, and K0.
+ * PAI_ERR_KEY when the tables are not resident.                                                        */
+int pai_ctx_public_fb_info(pai_ctx* ctx, uint8_t* bases_le, size_t base_bytes, int* nbases, int* digits,
+                           int* window, int* e0_digits);
+/* Break-even of the public tables, like pai_ctx_fixed_base_policy ($FLEXPAI_PFB_MIN_ELEMS overrides).  */
+int pai_ctx_public_fb_policy(pai_ctx* ctx, long long* seen, long long* threshold);
 
 /* Encrypt N plaintexts. dtype PAI_F32/F64/I64. obf_mode PAI_OBF_*.
  *   r_le:      PAI_OBF_GIVEN only: r values as little-endian byte strings of r_bytes each, element i

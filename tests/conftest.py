@@ -33,3 +33,10 @@ def golden_fb():
     import json
     with open(os.path.join(ROOT, "tests", "golden", "paillier_golden_fb.json")) as f:
         return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def golden_pfb():
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "paillier_golden_pfb.json")) as f:
+        return json.load(f)

@@ -43,7 +43,7 @@ def test_fixed_base_4096_params(ctx4096):
     assert (gp, gq) == (O.fb_base(key.p), O.fb_base(key.q))
     assert W == 12 and K == O.fb_digits(key.p, key.q, W)
     _, _, nbytes = ctx.fixed_base_setup()
-    assert nbytes == 2 * K * (1 << W) * 148 * 4          # rows of 148 canonical 28-bit limbs
+    assert nbytes == 2 * K * (1 << W) * 128 * 4          # rows: the canonical pair as 2 x 64 32-bit words
 
 
 @pytest.mark.parametrize("window", [12, 16, 21])

@@ -255,6 +255,9 @@ def main():
                          "whose tables fit the free HBM (nb = 2048: W = 23, 45 pair products per half, 2 x 96.6 GB; "
                          "nb = 4096: W = 21, 98 products per half, 2 x 121.7 GB). With the pair sampler W = 23 "
                          "measured 1.8 %% faster than 22 (profiles/r02_window_sweep_pair.txt)")
+    ap.add_argument("--pfb-window", type=int, default=20, choices=(8, 12, 16, 20),
+                    help="digit window of the public-key fixed-base leg (W = 20: 266 row products per element, "
+                         "139 GB of tables; the library default is 16)")
     ap.add_argument("--cpu-sample", type=int, default=16384)
     ap.add_argument("--cpu-threads", type=int, default=os.cpu_count() or 1,
                     help="threads of the GMP CPU baseline (default os.cpu_count(), like the reference's Pool)")
@@ -678,50 +681,7 @@ def main():
         if not same:
             raise SystemExit("CRT and public-key ciphertexts differ")
 
-    # ---- a party holding ONLY the public key (HE_OTP_LR / HE_LR_FP hosts): public fixed bases (kernels_pfb.hpp)
     pfb_check = None
-    if not args.no_public and solo and nb == 2048:
-        cpub = _native.Context(pk.n, local_rank)
-        t1 = time.perf_counter()
-        cpub.prepare_public_fixed_base()
-        pfb_setup_ms = (time.perf_counter() - t1) * 1e3
-        cpub.set_stage_timing(True)
-        ct3 = torch.empty_like(ct)
-        ex3 = torch.empty_like(ex)
-        runs = []
-        for _ in range(3):
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            rc = lib.pai_encrypt_dev(cpub.handle, _native.PAI_F32, x.data_ptr(), N, 0, 0, _native.PAI_OBF_RNG, None, 0, 0,
-                                     rng_key, index_base_chk, ct3.data_ptr(), ex3.data_ptr(), st.data_ptr(),
-                                     stream.cuda_stream)
-            if rc != 0:
-                raise RuntimeError(lib.pai_last_error().decode())
-            torch.cuda.synchronize()
-            runs.append((time.perf_counter() - t1, cpub.stage_times()))
-        wall, pst = min(runs, key=lambda r: r[0])
-        bases, Kp, Wp, K0p = cpub.public_fixed_base_info()
-        wpfb = float(Kp * _Mp(nb // 32))            # K pair products mod n^2 over the nb/32 32-bit limbs of n
-        # exact round trip through the key holder's decryption
-        valp = torch.empty(N, dtype=torch.float64, device=dev)
-        stp = torch.empty(N, dtype=torch.int32, device=dev)
-        decrypt(ct3, ex3, valp, stp)
-        torch.cuda.synchronize()
-        okp = bool(torch.equal(valp, x.double())) and int((stp > 1).sum().item()) == 0
-        extra["public_key_fixed_base"] = {
-            "value": N / wall, "unit": "encrypts/s per GPU", "elements": N,
-            "kernel": "k_pfb_digits + k_pfb + k_pe_fin", "stages_ms": dict(zip(["k_pfb_digits", "k_pfb", "k_pe_fin"], pst)),
-            "k_pfb_int_mac_frac": N * wpfb / (pst[1] * 1e-3) / INT_MAC_PEAK if len(pst) > 1 else None,
-            "work_mac_per_elem": wpfb, "digits": Kp, "window": Wp, "e0_digits": K0p,
-            "setup_ms": pfb_setup_ms, "table_bytes": Kp * (1 << Wp) * 512,
-            "roundtrip_exact": okp,
-            "note": "a public-key-only context: r = prod_j g_j^e_j mod n over 33 self-drawn bases (DESIGN.md §3), "
-                    "r^n as K table-row products; ciphertexts are the reference's encryption under that r"}
-        pfb_check = (bases, Wp, ct3[:4].cpu().numpy().view(np.uint32).copy(), ex3[:4].cpu().numpy().copy())
-        del ct3, ex3, valp, stp, cpub
-        torch.cuda.empty_cache()
-        if not okp:
-            raise SystemExit("public fixed-base ciphertexts do not decrypt to the input")
 
     # ---- configs[2] beside configs[1]: encrypt 8 arrays, one 8-way add (k_add), decrypt the sum
     if cfg_id == 1 and solo and not args.no_add8 and not args.no_decrypt:
@@ -819,6 +779,55 @@ def main():
         del buf, back, wire
         hb["host_vs_device"] = hb["host_buffers_encrypts_per_s"] / value
         extra["host_boundary"] = hb
+
+    # ---- a party holding ONLY the public key (HE_OTP_LR / HE_LR_FP hosts): public fixed bases (kernels_pfb.hpp)
+    if not args.no_public and solo and nb == 2048:
+        # the key holder's tables (2 x 96.6 GB at W = 23) make room for the public ones (W = 20: 139 GB); nothing
+        # after this leg encrypts with the key holder's context
+        ctx.set_fb_window(16)
+        torch.cuda.synchronize()
+        cpub = _native.Context(pk.n, local_rank)
+        cpub.set_pfb_window(args.pfb_window)
+        t1 = time.perf_counter()
+        cpub.prepare_public_fixed_base()
+        pfb_setup_ms = (time.perf_counter() - t1) * 1e3
+        cpub.set_stage_timing(True)
+        ct3 = torch.empty_like(ct)
+        ex3 = torch.empty_like(ex)
+        runs = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            rc = lib.pai_encrypt_dev(cpub.handle, _native.PAI_F32, x.data_ptr(), N, 0, 0, _native.PAI_OBF_RNG, None, 0, 0,
+                                     rng_key, index_base_chk, ct3.data_ptr(), ex3.data_ptr(), st.data_ptr(),
+                                     stream.cuda_stream)
+            if rc != 0:
+                raise RuntimeError(lib.pai_last_error().decode())
+            torch.cuda.synchronize()
+            runs.append((time.perf_counter() - t1, cpub.stage_times()))
+        wall, pst = min(runs, key=lambda r: r[0])
+        bases, Kp, Wp, K0p = cpub.public_fixed_base_info()
+        wpfb = float(Kp * _Mp(nb // 32))            # K pair products mod n^2 over the nb/32 32-bit limbs of n
+        # exact round trip through the key holder's decryption
+        valp = torch.empty(N, dtype=torch.float64, device=dev)
+        stp = torch.empty(N, dtype=torch.int32, device=dev)
+        decrypt(ct3, ex3, valp, stp)
+        torch.cuda.synchronize()
+        okp = bool(torch.equal(valp, x.double())) and int((stp > 1).sum().item()) == 0
+        extra["public_key_fixed_base"] = {
+            "value": N / wall, "unit": "encrypts/s per GPU", "elements": N,
+            "kernel": "k_pfb_digits + k_pfb + k_pe_fin", "stages_ms": dict(zip(["k_pfb_digits", "k_pfb", "k_pe_fin"], pst)),
+            "k_pfb_int_mac_frac": N * wpfb / (pst[1] * 1e-3) / INT_MAC_PEAK if len(pst) > 1 else None,
+            "work_mac_per_elem": wpfb, "digits": Kp, "window": Wp, "e0_digits": K0p,
+            "setup_ms": pfb_setup_ms, "table_bytes": Kp * (1 << Wp) * 512,
+            "roundtrip_exact": okp,
+            "note": "a public-key-only context: r = prod_j g_j^e_j mod n over 33 self-drawn bases (DESIGN.md §3), "
+                    "r^n as K table-row products; ciphertexts are the reference's encryption under that r"}
+        pfb_check = (bases, Wp, ct3[:4].cpu().numpy().view(np.uint32).copy(), ex3[:4].cpu().numpy().copy())
+        del ct3, ex3, valp, stp, cpub
+        torch.cuda.empty_cache()
+        if not okp:
+            raise SystemExit("public fixed-base ciphertexts do not decrypt to the input")
 
     if rank != 0:
         if world > 1:

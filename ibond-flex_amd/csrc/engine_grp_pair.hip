@@ -4,7 +4,7 @@
 namespace fpai {
 
 static size_t pg_lds() { return ((size_t)(BLOCK / FBGP_TPI) * 2 * FBGP_S + FBGP_S) * 4; }
-static size_t main_lds() { return ((size_t)(BLOCK / FBGP_TPI) * (2 * FBGP_S + 2 * FBGP_PW) + FBGP_S) * 4; }   // + row staging
+static size_t main_lds() { return pg_lds(); }   // + the static row staging (pair_table_products)
 static size_t w_lds() { return (size_t)(BLOCK / 4) * 4 * L * 4; }
 
 int fbgp_occupancy(int* occ) {

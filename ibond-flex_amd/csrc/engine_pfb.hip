@@ -4,7 +4,7 @@
 namespace fpai {
 
 static size_t pg_lds() { return ((size_t)(BLOCK / PFB_TPI) * 2 * PFB_S + PFB_S) * 4; }
-static size_t main_lds() { return ((size_t)(BLOCK / PFB_TPI) * (2 * PFB_S + 2 * PFB_PW) + PFB_S) * 4; }
+static size_t main_lds() { return pg_lds(); }   // + the static row staging (kernels_grp_pair.hpp)
 
 int pfb_occupancy(int* occ) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, k_pfb<PFB_TPI, PFB_LL>, BLOCK, main_lds()) != hipSuccess ||

@@ -113,59 +113,86 @@ __device__ __forceinline__ void pair_store_row(uint4* row, uint32_t* slot, const
   wave_lds_fence();
 }
 
-// The row's words (registers, prefetched) -> the group's staging words -> limbs in the slot [A: S][B: S].
-// Lane t owns limbs [LL t, LL t + LL) of A and of B: limb i = bits [28 i, 28 i + 28) of its component.
-template <int TPI, int LL>
-__device__ __forceinline__ void pair_row_to_slot(uint32_t* slot, uint32_t* stg, const uint4 (&rw)[8], int tig) {
-  constexpr int S = TPI * LL;
-  wave_lds_fence();
-  uint4* s4 = reinterpret_cast<uint4*>(stg) + tig * 8;
+// ---- rows stream HBM -> LDS by DMA, one product ahead, without registers
+// A wave holds 16 groups; one global_load_lds writes 16 B per lane at M0 + 16 lane, i.e. 1 KB: lanes 0-31 fetch
+// the 512-B row of group 2q, lanes 32-63 that of group 2q + 1, so eight instructions land the wave's 16 rows
+// contiguously (group g's row at wave_stage + 512 g). The row index of a group comes from its lane 0 by
+// readlane. The staging array is its own __shared__ object: the compiler then does not order the product's
+// slot reads behind the DMA in flight (they cannot alias), so the row of product k+1 streams in during k.
+constexpr int FBGP_STAGE_WORDS = 16 * 2 * FBGP_PW + 4;   // per wave (+4: the conversion's last read past a row)
+
+__device__ __forceinline__ void pair_rows_dma(const uint4* __restrict__ table, size_t k, int W, uint32_t d,
+                                              const uint32_t* wave_stage, int lane) {
+  typedef __attribute__((address_space(3))) uint32_t lds_u32;
+  const uint32_t lb = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds_u32*)wave_stage);
+  const size_t kb = k << W;
+  const int hi = lane >> 5, col = lane & 31;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) s4[q] = rw[q];
-  wave_lds_fence();
-  int t = tig;
-  asm volatile("" : "+v"(t));
-#pragma unroll
-  for (int comp = 0; comp < 2; ++comp) {
-    const uint32_t* cw = stg + comp * FBGP_PW;
-#pragma unroll
-    for (int r = 0; r < LL; ++r) {
-      const int i = t * LL + r;
-      const int bit = i * LB, w = bit >> 5, o = bit & 31;
-      uint32_t v = 0;
-      if (i < FBGP_SP) {
-        const uint32_t lo = cw[w];
-        const uint32_t hi = (o > 32 - LB && w + 1 < FBGP_PW) ? cw[w + 1] : 0u;
-        v = ((lo >> o) | (o ? hi << (32 - o) : 0u)) & LMASK;
-      }
-      slot[comp * S + i] = v;
-    }
+  for (int q = 0; q < 8; ++q) {
+    const uint32_t d0 = __builtin_amdgcn_readlane(d, 8 * q), d1 = __builtin_amdgcn_readlane(d, 8 * q + 4);
+    const uint4* src = table + (kb + (hi ? d1 : d0)) * FBGP_ROW4 + col;
+    uint32_t dst = lb + (uint32_t)(q * 1024);
+    asm volatile("" : "+s"(dst));
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(size_t)dst, 16, 0, 0);
   }
-  wave_lds_fence();
 }
 
-// (A, B) <- (A, B) prod_k T_k[dg[k stride]] over K word rows of 2^W entries; each row streams one product ahead
-// (its 512 B are in flight in registers while the previous product runs). stg: the group's 2 PW staging words.
+// The group's staged row (contiguous words) -> limbs in the slot [A: S][B: S]. Lane t owns limbs [LL t, LL t + LL)
+// of each component, i.e. bits from 28 LL t: it reads the 18 words from word (28 LL t) / 32, shifts them down by
+// (28 LL t) mod 32 (one funnel shift per word, the lane's own amount) and cuts 28-bit limbs at compile-time
+// offsets. Limbs >= FBGP_SP are zero.
+template <int TPI, int LL>
+__device__ __forceinline__ void pair_stage_to_slot(uint32_t* slot, const uint32_t* row, int tig) {
+  constexpr int S = TPI * LL;
+  constexpr int NW = (LB * LL + 31) / 32 + 1;   // 18 words cover a lane's 19 limbs at any bit offset
+  static_assert(LL == 19 && NW == 18, "geometry");
+  const uint32_t bit0 = (uint32_t)(LB * LL) * (uint32_t)tig;
+  const uint32_t w0 = bit0 >> 5, sh = bit0 & 31u;
+#pragma unroll
+  for (int comp = 0; comp < 2; ++comp) {
+    const uint32_t* src = row + comp * FBGP_PW + w0;
+    uint32_t v[NW];
+#pragma unroll
+    for (int k = 0; k < NW; ++k) v[k] = src[k];
+    uint32_t u[NW - 1];
+#pragma unroll
+    for (int k = 0; k + 1 < NW; ++k) u[k] = __builtin_amdgcn_alignbit(v[k + 1], v[k], sh);
+    uint32_t* dst = slot + comp * S + tig * LL;
+#pragma unroll
+    for (int r = 0; r < LL; ++r) {
+      const int b = LB * r, w = b >> 5, o = b & 31;
+      const uint32_t lo = u[w], hi = (w + 1 < NW - 1) ? u[w + 1] : 0u;
+      uint32_t limb = __builtin_amdgcn_alignbit(hi, lo, (uint32_t)o) & LMASK;
+      if (r + (TPI - 1) * LL >= 32 * FBGP_PW / LB) {
+        // limbs at or past bit 32 PW of the component: keep only its own bits (the words read past the component
+        // are the other component's, or the next row's)
+        const int lim = 32 * FBGP_PW - LB * (tig * LL + r);
+        limb = lim >= LB ? limb : lim > 0 ? (limb & ((1u << lim) - 1u)) : 0u;
+      }
+      dst[r] = limb;
+    }
+  }
+}
+
+// (A, B) <- (A, B) prod_k T_k[dg[k stride]] over K word rows of 2^W entries; row k+1 streams in by DMA during
+// product k. wave_stage: this wave's FBGP_STAGE_WORDS words (its own __shared__ object).
 template <int TPI, int LL>
 __device__ __forceinline__ void pair_table_products(uint32_t (&A)[LL], uint32_t (&B)[LL], const uint4* __restrict__ table,
                                                     const uint32_t* __restrict__ dg, long long stride, int K, int W,
-                                                    uint32_t* slot, uint32_t* stg, const uint32_t* xs, const uint32_t (&m)[LL],
-                                                    uint32_t mprime, int lane, int tig) {
-  uint4 rw[8];
-  uint32_t dnext = dg[0];
-  {
-    const uint4* r0 = table + (size_t)dnext * FBGP_ROW4 + tig * 8;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) rw[q] = r0[q];
-    dnext = K > 1 ? dg[(size_t)stride] : 0u;
-  }
+                                                    uint32_t* slot, const uint32_t* wave_stage, const uint32_t* xs,
+                                                    const uint32_t (&m)[LL], uint32_t mprime, int lane, int tig) {
+  const uint32_t* row = wave_stage + (lane / TPI) * 2 * FBGP_PW;
+  pair_rows_dma(table, 0, W, dg[0], wave_stage, lane);
+  uint32_t dn = K > 1 ? dg[(size_t)stride] : 0u;
   for (int k = 0; k < K; ++k) {
-    pair_row_to_slot<TPI, LL>(slot, stg, rw, tig);
+    lds_dma_wait();                                   // row k landed, digit k+1 loaded
+    wave_lds_fence();
+    pair_stage_to_slot<TPI, LL>(slot, row, tig);
+    wave_lds_fence();
     if (k + 1 < K) {
-      const uint4* rn = table + (((size_t)(k + 1) << W) + dnext) * FBGP_ROW4 + tig * 8;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) rw[q] = rn[q];
-      dnext = k + 2 < K ? dg[(size_t)(k + 2) * stride] : 0u;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the staged row is consumed before it is overwritten
+      pair_rows_dma(table, (size_t)(k + 1), W, dn, wave_stage, lane);
+      dn = k + 2 < K ? dg[(size_t)(k + 2) * stride] : 0u;
     }
     pgrp::montmul<TPI, LL, false>(A, B, slot, xs, m, mprime, lane, tig);
   }
@@ -181,9 +208,10 @@ __global__ __launch_bounds__(BLOCK, 2) void k_fbgp(FbgpParams p) {
   const int gib = threadIdx.x / TPI;
   const int half = blockIdx.y;
   const FbgpHalf* H = p.halves + half;
+  __shared__ __attribute__((aligned(16))) uint32_t stage[(BLOCK / 64) * FBGP_STAGE_WORDS];
   uint32_t* slot = smem + gib * 2 * S;
-  uint32_t* stg = smem + GPB * 2 * S + gib * 2 * FBGP_PW;
-  uint32_t* xs = smem + GPB * (2 * S + 2 * FBGP_PW);
+  const uint32_t* wstage = stage + (threadIdx.x / 64) * FBGP_STAGE_WORDS;
+  uint32_t* xs = smem + GPB * 2 * S;
   for (int i = threadIdx.x; i < S; i += BLOCK) xs[i] = H->X[i];
   __syncthreads();
   uint32_t m[LL];
@@ -232,7 +260,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_fbgp(FbgpParams p) {
         A[i] = (tig == 0 && i == 0) ? 1u : 0u;
       }
     }
-    pair_table_products<TPI, LL>(A, B, table, dg, p.n, K, W, slot, stg, xs, m, mprime, lane, tig);
+    pair_table_products<TPI, LL>(A, B, table, dg, p.n, K, W, slot, wstage, xs, m, mprime, lane, tig);
     pgrp::canon<TPI, LL>(A, B, m, lane, tig);
     if (valid) {
 #pragma unroll

@@ -224,9 +224,10 @@ __global__ __launch_bounds__(BLOCK, 2) void k_pfb(PfbParams p) {
   const int gib = threadIdx.x / TPI;
   const PfbConst* C = p.c;
   const FbgpHalf* H = &C->g;
+  __shared__ __attribute__((aligned(16))) uint32_t stage[(BLOCK / 64) * FBGP_STAGE_WORDS];
   uint32_t* slot = smem + gib * 2 * S;
-  uint32_t* stg = smem + GPB * 2 * S + gib * 2 * PFB_PW;
-  uint32_t* xs = smem + GPB * (2 * S + 2 * PFB_PW);
+  const uint32_t* wstage = stage + (threadIdx.x / 64) * FBGP_STAGE_WORDS;
+  uint32_t* xs = smem + GPB * 2 * S;
   for (int i = threadIdx.x; i < S; i += BLOCK) xs[i] = H->X[i];
   __syncthreads();
   uint32_t m[LL];
@@ -265,7 +266,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_pfb(PfbParams p) {
 #pragma unroll
       for (int i = 0; i < LL; ++i) B[i] = neg ? D[i] : ml[i];
     }
-    pair_table_products<TPI, LL>(A, B, table, dg, p.n, K, W, slot, stg, xs, m, mprime, lane, tig);
+    pair_table_products<TPI, LL>(A, B, table, dg, p.n, K, W, slot, wstage, xs, m, mprime, lane, tig);
     pgrp::canon<TPI, LL>(A, B, m, lane, tig);
     if (valid) {
 #pragma unroll

@@ -107,15 +107,16 @@ __device__ __forceinline__ void cond_sub(uint32_t (&r)[LL], const uint32_t (&m)[
   }
 }
 
-template <int TPI, int LL, bool SQR, int S_>
+template <int TPI, int LL, bool SQR, bool B2Z, int S_>
 __device__ __forceinline__ void step(uint64_t (&P1)[LL], uint64_t (&P2)[LL], const uint32_t (&A)[LL], const uint32_t (&B)[LL],
                                      const uint32_t* __restrict__ Ao, const uint32_t* __restrict__ Bo, uint32_t& acur,
                                      uint32_t& bcur, const uint32_t (&m)[LL], uint32_t mprime, int tig) {
   const uint32_t aj = acur, bj = bcur;
   if constexpr (S_ + 1 < LL) {
     acur = Ao[S_ + 1];
-    bcur = Bo[S_ + 1];
+    if constexpr (SQR || !B2Z) bcur = Bo[S_ + 1];
   }
+  (void)bj;
   if constexpr (SQR) {
     const uint32_t bj2 = bj << 1;
 #pragma unroll
@@ -128,8 +129,10 @@ __device__ __forceinline__ void step(uint64_t (&P1)[LL], uint64_t (&P2)[LL], con
     for (int i = 0; i < LL; ++i) {
       P1[(i + S_) % LL] += (uint64_t)A[i] * aj;
       P2[(i + S_) % LL] += (uint64_t)B[i] * aj;
-      asm volatile("" : "+v"(P2[(i + S_) % LL]));   // keeps both products accumulating MACs (LLVM would
-      P2[(i + S_) % LL] += (uint64_t)A[i] * bj;      // otherwise sum them first and add: 3 instructions)
+      if constexpr (!B2Z) {
+        asm volatile("" : "+v"(P2[(i + S_) % LL]));   // keeps both products accumulating MACs (LLVM would
+        P2[(i + S_) % LL] += (uint64_t)A[i] * bj;      // otherwise sum them first and add: 3 instructions)
+      }
     }
   }
   const uint32_t q1 = bcast0<TPI>(((uint32_t)P1[S_] * mprime) & LMASK);
@@ -150,17 +153,18 @@ __device__ __forceinline__ void step(uint64_t (&P1)[LL], uint64_t (&P2)[LL], con
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int TPI, int LL, bool SQR, int... Ss>
+template <int TPI, int LL, bool SQR, bool B2Z, int... Ss>
 __device__ __forceinline__ void outer(uint64_t (&P1)[LL], uint64_t (&P2)[LL], const uint32_t (&A)[LL], const uint32_t (&B)[LL],
                                       const uint32_t* __restrict__ Ao, const uint32_t* __restrict__ Bo, const uint32_t (&m)[LL],
                                       uint32_t mprime, int tig, std::integer_sequence<int, Ss...>) {
-  uint32_t acur = Ao[0], bcur = Bo[0];
-  (step<TPI, LL, SQR, Ss>(P1, P2, A, B, Ao, Bo, acur, bcur, m, mprime, tig), ...);
+  uint32_t acur = Ao[0], bcur = (SQR || !B2Z) ? Bo[0] : 0u;
+  (step<TPI, LL, SQR, B2Z, Ss>(P1, P2, A, B, Ao, Bo, acur, bcur, m, mprime, tig), ...);
 }
 
 // (A, B) <- (A, B) (A2, B2) R^-1, (A2, B2) in the group's LDS slot [A2: S][B2: S] (SQR: the slot holds (A, B)
-// itself); xs: (1 - R) mod p in LDS (S limbs)
-template <int TPI, int LL, bool SQR>
+// itself); xs: (1 - R) mod p in LDS (S limbs). B2Z: the multiplier is (A2, 0) (its B half is not read): the B row
+// drops the A B2 term, 4 S^2 lane-MACs instead of 5 S^2 (factored table rows, kernels_grp_pair.hpp).
+template <int TPI, int LL, bool SQR, bool B2Z = false>
 __device__ __forceinline__ void montmul(uint32_t (&A)[LL], uint32_t (&B)[LL], const uint32_t* slot, const uint32_t* xs,
                                         const uint32_t (&m)[LL], uint32_t mprime, int lane, int tig) {
   constexpr int S = TPI * LL;
@@ -171,9 +175,44 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[LL], uint32_t (&B)[LL], co
     P2[i] = xs[tig * LL + i];
   }
   for (int o = 0; o < TPI; ++o)
-    outer<TPI, LL, SQR>(P1, P2, A, B, slot + o * LL, slot + S + o * LL, m, mprime, tig, std::make_integer_sequence<int, LL>{});
+    outer<TPI, LL, SQR, B2Z>(P1, P2, A, B, slot + o * LL, slot + S + o * LL, m, mprime, tig, std::make_integer_sequence<int, LL>{});
   normalize<TPI, LL>(P1, A, lane, tig);
   normalize<TPI, LL>(P2, B, lane, tig);
+}
+
+// ---- single-row Montgomery products mod p on the group (table construction and the final correction)
+template <int TPI, int LL, int S_>
+__device__ __forceinline__ void step1(uint64_t (&P)[LL], const uint32_t (&A)[LL], const uint32_t* __restrict__ Ao, uint32_t& acur,
+                                      const uint32_t (&m)[LL], uint32_t mprime) {
+  const uint32_t aj = acur;
+  if constexpr (S_ + 1 < LL) acur = Ao[S_ + 1];
+#pragma unroll
+  for (int i = 0; i < LL; ++i) P[(i + S_) % LL] += (uint64_t)A[i] * aj;
+  const uint32_t q = bcast0<TPI>(((uint32_t)P[S_] * mprime) & LMASK);
+#pragma unroll
+  for (int i = 0; i < LL; ++i) P[(i + S_) % LL] += (uint64_t)q * m[i];
+  const uint64_t v = P[S_];
+  P[(S_ + 1) % LL] += v >> LB;
+  P[S_] = (uint64_t)dpp_from_next((uint32_t)v & LMASK);
+#pragma unroll
+  for (int i = 0; i < LL; ++i) asm volatile("" : "+v"(P[i]));
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int TPI, int LL, int... Ss>
+__device__ __forceinline__ void outer1(uint64_t (&P)[LL], const uint32_t (&A)[LL], const uint32_t* __restrict__ Ao,
+                                       const uint32_t (&m)[LL], uint32_t mprime, std::integer_sequence<int, Ss...>) {
+  uint32_t acur = Ao[0];
+  (step1<TPI, LL, Ss>(P, A, Ao, acur, m, mprime), ...);
+}
+// A <- A X R^-1 mod p (< 2p for A, X < 2p), X = the S limbs at `slot`
+template <int TPI, int LL>
+__device__ __forceinline__ void montmul1(uint32_t (&A)[LL], const uint32_t* slot, const uint32_t (&m)[LL], uint32_t mprime,
+                                         int lane, int tig) {
+  uint64_t P[LL];
+#pragma unroll
+  for (int i = 0; i < LL; ++i) P[i] = 0;
+  for (int o = 0; o < TPI; ++o) outer1<TPI, LL>(P, A, slot + o * LL, m, mprime, std::make_integer_sequence<int, LL>{});
+  normalize<TPI, LL>(P, A, lane, tig);
 }
 
 // canonical pair: A - p + p (B + 1) == A + p B; then B mod p (B <= 2p)

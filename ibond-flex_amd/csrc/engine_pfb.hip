@@ -13,7 +13,7 @@ int pfb_occupancy(int* occ) {
   return 0;
 }
 
-hipError_t pfb_build_tables(const PfbConst* d_c, int nbases, int K, int W, uint4* table, hipStream_t st) {
+hipError_t pfb_build_phase1(const PfbConst* d_c, int nbases, int K, int W, hipStream_t st) {
   constexpr int GPB = BLOCK / PFB_TPI;
   hipLaunchKernelGGL((k_pfb_chain<PFB_TPI, PFB_LL>), dim3((nbases + GPB - 1) / GPB), dim3(BLOCK), pg_lds(), st, d_c);
   hipError_t e = hipGetLastError();
@@ -24,6 +24,17 @@ hipError_t pfb_build_tables(const PfbConst* d_c, int nbases, int K, int W, uint4
   hipLaunchKernelGGL((k_fbgp_lohi<PFB_TPI, PFB_LL>), dim3((nent + GPB - 1) / GPB, K, 1), dim3(BLOCK), pg_lds(), st,
                      &d_c->g, K, W);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL((k_pair_inv_fwd<PFB_TPI, PFB_LL>), dim3((2 * K + GPB - 1) / GPB, 1), dim3(BLOCK),
+                     (size_t)GPB * PFB_S * 4, st, &d_c->g, K, W);
+  return hipGetLastError();
+}
+
+hipError_t pfb_build_phase2(const PfbConst* d_c, int K, int W, uint4* table, hipStream_t st) {
+  constexpr int GPB = BLOCK / PFB_TPI;
+  hipLaunchKernelGGL((k_pair_inv_bwd<PFB_TPI, PFB_LL>), dim3((2 * K + GPB - 1) / GPB, 1), dim3(BLOCK),
+                     (size_t)GPB * PFB_S * 4, st, &d_c->g, K, W);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_pfb_fill<PFB_TPI, PFB_LL>), dim3(((1 << W) + GPB - 1) / GPB, K), dim3(BLOCK), pg_lds(), st,
                      d_c, K, W, table);
   return hipGetLastError();

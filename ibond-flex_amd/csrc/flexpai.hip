@@ -650,6 +650,49 @@ static int fb_unavailable(pai_ctx* c, const std::string& why) {
   return 0;
 }
 
+// 28-bit limbs (device) -> HBig
+static HBig from_limbs(const uint32_t* l, int nl) {
+  HBig r;
+  r.w.assign(((size_t)nl * LB + 31) / 32 + 2, 0);
+  for (int i = 0; i < nl; ++i) {
+    const size_t bit = (size_t)LB * i;
+    const uint64_t v = (uint64_t)l[i] << (bit % 32);
+    r.w[bit / 32] |= (uint32_t)v;
+    r.w[bit / 32 + 1] |= (uint32_t)(v >> 32);
+  }
+  r.trim();
+  return r;
+}
+
+// The host step of the factored rows' batch inversion (kernels_grp_pair.hpp): the nv chain products v_i
+// (R-forms, < 2m, S limbs each at d_cval) -> v_i^-1 R_dev^2 mod m, R_dev = 2^(28 S), in place. Montgomery's
+// trick over the nv values and one binary extended-Euclid inversion: m may be composite (n).
+static int pair_host_invert(const HBig& m, uint32_t* d_cval, int nv, int S) {
+  std::vector<uint32_t> buf((size_t)nv * S);
+  HIPCHK(hipMemcpy(buf.data(), d_cval, buf.size() * 4, hipMemcpyDeviceToHost));
+  HMont M(m);
+  std::vector<HBig> xm(nv), pre(nv);
+  for (int i = 0; i < nv; ++i) {
+    HBig v = from_limbs(&buf[(size_t)i * S], S);
+    while (cmp(v, m) >= 0) v = sub(v, m);
+    if (v.is_zero()) return fail(PAI_ERR_KEY, "table construction: a zero chain product");
+    xm[i] = M.mul(v, M.r2);                       // host Montgomery form
+    pre[i] = i ? M.mul(pre[i - 1], xm[i]) : xm[i];
+  }
+  const HBig ti = inv_mod(M.from(pre[nv - 1]), m);
+  if (ti.is_zero()) return fail(PAI_ERR_KEY, "table construction: a chain product is not invertible");
+  const HBig rdm = M.mul(mul_pow2_mod(HBig(1), 2 * (size_t)LB * S, m), M.r2);   // R_dev^2, host Montgomery form
+  HBig I = M.mul(ti, M.r2);
+  for (int i = nv - 1; i >= 0; --i) {
+    const HBig inv = i ? M.mul(I, pre[i - 1]) : I;
+    if (i) I = M.mul(I, xm[i]);
+    const std::vector<uint32_t> l = M.from(M.mul(inv, rdm)).limbs(S, LB);
+    std::copy(l.begin(), l.end(), buf.begin() + (size_t)i * S);
+  }
+  HIPCHK(hipMemcpy(d_cval, buf.data(), buf.size() * 4, hipMemcpyHostToDevice));
+  return 0;
+}
+
 // Builds everything the fixed-base path needs for window c->fb_W (or the largest smaller window within
 // the memory budget). Returns 1 when the path is ready, 0 when it is unavailable (reason in fb_reason);
 // never fails the caller.
@@ -701,6 +744,8 @@ static int ensure_fb(pai_ctx* c) {
   int rc;
   void* t[2] = {nullptr, nullptr};
   void* lohi[2] = {nullptr, nullptr};
+  std::vector<void*> fb_scratch;   // further build scratch (freed with lohi)
+  uint32_t* gcval[2] = {nullptr, nullptr};
   for (int h = 0; h < 2; ++h) {
     if (!c->fb_g[h] && !(c->fb_g[h] = fb_base(primes[h]))) return fb_unavailable(c, "no base found");
     const HBig& m2 = sq[h];
@@ -805,8 +850,19 @@ static int ensure_fb(pai_ctx* c) {
           (rc = upload_fb(c, mul(P, pow2(20)).limbs(FBGP_S, LB), &gpbig)) || (rc = upload_fb(c, m2.limbs(sb, LB), &gp2)) ||
           (rc = upload_fb(c, mul_pow2_mod(P, RB, m2).limbs(sb, LB), &gpr2)))
         return fb_unavailable(c, pai_last_error());
+      // factored rows (kernels_grp_pair.hpp): inverse tables of the lo/hi entries and the inversion's prefix
+      // products -- build scratch, released with lohi
+      void *vinv = nullptr, *vpre = nullptr, *vcv = nullptr;
+      const size_t em = (size_t)1 << (W - W / 2);
+      if (hipMalloc(&vinv, (size_t)K * 2 * FB_LO * FBGP_S * 4) != hipSuccess ||
+          (c->fb_mem.push_back(vinv), hipMalloc(&vpre, (size_t)2 * K * em * FBGP_S * 4) != hipSuccess) ||
+          (c->fb_mem.push_back(vpre), hipMalloc(&vcv, (size_t)2 * K * FBGP_S * 4) != hipSuccess))
+        return fb_unavailable(c, "table allocation failed");
+      c->fb_mem.push_back(vcv);
+      for (void* q : {vinv, vpre, vcv}) fb_scratch.push_back(q);
+      gcval[h] = (uint32_t*)vcv;
       gv[h] = FbgpHalf{(const uint32_t*)t[h], gp, gx, gone, gbases, dlohi, gnm, gpbig, gp2, gpr2, mont_prime(P, LB),
-                       mont_prime(m2, LB)};
+                       mont_prime(m2, LB), (uint32_t*)vinv, (uint32_t*)vpre, (uint32_t*)vcv};
     }
     if (h == 0) {
       c->d_fb_m0 = dm;
@@ -864,13 +920,20 @@ static int ensure_fb(pai_ctx* c) {
     std::vector<FbgpHalf> gvv(gv, gv + 2);
     if ((rc = upload_fb(c, gvv, &c->d_fbgp_halves))) return fb_unavailable(c, pai_last_error());
   }
-  const hipError_t be = gpair_ok  ? fbgp_build_tables(c->d_fbgp_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
+  if (gpair_ok) {   // factored rows: the chain products are inverted on the host between the two phases
+    if (fbgp_build_phase1(c->d_fbgp_halves, K, W, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+      return fb_unavailable(c, "table construction failed");
+    for (int h = 0; h < 2; ++h)
+      if (pair_host_invert(primes[h], gcval[h], 2 * K, FBGP_S)) return fb_unavailable(c, pai_last_error());
+  }
+  const hipError_t be = gpair_ok  ? fbgp_build_phase2(c->d_fbgp_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
                         : grp     ? grp_build_tables(c->d_fb_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
                         : pair_ok ? fbp_build_tables(ps, c->d_fbp_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr)
                                   : fb_build_tables(sb, c->d_fb_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
   if (be != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return fb_unavailable(c, "table construction failed");
-  for (void* p : lohi) {
+  for (void* p : lohi) fb_scratch.push_back(p);
+  for (void* p : fb_scratch) {
     c->fb_mem.erase(std::find(c->fb_mem.begin(), c->fb_mem.end(), p));
     (void)hipFree(p);
   }
@@ -1603,7 +1666,15 @@ static int ensure_pfb(pai_ctx* c) {
       (rc = upload_pfb(c, split(oneR), &done)) || (rc = upload_pfb(c, split(R2), &dr2)) ||
       (rc = upload_pfb(c, gl, &dgl)) || (rc = upload_pfb(c, n.words(PFB_PW), &dnw)))
     return pfb_unavailable(c, pai_last_error());
-  void *vb = nullptr, *vl = nullptr, *vt = nullptr;
+  void *vb = nullptr, *vl = nullptr, *vt = nullptr, *vinv = nullptr, *vpre = nullptr;
+  void* vcv = nullptr;
+  if (hipMalloc(&vcv, (size_t)2 * K * PFB_S * 4) != hipSuccess) return pfb_unavailable(c, "table allocation failed");
+  c->pfb_mem.push_back(vcv);
+  if (hipMalloc(&vinv, (size_t)K * 2 * FB_LO * PFB_S * 4) != hipSuccess) return pfb_unavailable(c, "table allocation failed");
+  c->pfb_mem.push_back(vinv);
+  if (hipMalloc(&vpre, (size_t)2 * K * ((size_t)1 << (W - W / 2)) * PFB_S * 4) != hipSuccess)
+    return pfb_unavailable(c, "table allocation failed");
+  c->pfb_mem.push_back(vpre);
   if (hipMalloc(&vb, (size_t)K * 2 * 2 * PFB_S * 4) != hipSuccess) return pfb_unavailable(c, "table allocation failed");
   c->pfb_mem.push_back(vb);
   if (hipMalloc(&vl, (size_t)K * 2 * FB_LO * 2 * PFB_S * 4) != hipSuccess) return pfb_unavailable(c, "table allocation failed");
@@ -1616,7 +1687,7 @@ static int ensure_pfb(pai_ctx* c) {
   dtab = (uint4*)vt;
   PfbConst pc{};
   pc.g = FbgpHalf{(const uint32_t*)dtab, dn, dx, done, dbases, dlohi, nullptr, nullptr, nullptr, nullptr,
-                  mont_prime(n, LB), 0u};
+                  mont_prime(n, LB), 0u, (uint32_t*)vinv, (uint32_t*)vpre, (uint32_t*)vcv};
   pc.table = dtab;
   pc.gl = dgl;
   pc.r2 = dr2;
@@ -1631,9 +1702,12 @@ static int ensure_pfb(pai_ctx* c) {
   PfbConst* dpc = nullptr;
   if ((rc = upload_pfb(c, pv, &dpc))) return pfb_unavailable(c, pai_last_error());
   const auto t1 = std::chrono::steady_clock::now();
-  if (pfb_build_tables(dpc, pc.nbases, K, W, dtab, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+  if (pfb_build_phase1(dpc, pc.nbases, K, W, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return pfb_unavailable(c, "table construction failed");
-  for (void* q : {vb, vl}) {   // build scratch
+  if (pair_host_invert(n, (uint32_t*)vcv, 2 * K, PFB_S)) return pfb_unavailable(c, pai_last_error());
+  if (pfb_build_phase2(dpc, K, W, dtab, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    return pfb_unavailable(c, "table construction failed");
+  for (void* q : {vb, vl, vinv, vpre, vcv}) {   // build scratch
     c->pfb_mem.erase(std::find(c->pfb_mem.begin(), c->pfb_mem.end(), q));
     (void)hipFree(q);
   }

@@ -31,6 +31,10 @@ struct FbgpHalf {
   const uint32_t* pR2;     // p_h R' mod p_h^2, R' = 2^(28 148), 148 limbs (k_fbgp_w)
   uint32_t mprime;         // -p_h^-1 mod 2^28
   uint32_t mprime2;        // -p_h^-2 mod 2^28
+  // factored rows (below): inverses of the lo/hi entries' A parts, and the construction scratch
+  uint32_t* inv;           // [K][2][FB_LO][S]: (A of lo/hi entry)^-1 R mod p_h
+  uint32_t* pre;           // [2K][2^HI][S] prefix products of the batch inversion (scratch)
+  uint32_t* cval;          // [2K][S]: each chain's product (k_pair_inv_fwd), then its inverse R^2 (host)
 };
 
 struct FbgpParams {
@@ -70,6 +74,11 @@ __device__ __forceinline__ void fbgp_pair_to_slot(uint32_t* slot, const uint32_t
     slot[S + t * LL + i] = b[i];
   }
   wave_lds_fence();
+}
+template <int TPI, int LL>
+__device__ __forceinline__ void pfb_store_limbs(uint32_t* dst, const uint32_t (&x)[LL], int tig) {
+#pragma unroll
+  for (int i = 0; i < LL; ++i) dst[tig * LL + i] = x[i];
 }
 template <int TPI, int LL>
 __device__ __forceinline__ void fbgp_regs_to_slot(uint32_t* slot, const uint32_t (&A)[LL], const uint32_t (&B)[LL], int tig) {
@@ -141,7 +150,7 @@ __device__ __forceinline__ void pair_rows_dma(const uint4* __restrict__ table, s
 // of each component, i.e. bits from 28 LL t: it reads the 18 words from word (28 LL t) / 32, shifts them down by
 // (28 LL t) mod 32 (one funnel shift per word, the lane's own amount) and cuts 28-bit limbs at compile-time
 // offsets. Limbs >= FBGP_SP are zero.
-template <int TPI, int LL>
+template <int TPI, int LL, int NCOMP = 2, int CW = FBGP_PW>
 __device__ __forceinline__ void pair_stage_to_slot(uint32_t* slot, const uint32_t* row, int tig) {
   constexpr int S = TPI * LL;
   constexpr int NW = (LB * LL + 31) / 32 + 1;   // 18 words cover a lane's 19 limbs at any bit offset
@@ -149,7 +158,7 @@ __device__ __forceinline__ void pair_stage_to_slot(uint32_t* slot, const uint32_
   const uint32_t bit0 = (uint32_t)(LB * LL) * (uint32_t)tig;
   const uint32_t w0 = bit0 >> 5, sh = bit0 & 31u;
 #pragma unroll
-  for (int comp = 0; comp < 2; ++comp) {
+  for (int comp = 0; comp < NCOMP; ++comp) {
     const uint32_t* src = row + comp * FBGP_PW + w0;
     uint32_t v[NW];
 #pragma unroll
@@ -163,10 +172,10 @@ __device__ __forceinline__ void pair_stage_to_slot(uint32_t* slot, const uint32_
       const int b = LB * r, w = b >> 5, o = b & 31;
       const uint32_t lo = u[w], hi = (w + 1 < NW - 1) ? u[w + 1] : 0u;
       uint32_t limb = __builtin_amdgcn_alignbit(hi, lo, (uint32_t)o) & LMASK;
-      if (r + (TPI - 1) * LL >= 32 * FBGP_PW / LB) {
-        // limbs at or past bit 32 PW of the component: keep only its own bits (the words read past the component
+      if (r + (TPI - 1) * LL >= 32 * CW / LB) {
+        // limbs at or past bit 32 CW of the component: keep only its own bits (the words read past the component
         // are the other component's, or the next row's)
-        const int lim = 32 * FBGP_PW - LB * (tig * LL + r);
+        const int lim = 32 * CW - LB * (tig * LL + r);
         limb = lim >= LB ? limb : lim > 0 ? (limb & ((1u << lim) - 1u)) : 0u;
       }
       dst[r] = limb;
@@ -174,28 +183,105 @@ __device__ __forceinline__ void pair_stage_to_slot(uint32_t* slot, const uint32_
   }
 }
 
-// (A, B) <- (A, B) prod_k T_k[dg[k stride]] over K word rows of 2^W entries; row k+1 streams in by DMA during
-// product k. wave_stage: this wave's FBGP_STAGE_WORDS words (its own __shared__ object).
+// ---- factored rows
+// A table entry T' = T R mod p^2 is stored as T' = a (1 + p b) with a = T' mod p and b = (T' div p) a^-1 mod p
+// (rows: the words of a, then of b R mod p). The product of the K entries an element selects is then
+//   prod_k T'_k = (prod_k a_k) (1 + p sum_k b_k)   (mod p^2)
+// so the loop multiplies by the pairs (a_k, 0) -- the B row loses its A B2 term: 4 S^2 lane-MACs instead of
+// 5 S^2 -- while each lane adds its quarter of the b R words into a running sum (16 words + a carry count),
+// and one correction at the end applies the factor: (A + p B)(1 + p bs) = A + p (B + A bs) (mod p^2),
+// B += REDC(A (bs R)). Same value, same ciphertext bits.
+
+// the bR words of the group's staged row (words PW .. 2 PW) into this lane's quarter of the running sum, which
+// lives in the slot's B half (the B2 = 0 products never read it): 16 words at slot + S + 16 t, the carry count
+// at slot + S + PW + t
+template <int TPI, int LL>
+__device__ __forceinline__ void pair_bsum_add(uint32_t* slot, const uint32_t* row, int tig) {
+  constexpr int S = TPI * LL, NB = FBGP_PW / TPI;
+  const uint4* src = reinterpret_cast<const uint4*>(row + FBGP_PW) + tig * (NB / 4);
+  uint4* acc = reinterpret_cast<uint4*>(slot + S) + tig * (NB / 4);
+  uint32_t w[NB], a[NB];
+#pragma unroll
+  for (int q = 0; q < NB / 4; ++q) {
+    const uint4 v = src[q], u = acc[q];
+    w[4 * q] = v.x, w[4 * q + 1] = v.y, w[4 * q + 2] = v.z, w[4 * q + 3] = v.w;
+    a[4 * q] = u.x, a[4 * q + 1] = u.y, a[4 * q + 2] = u.z, a[4 * q + 3] = u.w;
+  }
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const uint64_t v = (uint64_t)a[i] + w[i] + c;
+    a[i] = (uint32_t)v;
+    c = v >> 32;
+  }
+#pragma unroll
+  for (int q = 0; q < NB / 4; ++q) acc[q] = make_uint4(a[4 * q], a[4 * q + 1], a[4 * q + 2], a[4 * q + 3]);
+  slot[S + FBGP_PW + tig] += (uint32_t)c;
+}
+
+// (A, B) <- (A, B) prod_k T_k[dg[k stride]] over K factored word rows of 2^W entries; row k+1 streams in by DMA
+// during product k. wave_stage: this wave's FBGP_STAGE_WORDS words (its own __shared__ object). Leaves the
+// running b sum in the slot's B half for pair_apply_bsum.
 template <int TPI, int LL>
 __device__ __forceinline__ void pair_table_products(uint32_t (&A)[LL], uint32_t (&B)[LL], const uint4* __restrict__ table,
                                                     const uint32_t* __restrict__ dg, long long stride, int K, int W,
                                                     uint32_t* slot, const uint32_t* wave_stage, const uint32_t* xs,
                                                     const uint32_t (&m)[LL], uint32_t mprime, int lane, int tig) {
+  constexpr int S = TPI * LL;
   const uint32_t* row = wave_stage + (lane / TPI) * 2 * FBGP_PW;
+  wave_lds_fence();
+  for (int i = tig; i < FBGP_PW + TPI; i += TPI) slot[S + i] = 0u;   // the b sum and its carry counts
   pair_rows_dma(table, 0, W, dg[0], wave_stage, lane);
   uint32_t dn = K > 1 ? dg[(size_t)stride] : 0u;
   for (int k = 0; k < K; ++k) {
     lds_dma_wait();                                   // row k landed, digit k+1 loaded
     wave_lds_fence();
-    pair_stage_to_slot<TPI, LL>(slot, row, tig);
+    pair_stage_to_slot<TPI, LL, 1>(slot, row, tig);   // a (the B half of the slot is not read)
+    pair_bsum_add<TPI, LL>(slot, row, tig);
     wave_lds_fence();
     if (k + 1 < K) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the staged row is consumed before it is overwritten
       pair_rows_dma(table, (size_t)(k + 1), W, dn, wave_stage, lane);
       dn = k + 2 < K ? dg[(size_t)(k + 2) * stride] : 0u;
     }
-    pgrp::montmul<TPI, LL, false>(A, B, slot, xs, m, mprime, lane, tig);
+    pgrp::montmul<TPI, LL, false, true>(A, B, slot, xs, m, mprime, lane, tig);
   }
+}
+
+// B += REDC(A bsR) with bsR = sum_k b_k R (the lanes' words plus their carries, < 2^(32 PW + 7)): then
+// A + p B == (A + p B)(1 + p sum b_k) (mod p^2). Uses the group's staging row and slot. B < 4p on exit.
+template <int TPI, int LL>
+__device__ __forceinline__ void pair_apply_bsum(uint32_t (&A)[LL], uint32_t (&B)[LL], uint32_t* slot, uint32_t* row,
+                                                const uint32_t (&m)[LL], uint32_t mprime, int lane, int tig) {
+  constexpr int S = TPI * LL, NB = FBGP_PW / TPI;
+  constexpr int CW = FBGP_PW + 4;   // the sum's words (carries above word PW)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  wave_lds_fence();
+  for (int i = tig; i < FBGP_PW; i += TPI) row[i] = slot[S + i];
+  for (int i = FBGP_PW + tig; i < CW + 2; i += TPI) row[i] = 0u;
+  wave_lds_fence();
+  // carry count of lane t enters at word NB (t + 1): applied one lane at a time (a few words ripple at most)
+  for (int t = 0; t < TPI; ++t) {
+    if (tig == t) {
+      uint64_t c = slot[S + FBGP_PW + t];
+      for (int w = NB * (t + 1); c != 0 && w < CW; ++w) {
+        const uint64_t v = (uint64_t)row[w] + c;
+        row[w] = (uint32_t)v;
+        c = v >> 32;
+      }
+    }
+    wave_lds_fence();
+  }
+  pair_stage_to_slot<TPI, LL, 1, CW>(slot, row, tig);
+  wave_lds_fence();
+  uint32_t U[LL];
+#pragma unroll
+  for (int i = 0; i < LL; ++i) U[i] = A[i];
+  pgrp::montmul1<TPI, LL>(U, slot, m, mprime, lane, tig);   // A bs mod p, < 2p
+  uint64_t P[LL];
+#pragma unroll
+  for (int i = 0; i < LL; ++i) P[i] = (uint64_t)B[i] + U[i];
+  pgrp::normalize<TPI, LL>(P, B, lane, tig);
 }
 
 template <int TPI, int LL>
@@ -261,6 +347,9 @@ __global__ __launch_bounds__(BLOCK, 2) void k_fbgp(FbgpParams p) {
       }
     }
     pair_table_products<TPI, LL>(A, B, table, dg, p.n, K, W, slot, wstage, xs, m, mprime, lane, tig);
+    pair_apply_bsum<TPI, LL>(A, B, slot, const_cast<uint32_t*>(wstage) + (lane / TPI) * 2 * FBGP_PW, m, mprime, lane, tig);
+    pgrp::cond_sub<TPI, LL>(B, m, lane, tig);   // B < 4p -> < 2p: canon takes B + 1 <= 2p
+    pgrp::cond_sub<TPI, LL>(B, m, lane, tig);
     pgrp::canon<TPI, LL>(A, B, m, lane, tig);
     if (valid) {
 #pragma unroll
@@ -317,6 +406,132 @@ __global__ __launch_bounds__(BLOCK) void k_fbgp_w(FbgpParams p) {
       for (int i = 0; i < L; ++i) p.out[((size_t)half * S + tig * L + i) * p.n + ii] = t[i];
     }
   }
+}
+
+// ---- construction of factored rows
+// lo[j], hi[j] represent L_j R, H_j R mod p^2 (their A parts: A_j == L_j R mod p); the fill's pair product gives
+// the canonical (A, B) of T' = L H R, A == L H R (mod p). The factored row needs b R = B A^-1 R = B (L H)^-1 mod p.
+// With inv_x = L_x^-1 R (k_pair_inv, R-forms): X = mont(inv_lo, inv_hi) = (L H)^-1 R, and mont(B, X) = B (L H)^-1.
+template <int TPI, int LL>
+__device__ __forceinline__ void pair_factor_row(uint32_t (&B)[LL], const FbgpHalf* H, int k, int d, int W, uint32_t* slot,
+                                                const uint32_t (&m)[LL], int lane, int tig) {
+  constexpr int S = TPI * LL;
+  const int LO = W / 2;
+  const uint32_t* il = H->inv + (((size_t)k * 2 + 0) * FB_LO + (d & ((1 << LO) - 1))) * S;
+  const uint32_t* ih = H->inv + (((size_t)k * 2 + 1) * FB_LO + (d >> LO)) * S;
+  uint32_t X[LL], Y[LL];
+  fbgp_load<TPI, LL>(il, X, tig);
+  fbgp_load<TPI, LL>(ih, Y, tig);
+  wave_lds_fence();
+#pragma unroll
+  for (int i = 0; i < LL; ++i) slot[tig * LL + i] = Y[i];
+  wave_lds_fence();
+  pgrp::montmul1<TPI, LL>(X, slot, m, H->mprime, lane, tig);   // X = (L H)^-1 R
+  wave_lds_fence();
+#pragma unroll
+  for (int i = 0; i < LL; ++i) slot[tig * LL + i] = X[i];
+  wave_lds_fence();
+  pgrp::montmul1<TPI, LL>(B, slot, m, H->mprime, lane, tig);   // b R = B (L H)^-1
+  pgrp::cond_sub<TPI, LL>(B, m, lane, tig);
+}
+
+// Batch inversion of the lo/hi entries' A parts (Montgomery's trick), one group per chain (half, k, lo|hi), in
+// R-forms throughout. k_pair_inv_fwd: prefix products P_j = (L_0 .. L_j) R (scratch) and the chain's product
+// P = (L_0 .. L_EM-1) R; the host inverts the 2K chain products of a half at once (one extended-Euclid inversion,
+// batch trick) -- the modulus may be composite (n, for the public fixed bases), so no Fermat -- and writes back
+// I = P^-1 R^2 = (L_0 .. L_EM-1)^-1 R; k_pair_inv_bwd: inv_j = I_j P_(j-1), I_(j-1) = I_j x_j, i.e.
+// inv_j = L_j^-1 R. Every group runs the longest chain (wave-uniform trip counts: the groups' DPP shifts read their
+// neighbours); shorter chains are padded with the Montgomery one.
+template <int TPI, int LL>
+struct PairInvChain {
+  int k, sp, E, EM;
+  bool valid;
+  const uint32_t* lh;
+  uint32_t* pre;
+  __device__ PairInvChain(const FbgpHalf* H, int K, int W, int gib) {
+    const int c0 = blockIdx.x * (BLOCK / TPI) + gib;
+    valid = c0 < 2 * K;
+    const int c = valid ? c0 : 0;
+    k = c >> 1;
+    sp = c & 1;
+    const int LO = W / 2, HI = W - LO;
+    E = 1 << (sp ? HI : LO);
+    EM = 1 << (HI > LO ? HI : LO);
+    constexpr int S = TPI * LL;
+    lh = H->lohi + ((size_t)k * 2 + sp) * FB_LO * 2 * S;
+    pre = H->pre + (size_t)c * EM * S;
+  }
+};
+
+template <int TPI, int LL>
+__device__ __forceinline__ void pair_inv_mul(uint32_t (&a)[LL], const uint32_t (&b)[LL], uint32_t* slot, const uint32_t (&m)[LL],
+                                             uint32_t mprime, int lane, int tig) {
+  wave_lds_fence();
+#pragma unroll
+  for (int i = 0; i < LL; ++i) slot[tig * LL + i] = b[i];
+  wave_lds_fence();
+  pgrp::montmul1<TPI, LL>(a, slot, m, mprime, lane, tig);
+}
+
+template <int TPI, int LL>
+__global__ __launch_bounds__(BLOCK) void k_pair_inv_fwd(const FbgpHalf* halves, int K, int W) {
+  constexpr int S = TPI * LL;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int lane = threadIdx.x & 63, tig = threadIdx.x % TPI, gib = threadIdx.x / TPI;
+  uint32_t* slot = smem + gib * S;
+  const FbgpHalf* H = halves + blockIdx.y;
+  const PairInvChain<TPI, LL> ch(H, K, W, gib);
+  uint32_t m[LL], one[LL], acc[LL], x[LL];
+  fbgp_load<TPI, LL>(H->p, m, tig);
+  fbgp_load<TPI, LL>(H->oneR, one, tig);          // R mod p: the Montgomery one
+  for (int j = 0; j < ch.EM; ++j) {
+    if (j < ch.E) fbgp_load<TPI, LL>(ch.lh + (size_t)j * 2 * S, x, tig);
+    else {
+#pragma unroll
+      for (int i = 0; i < LL; ++i) x[i] = one[i];
+    }
+    if (j == 0) {
+#pragma unroll
+      for (int i = 0; i < LL; ++i) acc[i] = x[i];
+    } else {
+      pair_inv_mul<TPI, LL>(acc, x, slot, m, H->mprime, lane, tig);
+    }
+    if (ch.valid) pfb_store_limbs<TPI, LL>(ch.pre + (size_t)j * S, acc, tig);
+  }
+  pgrp::cond_sub<TPI, LL>(acc, m, lane, tig);
+  if (ch.valid) pfb_store_limbs<TPI, LL>(H->cval + (size_t)(2 * ch.k + ch.sp) * S, acc, tig);
+}
+
+template <int TPI, int LL>
+__global__ __launch_bounds__(BLOCK) void k_pair_inv_bwd(const FbgpHalf* halves, int K, int W) {
+  constexpr int S = TPI * LL;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const int lane = threadIdx.x & 63, tig = threadIdx.x % TPI, gib = threadIdx.x / TPI;
+  uint32_t* slot = smem + gib * S;
+  const FbgpHalf* H = halves + blockIdx.y;
+  const PairInvChain<TPI, LL> ch(H, K, W, gib);
+  uint32_t m[LL], one[LL], I[LL], x[LL];
+  fbgp_load<TPI, LL>(H->p, m, tig);
+  fbgp_load<TPI, LL>(H->oneR, one, tig);
+  fbgp_load<TPI, LL>(H->cval + (size_t)(2 * ch.k + ch.sp) * S, I, tig);
+  uint32_t* out = H->inv + ((size_t)ch.k * 2 + ch.sp) * FB_LO * S;
+  for (int j = ch.EM - 1; j >= 1; --j) {
+    uint32_t t[LL];
+    fbgp_load<TPI, LL>(ch.pre + (size_t)(j - 1) * S, x, tig);
+#pragma unroll
+    for (int i = 0; i < LL; ++i) t[i] = I[i];
+    pair_inv_mul<TPI, LL>(t, x, slot, m, H->mprime, lane, tig);
+    pgrp::cond_sub<TPI, LL>(t, m, lane, tig);
+    if (ch.valid && j < ch.E) pfb_store_limbs<TPI, LL>(out + (size_t)j * S, t, tig);
+    if (j < ch.E) fbgp_load<TPI, LL>(ch.lh + (size_t)j * 2 * S, x, tig);
+    else {
+#pragma unroll
+      for (int i = 0; i < LL; ++i) x[i] = one[i];
+    }
+    pair_inv_mul<TPI, LL>(I, x, slot, m, H->mprime, lane, tig);
+  }
+  pgrp::cond_sub<TPI, LL>(I, m, lane, tig);
+  if (ch.valid) pfb_store_limbs<TPI, LL>(out, I, tig);
 }
 
 // lo[j] = B_k^j R (j < 2^LO), hi[j] = (B_k^(2^LO))^j R (j < 2^(W - LO)): one group per entry, square-and-
@@ -411,6 +626,7 @@ __global__ __launch_bounds__(BLOCK) void k_fbgp_fill(const FbgpHalf* halves, int
   }
   pgrp::montmul<TPI, LL, false>(A, B, slot, xs, m, H->mprime, lane, tig);
   pgrp::canon<TPI, LL>(A, B, m, lane, tig);
+  pair_factor_row<TPI, LL>(B, H, k, d, W, slot, m, lane, tig);
   uint4* t = reinterpret_cast<uint4*>(half ? table1 : table0);
   pair_store_row<TPI, LL>(valid ? t + ((size_t)k * ent + d) * FBGP_ROW4 : nullptr, slot, A, B, tig);
 }

@@ -12,10 +12,12 @@
 //   k_pfb_chain   once per key: one group per base: h_j R = (g_j R)^n by square-and-multiply, then the digit
 //                 bases B_k R = (h_j R)^(2^(W pos)) and B_k^(2^LO) R, canonical pairs, for k_fbgp_lohi
 //   k_fbgp_lohi   (kernels_grp_pair.hpp, one "half") lo/hi half-digit powers
-//   k_pfb_fill    T_k[d] R = lo * hi, canonical pair, stored as 32-bit words: [K][2^W][A: PW][B: PW]
-//                 (512 B per row at nb = 2048: four aligned 128-B lines)
+//   k_pair_inv   (kernels_grp_pair.hpp) batch inversion of the lo/hi entries' A parts
+//   k_pfb_fill    T_k[d] R = lo * hi as a factored row a (1 + n b): the words of a, then of b R mod n
+//                 (512 B per row at nb = 2048: four aligned 128-B lines; kernels_grp_pair.hpp "factored rows")
 //   k_pfb_digits  per element: the ChaCha20 stream (nonce: index, 0x70666230) cut into K W-bit digits
-//   k_pfb         per element: encode, c0 = the pair (1, M mod n), K row products, canonical pair -> xw
+//   k_pfb         per element: encode, c0 = the pair (1, M mod n), K products by (a_k, 0) + the b sum, the
+//                 correction (1 + n sum b_k), canonical pair -> xw
 //   k_pe_fin      (kernels_pe.hpp) c = A + n B -> ciphertext words
 #pragma once
 #include "kernels_grp_pair.hpp"
@@ -181,6 +183,7 @@ __global__ __launch_bounds__(BLOCK) void k_pfb_fill(const PfbConst* c, int K, in
   }
   pgrp::montmul<TPI, LL, false>(A, B, slot, xs, m, H->mprime, lane, tig);
   pgrp::canon<TPI, LL>(A, B, m, lane, tig);
+  pair_factor_row<TPI, LL>(B, H, k, d, W, slot, m, lane, tig);
   if (valid) pair_store_row<TPI, LL>(table + ((size_t)k * ent + d) * FBGP_ROW4, slot, A, B, tig);
   else pair_store_row<TPI, LL>(nullptr, slot, A, B, tig);
 }
@@ -267,6 +270,9 @@ __global__ __launch_bounds__(BLOCK, 2) void k_pfb(PfbParams p) {
       for (int i = 0; i < LL; ++i) B[i] = neg ? D[i] : ml[i];
     }
     pair_table_products<TPI, LL>(A, B, table, dg, p.n, K, W, slot, wstage, xs, m, mprime, lane, tig);
+    pair_apply_bsum<TPI, LL>(A, B, slot, const_cast<uint32_t*>(wstage) + (lane / TPI) * 2 * FBGP_PW, m, mprime, lane, tig);
+    pgrp::cond_sub<TPI, LL>(B, m, lane, tig);   // B < 4p -> < 2p
+    pgrp::cond_sub<TPI, LL>(B, m, lane, tig);
     pgrp::canon<TPI, LL>(A, B, m, lane, tig);
     if (valid) {
 #pragma unroll

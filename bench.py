@@ -123,12 +123,25 @@ def work_fbg(nb: int, digits: int) -> dict:
     return {"k_fb_digits": 0.0, "k_fbg": float(2 * digits * _M(s)), "k_fbg_fin": float(_M(s) + _M(nb // 16))}
 
 
+def _Mf(s: int) -> int:
+    """Pair product by a factored row (a, 0) (kernels_grp_pair.hpp): A a + q1 p, B a + q2 p: 4 s^2 + 2 s."""
+    return 4 * s * s + 2 * s
+
+
 def work_fbgp(nb: int, digits: int) -> dict:
-    """The 4096-bit sampler on pair groups (kernels_grp_pair.hpp): K pair products per half over the nb/64
-    32-bit limbs of p_h; the fin stage adds k_fbgp_w's product mod p_h^2 per half to the Garner work."""
+    """The 4096-bit sampler on pair groups with factored rows (kernels_grp_pair.hpp): K products by (a_k, 0) per half
+    over the nb/64 32-bit limbs of p_h, plus the correction B += REDC(A bs) (one s-limb Montgomery product, M(s));
+    the fin stage adds k_fbgp_w's product mod p_h^2 per half to the Garner work."""
     s = nb // 64
-    return {"k_fb_digits": 0.0, "k_fbgp": float(2 * digits * _Mp(s)),
+    return {"k_fb_digits": 0.0, "k_fbgp": float(2 * (digits * _Mf(s) + _M(s))),
             "k_fbg_fin": float(2 * _M(nb // 32) + _M(nb // 32) + _M(nb // 16))}
+
+
+def work_pfb(nb: int, digits: int) -> float:
+    """Public fixed bases (kernels_pfb.hpp): K products by factored rows over the nb/32 32-bit limbs of n, plus the
+    correction (one Montgomery product mod n)."""
+    s = nb // 32
+    return float(digits * _Mf(s) + _M(s))
 
 
 def work_dec(nb: int) -> float:
@@ -807,7 +820,7 @@ def main():
             runs.append((time.perf_counter() - t1, cpub.stage_times()))
         wall, pst = min(runs, key=lambda r: r[0])
         bases, Kp, Wp, K0p = cpub.public_fixed_base_info()
-        wpfb = float(Kp * _Mp(nb // 32))            # K pair products mod n^2 over the nb/32 32-bit limbs of n
+        wpfb = work_pfb(nb, Kp)                     # K factored-row products mod n^2 + the correction
         # exact round trip through the key holder's decryption
         valp = torch.empty(N, dtype=torch.float64, device=dev)
         stp = torch.empty(N, dtype=torch.int32, device=dev)
@@ -960,7 +973,11 @@ def main():
                      "kernel": dom, "kernel_ms": dom_ms,
                      "work_per_unit": (f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} pair "
                                        f"products mod p_h^2 per half, 5 s^2 + 2 s each over s = nb/64 32-bit limbs of p_h, "
-                                       f"kernels_fbp.hpp), not SURVEY.md §8d's W_enc" if dom in ("k_fbp", "k_fbgp") else
+                                       f"kernels_fbp.hpp), not SURVEY.md §8d's W_enc" if dom == "k_fbp" else
+                                       f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} products by "
+                                       f"factored rows (a, 0) mod p_h^2 per half, 4 s^2 + 2 s each over s = nb/64 32-bit limbs "
+                                       f"of p_h, + the b-sum correction, kernels_grp_pair.hpp), not SURVEY.md §8d's W_enc"
+                                       if dom == "k_fbgp" else
                                        f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} table "
                                        f"products per half, 32-bit limbs, kernels_fb.hpp), not SURVEY.md §8d's W_enc"
                                        if dom in ("k_fb", "k_fbg") else f"{dom_work:.4g} canonical 32x32->64 MAC per element (SURVEY.md §8d)")},

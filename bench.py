@@ -108,11 +108,12 @@ def _Mp(s: int) -> int:
 
 
 def work_fbp(nb: int, digits: int) -> dict:
-    """Per-element MACs of the pair fixed-base path (kernels_fbp.hpp): k_fbp = K pair products per half
-    (s = nb/64 limbs of p_h) + the c0 chunk sum (s^2); k_fbp_fin = Garner on pairs: q B_q (4 s^2, B row zero),
-    h (5 s^2), c = A_q + q B_q + q^2 H_A + p q^2 H_B (6 s^2)."""
+    """Per-element MACs of the pair fixed-base path (kernels_fbp.hpp): k_fbp = K products by factored rows (a_k, 0)
+    per half (s = nb/64 limbs of p_h, 4 s^2 + 2 s each) + the c0 chunk sum (s^2) + the b-sum correction
+    B += REDC(A bs) (one s-limb Montgomery product, M(s)); k_fbp_fin = Garner on pairs: q B_q (4 s^2, B row
+    zero), h (5 s^2), c = A_q + q B_q + q^2 H_A + p q^2 H_B (6 s^2)."""
     s = nb // 64
-    return {"k_fb_digits": 0.0, "k_fbp": float(2 * (digits * _Mp(s) + s * s)), "k_fbp_fin": float(15 * s * s)}
+    return {"k_fb_digits": 0.0, "k_fbp": float(2 * (digits * _Mf(s) + s * s + _M(s))), "k_fbp_fin": float(15 * s * s)}
 
 
 def work_fbg(nb: int, digits: int) -> dict:
@@ -971,13 +972,11 @@ def main():
                      "unit": "TMAC/s", "frac": achieved / INT_MAC_PEAK,
                      "traffic": load_traffic(dom, N, nb, fb_info[3] if (use_fb and dom in ("k_fb", "k_fbp", "k_fbg", "k_fbgp")) else None),
                      "kernel": dom, "kernel_ms": dom_ms,
-                     "work_per_unit": (f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} pair "
-                                       f"products mod p_h^2 per half, 5 s^2 + 2 s each over s = nb/64 32-bit limbs of p_h, "
-                                       f"kernels_fbp.hpp), not SURVEY.md §8d's W_enc" if dom == "k_fbp" else
-                                       f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} products by "
+                     "work_per_unit": (f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} products by "
                                        f"factored rows (a, 0) mod p_h^2 per half, 4 s^2 + 2 s each over s = nb/64 32-bit limbs "
-                                       f"of p_h, + the b-sum correction, kernels_grp_pair.hpp), not SURVEY.md §8d's W_enc"
-                                       if dom == "k_fbgp" else
+                                       f"of p_h, + the c0 sum and the b-sum correction, "
+                                       f"{'kernels_fbp.hpp' if dom == 'k_fbp' else 'kernels_grp_pair.hpp'}), not SURVEY.md §8d's W_enc"
+                                       if dom in ("k_fbp", "k_fbgp") else
                                        f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} table "
                                        f"products per half, 32-bit limbs, kernels_fb.hpp), not SURVEY.md §8d's W_enc"
                                        if dom in ("k_fb", "k_fbg") else f"{dom_work:.4g} canonical 32x32->64 MAC per element (SURVEY.md §8d)")},

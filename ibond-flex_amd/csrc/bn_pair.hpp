@@ -133,6 +133,106 @@ __device__ __forceinline__ void mont_mul(uint32_t (&A)[S], uint32_t (&B)[S], Get
   normalize_signed<S>(P2, B);
 }
 
+// ---- products by a pair (a, 0): a factored table row (kernels_fbp.hpp)
+// (A + p B) a R^-1 == U + p REDC(B a - m) (mod p^2): the A1 B2 term is gone, 4 S^2 MACs. Run as two CIOS passes
+// over the digits of a -- U = REDC(A a), handing each reduction digit q1_j to put(j, q1_j), then REDC(B a - m),
+// m = sum q1_j 2^(28 j), with gb(j) returning (a_j, q1_j) -- so that only one 64-bit accumulator row (2S VGPRs)
+// is live at a time; the caller keeps the digits where it has room. Bounds as above (the second pass is the
+// signed row of the lock-step product with one product per position and digit fewer).
+template <int S, int Z>
+__device__ __forceinline__ void pin1(uint64_t (&P)[S]) {
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+    if (i != Z) asm volatile("" : "+v"(P[i]));
+}
+
+template <int S, int J, class Get, class Put>
+__device__ __forceinline__ void a0_step_u(uint64_t (&P)[S], const uint32_t (&A)[S], Get& get, Put& put, const uint32_t (&m)[S],
+                                          uint32_t mprime) {
+  const uint32_t aj = get(std::integral_constant<int, J>{});
+#pragma unroll
+  for (int i = 0; i < S; ++i) P[(i + J) % S] += (uint64_t)A[i] * aj;
+  const uint32_t q = ((uint32_t)P[J] * mprime) & LMASK;
+  put(std::integral_constant<int, J>{}, q);
+#pragma unroll
+  for (int i = 0; i < S; ++i) P[(i + J) % S] += (uint64_t)q * m[i];
+  P[(J + 1) % S] += P[J] >> LB;
+  P[J] = 0;
+  pin1<S, J>(P);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int S, int J, class Get>
+__device__ __forceinline__ void a0_step_b(uint64_t (&P)[S], const uint32_t (&B)[S], Get& get, const uint32_t (&m)[S],
+                                          uint32_t mprime) {
+  const uint2 d = get(std::integral_constant<int, J>{});   // (a_J, q1_J)
+#pragma unroll
+  for (int i = 0; i < S; ++i) P[(i + J) % S] += (uint64_t)B[i] * d.x;
+  P[J] -= (uint64_t)d.y;
+  const uint32_t q2 = ((uint32_t)P[J] * mprime) & LMASK;
+#pragma unroll
+  for (int i = 0; i < S; ++i) P[(i + J) % S] += (uint64_t)q2 * m[i];
+  P[(J + 1) % S] += (uint64_t)((int64_t)P[J] >> LB);
+  P[J] = 0;
+  pin1<S, J>(P);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int S, class Get, class Put, int... Js>
+__device__ __forceinline__ void a0_pass_u(uint64_t (&P)[S], const uint32_t (&A)[S], Get& get, Put& put, const uint32_t (&m)[S],
+                                          uint32_t mprime, std::integer_sequence<int, Js...>) {
+  (a0_step_u<S, Js>(P, A, get, put, m, mprime), ...);
+}
+template <int S, class Get, int... Js>
+__device__ __forceinline__ void a0_pass_b(uint64_t (&P)[S], const uint32_t (&B)[S], Get& get, const uint32_t (&m)[S],
+                                          uint32_t mprime, std::integer_sequence<int, Js...>) {
+  (a0_step_b<S, Js>(P, B, get, m, mprime), ...);
+}
+
+// normalisation into 32-bit registers: the limb is cut by an explicit v_and_b32 into a fresh register -- left to
+// LLVM, the mask is applied to the 64-bit sum and the limb stays the low half of a live register pair (every
+// loop-carried limb then holds two VGPRs)
+__device__ __forceinline__ uint32_t limb32(uint64_t v) {
+  uint32_t r;
+  asm("v_and_b32 %0, 0xfffffff, %1" : "=v"(r) : "v"((uint32_t)v));
+  return r;
+}
+template <int S>
+__device__ __forceinline__ void normalize32(const uint64_t (&P)[S], uint32_t (&r)[S]) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const uint64_t v = P[i] + c;
+    r[i] = limb32(v);
+    c = v >> LB;
+  }
+}
+template <int S>
+__device__ __forceinline__ void normalize32_signed(const uint64_t (&P)[S], uint32_t (&r)[S]) {
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const int64_t v = (int64_t)P[i] + c;
+    r[i] = limb32((uint64_t)v);
+    c = v >> LB;
+  }
+}
+
+// (A, B) <- (A, B)(a, 0) R^-1 (above)
+template <int S, class GetU, class Put, class GetB>
+__device__ __forceinline__ void mont_mul_a0(uint32_t (&A)[S], uint32_t (&B)[S], GetU&& ga, Put&& put, GetB&& gb,
+                                            const uint32_t (&m)[S], uint32_t mprime) {
+  uint64_t P[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) P[i] = 0;
+  a0_pass_u<S>(P, A, ga, put, m, mprime, std::make_integer_sequence<int, S>{});
+  normalize32<S>(P, A);
+#pragma unroll
+  for (int i = 0; i < S; ++i) P[i] = 0;
+  a0_pass_b<S>(P, B, gb, m, mprime, std::make_integer_sequence<int, S>{});
+  normalize32_signed<S>(P, B);
+}
+
 // (A, B) with A, B < 2p -> the canonical pair A < p, B < p of the same residue mod p^2
 // (A - p + p (B + 1) == A + p B)
 template <int S>

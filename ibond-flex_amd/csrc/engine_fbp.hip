@@ -35,13 +35,31 @@ hipError_t fbp_launch_fin(int s, const FbpFinParams& p, int gx, hipStream_t st) 
   return hipGetLastError();
 }
 
-hipError_t fbp_build_tables(int s, const FbpHalf* d_halves, uint4* t0, uint4* t1, int K, int W, hipStream_t st) {
-  const int per = ((1 << W) + LANE_BLOCK - 1) / LANE_BLOCK;
+// table construction, phase 1: lo/hi half-digit powers, then the forward pass of the batch inversion (the chain
+// products land in FbpHalf::cval for the host's inversion)
+hipError_t fbp_build_phase1(int s, const FbpHalf* d_halves, int K, int W, hipStream_t st) {
+  const dim3 ig((2 * K + 63) / 64, 2);
   if (s == 19) {
     hipLaunchKernelGGL(k_fbp_lohi<19>, dim3(K, 2), dim3(LANE_BLOCK), 0, st, d_halves, K, W);
-    hipLaunchKernelGGL(k_fbp_fill<19>, dim3(K * per, 2), dim3(LANE_BLOCK), 0, st, d_halves, K, W, t0, t1);
+    hipLaunchKernelGGL(k_fbp_inv_fwd<19>, ig, dim3(64), 0, st, d_halves, K, W);
   } else if (s == 37) {
     hipLaunchKernelGGL(k_fbp_lohi<37>, dim3(K, 2), dim3(LANE_BLOCK), 0, st, d_halves, K, W);
+    hipLaunchKernelGGL(k_fbp_inv_fwd<37>, ig, dim3(64), 0, st, d_halves, K, W);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+// phase 2 (after the host wrote the chain inverses): the inverse tables, then the factored rows
+hipError_t fbp_build_phase2(int s, const FbpHalf* d_halves, uint4* t0, uint4* t1, int K, int W, hipStream_t st) {
+  const int per = ((1 << W) + LANE_BLOCK - 1) / LANE_BLOCK;
+  const dim3 ig((2 * K + 63) / 64, 2);
+  if (s == 19) {
+    hipLaunchKernelGGL(k_fbp_inv_bwd<19>, ig, dim3(64), 0, st, d_halves, K, W);
+    hipLaunchKernelGGL(k_fbp_fill<19>, dim3(K * per, 2), dim3(LANE_BLOCK), 0, st, d_halves, K, W, t0, t1);
+  } else if (s == 37) {
+    hipLaunchKernelGGL(k_fbp_inv_bwd<37>, ig, dim3(64), 0, st, d_halves, K, W);
     hipLaunchKernelGGL(k_fbp_fill<37>, dim3(K * per, 2), dim3(LANE_BLOCK), 0, st, d_halves, K, W, t0, t1);
   } else {
     return hipErrorInvalidValue;

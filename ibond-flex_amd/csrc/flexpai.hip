@@ -746,6 +746,7 @@ static int ensure_fb(pai_ctx* c) {
   void* lohi[2] = {nullptr, nullptr};
   std::vector<void*> fb_scratch;   // further build scratch (freed with lohi)
   uint32_t* gcval[2] = {nullptr, nullptr};
+  uint32_t* pcval[2] = {nullptr, nullptr};
   for (int h = 0; h < 2; ++h) {
     if (!c->fb_g[h] && !(c->fb_g[h] = fb_base(primes[h]))) return fb_unavailable(c, "no base found");
     const HBig& m2 = sq[h];
@@ -815,7 +816,19 @@ static int ensure_fb(pai_ctx* c) {
           (rc = upload_fb(c, bases_p, &pbases)) || (rc = upload_fb(c, nm_p, &pnm)) ||
           (rc = upload_fb(c, mul(P, pow2(FBP_PB)).limbs(ps, LB), &ppbig)))
         return fb_unavailable(c, pai_last_error());
-      pv[h] = FbpHalf{(const uint4*)t[h], pp, pone, pbases, dlohi, pnm, ppbig, mont_prime(P, LB)};
+      // factored rows (kernels_fbp.hpp): inverse tables of the lo/hi entries' A parts and the batch inversion's
+      // scratch -- released with lohi
+      void *vinv = nullptr, *vpre = nullptr, *vcv = nullptr;
+      const size_t em = (size_t)1 << (W - W / 2);
+      if (hipMalloc(&vinv, (size_t)K * 2 * FB_LO * ps * 4) != hipSuccess ||
+          (c->fb_mem.push_back(vinv), hipMalloc(&vpre, (size_t)2 * K * em * ps * 4) != hipSuccess) ||
+          (c->fb_mem.push_back(vpre), hipMalloc(&vcv, (size_t)2 * K * ps * 4) != hipSuccess))
+        return fb_unavailable(c, "table allocation failed");
+      c->fb_mem.push_back(vcv);
+      for (void* q : {vinv, vpre, vcv}) fb_scratch.push_back(q);
+      pcval[h] = (uint32_t*)vcv;
+      pv[h] = FbpHalf{(const uint4*)t[h], pp, pone, pbases, dlohi, pnm, ppbig, mont_prime(P, LB),
+                      (uint32_t*)vinv, (uint32_t*)vpre, (uint32_t*)vcv};
     }
     if (gpair_ok) {
       // pair-group constants: S = 76 limbs of p_h, R = 2^(28 S); pairs as [A: S][B: S]
@@ -920,15 +933,17 @@ static int ensure_fb(pai_ctx* c) {
     std::vector<FbgpHalf> gvv(gv, gv + 2);
     if ((rc = upload_fb(c, gvv, &c->d_fbgp_halves))) return fb_unavailable(c, pai_last_error());
   }
-  if (gpair_ok) {   // factored rows: the chain products are inverted on the host between the two phases
-    if (fbgp_build_phase1(c->d_fbgp_halves, K, W, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
-      return fb_unavailable(c, "table construction failed");
+  if (gpair_ok || pair_ok) {   // factored rows: the chain products are inverted on the host between the two phases
+    const hipError_t e1 = gpair_ok ? fbgp_build_phase1(c->d_fbgp_halves, K, W, nullptr)
+                                   : fbp_build_phase1(ps, c->d_fbp_halves, K, W, nullptr);
+    if (e1 != hipSuccess || hipDeviceSynchronize() != hipSuccess) return fb_unavailable(c, "table construction failed");
     for (int h = 0; h < 2; ++h)
-      if (pair_host_invert(primes[h], gcval[h], 2 * K, FBGP_S)) return fb_unavailable(c, pai_last_error());
+      if (pair_host_invert(primes[h], gpair_ok ? gcval[h] : pcval[h], 2 * K, gpair_ok ? FBGP_S : ps))
+        return fb_unavailable(c, pai_last_error());
   }
   const hipError_t be = gpair_ok  ? fbgp_build_phase2(c->d_fbgp_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
                         : grp     ? grp_build_tables(c->d_fb_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
-                        : pair_ok ? fbp_build_tables(ps, c->d_fbp_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr)
+                        : pair_ok ? fbp_build_phase2(ps, c->d_fbp_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr)
                                   : fb_build_tables(sb, c->d_fb_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
   if (be != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return fb_unavailable(c, "table construction failed");

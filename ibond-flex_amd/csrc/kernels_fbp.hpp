@@ -1,14 +1,19 @@
 // Fixed-base obfuscation on p-adic pairs (bn_pair.hpp): the sampler of kernels_fb.hpp with every
-// product mod p_h^2 done as a pair product over the S limbs of p_h (5 S^2 MACs) instead of a Montgomery
-// product over the 2S limbs of p_h^2 (8 S^2 MACs). Same distribution, same ciphertext bits.
+// product mod p_h^2 done over the S limbs of p_h instead of a Montgomery product over the 2S limbs of
+// p_h^2 (8 S^2 MACs). Same distribution, same ciphertext bits.
 //
-// Table rows hold the canonical pair (A, B) of T_k[d] R mod p_h^2 (R = 2^(28 S)): PW 32-bit words of A
-// then PW words of B -- 256 B for a 2048-bit key, the row size of k_fb. The accumulator starts at c0 =
-// 1 + n M = 1 + p_h (n / p_h) M, i.e. the pair (1, (n / p_h) M mod p_h), with the second component an
-// unreduced sum of 8-bit chunks of |M| (< 2^PB p_h; the first product keeps B < 2 p_h while R >= 2^(PB+1) p_h).
-// Every product multiplies a plain pair by a Montgomery-form row, so the result stays plain: after the
-// K products the pair is c0 G_h^(a_h) mod p_h^2, written as its canonical pair for k_fbp_fin's Garner
-// recombination (below).
+// Factored rows. A table entry T' = T_k[d] R mod p_h^2 (R = 2^(28 S)) is stored as T' = a (1 + p_h b) with
+// a = T' mod p_h and b = (T' div p_h) a^-1 mod p_h: PW 32-bit words of a, then PW words of b R mod p_h -- 256 B
+// for a 2048-bit key. The product of the K entries an element selects is
+//   prod_k T'_k = (prod_k a_k) (1 + p_h sum_k b_k)   (mod p_h^2)
+// so the loop multiplies the pair by (a_k, 0) -- 4 S^2 MACs instead of the 5 S^2 of a general pair product
+// (bn_pair.hpp mont_mul_a0) -- while the b R words go into a running sum (PW words + a carry word, in VGPRs),
+// and one product mod p_h at the end applies the factor: (A + p B)(1 + p bs) = A + p (B + A bs). The
+// accumulator starts at c0 = 1 + n M = 1 + p_h (n / p_h) M, i.e. the pair (1, (n / p_h) M mod p_h), with the
+// second component an unreduced sum of 8-bit chunks of |M| (< 2^PB p_h; the first product keeps B < 2 p_h
+// while R >= 2^(PB+1) p_h). Every product multiplies a plain pair by a Montgomery-form row, so the result stays
+// plain: after the K products and the correction the pair is c0 G_h^(a_h) mod p_h^2, written as its canonical
+// pair for k_fbp_fin's Garner recombination (below).
 #pragma once
 #include "bn_pair.hpp"
 #include "kernels_fb.hpp"
@@ -28,7 +33,7 @@ struct FbpGeom<37> {   // 2048-bit keys: p_h < 2^1024
 constexpr int FBP_CB = 8, FBP_NC = 8, FBP_PB = 11;    // c0 chunks: 8 x 8 bits of |M| (sum < 2^11 p_h); offset 2^11 p_h
 
 struct FbpHalf {
-  const uint4* table;      // [K][2^W][2 PW / 4] quads: words of A, then of B, of the pair of T_k[d] R mod p_h^2
+  const uint4* table;      // [K][2^W][2 PW / 4] quads: words of a, then of b R mod p_h, of T_k[d] R mod p_h^2 (header)
   const uint32_t* p;       // p_h, S limbs
   const uint32_t* oneR;    // pair of R mod p_h^2 (2S limbs: A then B)
   const uint32_t* bases;   // [K][2][2S] pairs of B_k R and B_k^(2^LO) R mod p_h^2 (table construction)
@@ -36,6 +41,10 @@ struct FbpHalf {
   const uint32_t* nm;      // [NC][S] (n / p_h) 2^(CB c) mod p_h
   const uint32_t* pbig;    // [S] 2^PB p_h
   uint32_t mprime;         // -p_h^-1 mod 2^28
+  // factored rows: inverses of the lo/hi entries' A parts, and the batch inversion's scratch (k_fbp_inv_*)
+  uint32_t* inv;           // [K][2][FB_LO][S]: (A of lo/hi entry)^-1 R mod p_h
+  uint32_t* pre;           // [2K][2^max(LO,HI)][S] prefix products
+  uint32_t* cval;          // [2K][S]: each chain's product, then its inverse R^2 (host)
 };
 
 struct FbpParams {
@@ -50,50 +59,172 @@ struct FbpParams {
   int32_t* status;
 };
 
-// The multiplier's digit pairs from this lane's word row in LDS ([quad][lane] layout, A words then B
-// words), read D words ahead: digit J needs words (28 J) / 32 and (28 J + 27) / 32 of each half-row.
+// LDS words at a byte offset from this lane's row base (offsets past the 16-bit immediate take a second base)
+template <int OFF>
+__device__ __forceinline__ uint32_t lds_word_rd(uint32_t addr) {
+  if constexpr (OFF < 65536) return lds_read_word<OFF>(addr);
+  else return lds_read_word<OFF - 65536>(addr + 65536u);
+}
+template <int OFF>
+__device__ __forceinline__ void lds_word_wr(uint32_t addr, uint32_t v) {
+  if constexpr (OFF < 65536) asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(addr), "v"(v), "i"(OFF) : "memory");
+  else asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(addr + 65536u), "v"(v), "i"(OFF - 65536) : "memory");
+}
+
+// Per product with a factored row, in LDS ([quad][lane] layout, quads of LANE_BLOCK x 16 B): the a words in quads
+// 0 .. PW/4 - 1, the b R words in quads PW/4 .. PW/2 - 1 (summed first, then dead), and the first pass's reduction
+// digits q1_j in word slots j of quads PW/4 + j/4 (the dead b R quads, then FBP_XQ extra quads).
+template <int S, int PW>
+struct FbpLds {
+  static constexpr int TQ = PW / 2;                                       // quads of a DMA'd row
+  static constexpr int NQ = PW / 4 + (S + 3) / 4 > TQ ? PW / 4 + (S + 3) / 4 : TQ;   // quads per lane
+  static constexpr int a_off(int w) { return (w / 4) * LANE_BLOCK * 16 + (w % 4) * 4; }
+  static constexpr int q_off(int j) { return (PW / 4 + j / 4) * LANE_BLOCK * 16 + (j % 4) * 4; }
+};
+
+// The multiplier's digits a_J from the a words, read D words ahead: digit J needs words (28 J) / 32 and
+// (28 J + 27) / 32. Pass 1 of mont_mul_a0 (FbpAReader): the LDS operations in flight are the word reads, issued at
+// the digits, and one q1 write after each digit (FbpQPut), and every wait names the exact count of operations
+// issued after the words it needs. Pass 2 (FbpAQReader): the word reads and the q1 reads, q1_j read QD digits ahead.
 template <int S, int PW, int D>
-struct FbpRowDigits {
-  uint32_t addr;
-  uint32_t wa[PW], wb[PW];
+struct FbpWordSched {
   static constexpr int lo(int J) { return (28 * J) >> 5; }
   static constexpr int hi(int J) { return (28 * J + 27) >> 5 < PW - 1 ? (28 * J + 27) >> 5 : PW - 1; }
   static constexpr int issued(int J) { return J < 0 ? -1 : (hi(J) + D < PW - 1 ? hi(J) + D : PW - 1); }
-  template <int WI>
-  __device__ __forceinline__ void issue_word() {
-    wa[WI] = lds_read_word<(WI / 4) * LANE_BLOCK * 16 + (WI % 4) * 4>(addr);
-    wb[WI] = lds_read_word<((PW + WI) / 4) * LANE_BLOCK * 16 + ((PW + WI) % 4) * 4>(addr);
+  static constexpr int nA(int J) { return issued(J) - issued(J - 1); }
+  static constexpr int batch_of(int w) {   // the digit whose issue phase reads word w
+    int j = 0;
+    while (issued(j) < w) ++j;
+    return j;
   }
+  __device__ static __forceinline__ uint32_t digit(int, uint32_t) { return 0; }
+};
+
+template <int S, int PW, int D>
+struct FbpAReader {
+  using Sc = FbpWordSched<S, PW, D>;
+  uint32_t addr;
+  uint32_t wa[PW];
+  // operations issued before digit J's issue phase: the words of digits < J and their q1 writes
+  static constexpr int before(int J) { return Sc::issued(J - 1) + 1 + J; }
+  static constexpr int pos(int w) { return before(Sc::batch_of(w)) + (w - Sc::issued(Sc::batch_of(w) - 1) - 1); }
   template <int W0, int... Ws>
   __device__ __forceinline__ void issue(std::integer_sequence<int, Ws...>) {
-    (issue_word<W0 + Ws>(), ...);
+    ((wa[W0 + Ws] = lds_word_rd<FbpLds<S, PW>::a_off(W0 + Ws)>(addr)), ...);
+  }
+  template <int J>
+  __device__ __forceinline__ uint32_t operator()(std::integral_constant<int, J>) {
+    constexpr int from = Sc::issued(J - 1) + 1, to = Sc::issued(J);
+    issue<from>(std::make_integer_sequence<int, (to >= from ? to - from + 1 : 0)>{});
+    constexpr int l = Sc::lo(J), h = Sc::hi(J);
+    constexpr int pending = before(J) + Sc::nA(J) - 1 - pos(h);
+    static_assert(pending >= 0 && pending <= 15, "lgkmcnt range");
+    if constexpr (l == h) asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(wa[l]) : "i"(pending));
+    else asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(wa[l]), "+v"(wa[h]) : "i"(pending));
+    constexpr int sh = (28 * J) & 31;
+    if constexpr (sh + 28 <= 32) return (wa[l] >> sh) & lane::LMASK;
+    else if constexpr (l + 1 < PW) return __builtin_amdgcn_alignbit(wa[l + 1], wa[l], sh) & lane::LMASK;
+    else return wa[l] >> sh;
+  }
+};
+
+template <int S, int PW>
+struct FbpQPut {
+  uint32_t addr;
+  template <int J>
+  __device__ __forceinline__ void operator()(std::integral_constant<int, J>, uint32_t q) {
+    lds_word_wr<FbpLds<S, PW>::q_off(J)>(addr, q);
+  }
+};
+
+template <int S, int PW, int D, int QD>
+struct FbpAQReader {
+  using Sc = FbpWordSched<S, PW, D>;
+  static_assert(QD >= 1 && QD < S, "q1 read-ahead");
+  uint32_t addr;
+  uint32_t wa[PW], wq[S];
+  // issue phase of digit J: (J = 0: q1_0 .. q1_(QD-1)), the words of batch J, then q1_(J+QD) if it exists
+  static constexpr int nq(int J) { return (J == 0 ? QD : 0) + (J + QD < S ? 1 : 0); }
+  static constexpr int before(int J) {
+    int s = 0;
+    for (int t = 0; t < J; ++t) s += Sc::nA(t) + nq(t);
+    return s;
+  }
+  static constexpr int pos_a(int w) {
+    const int jb = Sc::batch_of(w);
+    return before(jb) + (jb == 0 ? QD : 0) + (w - Sc::issued(jb - 1) - 1);
+  }
+  static constexpr int pos_q(int i) { return i < QD ? i : before(i - QD) + (i == QD ? QD : 0) + Sc::nA(i - QD); }
+  template <int W0, int... Ws>
+  __device__ __forceinline__ void issue(std::integer_sequence<int, Ws...>) {
+    ((wa[W0 + Ws] = lds_word_rd<FbpLds<S, PW>::a_off(W0 + Ws)>(addr)), ...);
+  }
+  template <int... Is>
+  __device__ __forceinline__ void issue_q(std::integer_sequence<int, Is...>) {
+    ((wq[Is] = lds_word_rd<FbpLds<S, PW>::q_off(Is)>(addr)), ...);
   }
   template <int J>
   __device__ __forceinline__ uint2 operator()(std::integral_constant<int, J>) {
-    constexpr int from = issued(J - 1) + 1, to = issued(J);
+    if constexpr (J == 0) issue_q(std::make_integer_sequence<int, QD>{});
+    constexpr int from = Sc::issued(J - 1) + 1, to = Sc::issued(J);
     issue<from>(std::make_integer_sequence<int, (to >= from ? to - from + 1 : 0)>{});
-    constexpr int l = lo(J), h = hi(J);
-    constexpr int pending = 2 * (to - h);   // reads issued after the words digit J needs
-    static_assert(pending <= 15, "lgkmcnt range");
-    if constexpr (l == h) asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(wa[l]), "+v"(wb[l]) : "i"(pending));
-    else asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(wa[l]), "+v"(wa[h]), "+v"(wb[l]), "+v"(wb[h]) : "i"(pending));
-    constexpr int bit = 28 * J, sh = bit & 31;
-    uint32_t x, y;
-    if constexpr (l >= PW) {
-      x = y = 0u;
-    } else if constexpr (sh + 28 <= 32) {
-      x = (wa[l] >> sh) & lane::LMASK;
-      y = (wb[l] >> sh) & lane::LMASK;
-    } else if constexpr (l + 1 < PW) {
-      x = __builtin_amdgcn_alignbit(wa[l + 1], wa[l], sh) & lane::LMASK;
-      y = __builtin_amdgcn_alignbit(wb[l + 1], wb[l], sh) & lane::LMASK;
-    } else {
-      x = wa[l] >> sh;
-      y = wb[l] >> sh;
-    }
-    return make_uint2(x, y);
+    if constexpr (J + QD < S) wq[J + QD] = lds_word_rd<FbpLds<S, PW>::q_off(J + QD)>(addr);
+    constexpr int l = Sc::lo(J), h = Sc::hi(J);
+    constexpr int need = pos_a(h) > pos_q(J) ? pos_a(h) : pos_q(J);
+    constexpr int pending = before(J) + Sc::nA(J) + nq(J) - 1 - need;
+    static_assert(pending >= 0 && pending <= 15, "lgkmcnt range");
+    if constexpr (l == h) asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(wa[l]), "+v"(wq[J]) : "i"(pending));
+    else asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(wa[l]), "+v"(wa[h]), "+v"(wq[J]) : "i"(pending));
+    constexpr int sh = (28 * J) & 31;
+    uint32_t x;
+    if constexpr (sh + 28 <= 32) x = (wa[l] >> sh) & lane::LMASK;
+    else if constexpr (l + 1 < PW) x = __builtin_amdgcn_alignbit(wa[l + 1], wa[l], sh) & lane::LMASK;
+    else x = wa[l] >> sh;
+    return make_uint2(x, wq[J]);
   }
 };
+
+// the b R words of this lane's row in LDS (quads PW/4 .. PW/2 - 1) into the running sum bs (PW words) + bc
+template <int PW>
+__device__ __forceinline__ void fbp_bsum_add(uint32_t (&bs)[PW], uint32_t& bc, const uint4* lrow) {
+  unsigned int c = 0;
+#pragma unroll
+  for (int q = 0; q < PW / 4; ++q) {
+    const uint4 v = lrow[(PW / 4 + q) * LANE_BLOCK];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) bs[4 * q + t] = __builtin_addc(bs[4 * q + t], w[t], c, &c);   // 32-bit add-with-carry chain
+  }
+  bc += c;
+  // the sum is complete here: otherwise LLVM sinks the adds past the product (the sum is not read there) and keeps
+  // the row words it loaded live across it
+#pragma unroll
+  for (int j = 0; j < PW; ++j) asm volatile("" : "+v"(bs[j]));
+  asm volatile("" : "+v"(bc));
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// (A, B) <- (A, B)(1 + p bs) = (A, B + REDC(A (bs R))), bs R = the words bs + bc 2^(32 PW) (< 2^(32 PW + 7), i.e.
+// S canonical limbs); REDC(A bs R) < p + 2^8 p^2 / R < 2p, so B < 4p on exit
+template <int S, int PW>
+__device__ __forceinline__ void fbp_apply_bsum(uint32_t (&A)[S], uint32_t (&B)[S], const uint32_t (&bs)[PW], uint32_t bc,
+                                               const uint32_t (&m)[S], uint32_t mprime) {
+  static_assert(28 * S >= 32 * PW + 7, "the sum fits S limbs");
+  uint32_t bl[S], U[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    bl[j] = lane::limb_from_words([&](int w) { return w < PW ? bs[w] : bc; }, PW + 1, j);
+    U[j] = A[j];
+  }
+  lane::mont_mul<S>(U, bl, m, mprime);
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const uint32_t v = B[j] + U[j] + c;
+    B[j] = v & lane::LMASK;
+    c = v >> lane::LB;
+  }
+}
 
 // c0 = 1 + n M as the pair (1, (n / p_h) M mod p_h), second component partially reduced (header)
 template <int S>
@@ -135,13 +266,19 @@ __device__ __forceinline__ void fbp_store_w(const uint32_t (&A)[S], const uint32
   ((acc += fbp_col<S, Ks>(A, B, m), out[(size_t)Ks * n] = (uint32_t)acc & lane::LMASK, acc >>= lane::LB), ...);
 }
 
-// Per element and half: c0 prod_k T_k[d_k] mod p_h^2 by pair products; row k in LDS (DMA one digit
-// ahead, one buffer per wave, two waves per SIMD), as k_fb.
+// Per element and half: c0 prod_k T_k[d_k] mod p_h^2 by products with factored rows (header); row k in LDS
+// (DMA one digit ahead, one buffer per wave, two waves per SIMD), as k_fb.
+#ifndef FBP_RD
+#define FBP_RD 3   // words read ahead of the digit that needs them
+#endif
+#ifndef FBP_QD
+#define FBP_QD 2   // q1 digits read ahead in the second pass
+#endif
 template <int S>
 __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp(FbpParams p) {
   using G = FbpGeom<S>;
   constexpr int SB = G::SB, PW = G::PW, TQ = 2 * PW / 4;
-  __shared__ uint4 lbuf[TQ * LANE_BLOCK];
+  __shared__ uint4 lbuf[FbpLds<S, PW>::NQ * LANE_BLOCK];
   const int half = blockIdx.y;
   const FbpHalf* H = p.halves + half;
   uint32_t m[S];
@@ -177,14 +314,16 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp(FbpParams p) {
     }
     uint32_t A[S], B[S];
     fbp_c0<S>(M, H, A, B);
+    uint32_t bs[PW], bc = 0;
+#pragma unroll
+    for (int j = 0; j < PW; ++j) bs[j] = 0;
     uint32_t dn2 = K > 2 ? dg[2 * p.n] : 0u;
     for (int k = 0; k < K; ++k) {
       lds_dma_wait();                                     // row k landed, digit k+2 loaded
-      {
-        FbpRowDigits<S, PW, 2> rd{addr0};
-        pair::mont_mul<S>(A, B, rd, m, mprime);           // every read of the row completes inside
-      }
-      if (k + 1 < K) {
+      fbp_bsum_add<PW>(bs, bc, lbuf + threadIdx.x);
+      pair::mont_mul_a0<S>(A, B, FbpAReader<S, PW, FBP_RD>{addr0}, FbpQPut<S, PW>{addr0},
+                           FbpAQReader<S, PW, FBP_RD, FBP_QD>{addr0}, m, mprime);
+      if (k + 1 < K) {                                    // (every read of the row completed inside)
         const uint32_t dk1 = dn;
         dn = dn2;
         if (k + 3 < K) dn2 = dg[(size_t)(k + 3) * p.n];
@@ -192,6 +331,9 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp(FbpParams p) {
       }
     }
     if (i < p.n) {
+      fbp_apply_bsum<S, PW>(A, B, bs, bc, m, mprime);
+      lane::cond_sub<S>(B, m);                            // B < 4p -> < 2p
+      lane::cond_sub<S>(B, m);
       pair::canon<S>(A, B, m);
       // (opaque base and stride: their 2S addresses must not be hoisted into registers live across the k loop)
       uint32_t* o = p.out + (size_t)half * 2 * S * p.n + i;
@@ -339,8 +481,8 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
 
 // ---------------------------------------------------------------- per-key table in pair form
 // k_fbp_lohi: per position k, lo[j] = B_k^j R (j < 2^LO) and hi[j] = B_k^(2^LO j) R (j < 2^(W-LO)) by
-// square-and-multiply from R (the pair of one); k_fbp_fill: T_k[d] R = lo[d & (2^LO - 1)] hi[d >> LO] R^-1,
-// one pair product per entry, canonicalised and stored as words.
+// square-and-multiply from R (the pair of one); k_fbp_inv_*: the inverses of their A parts mod p_h; k_fbp_fill:
+// T_k[d] R = lo[d & (2^LO - 1)] hi[d >> LO] R^-1, one pair product per entry, factored (header) and stored as words.
 template <int S>
 __global__ __launch_bounds__(LANE_BLOCK) void k_fbp_lohi(const FbpHalf* halves, int K, int W) {
   const int k = blockIdx.x, half = blockIdx.y;
@@ -383,6 +525,88 @@ __device__ __forceinline__ void fbp_store_row(uint4* __restrict__ dst, const uin
    ...);
 }
 
+// Batch inversion of the lo/hi entries' A parts (Montgomery's trick; kernels_grp_pair.hpp's k_pair_inv_* on the lane
+// engine), one lane per chain c = (k, lo|hi) of a half, R-forms throughout: k_fbp_inv_fwd writes the prefix products
+// P_j = (L_0 .. L_j) R and the chain's product; the host (pair_host_invert) turns each chain product into its inverse
+// I = (L_0 .. L_(E-1))^-1 R; k_fbp_inv_bwd: inv_j = I_j P_(j-1) = L_j^-1 R, I_(j-1) = I_j L_j.
+template <int S>
+struct FbpInvChain {
+  int E;
+  bool valid;
+  const uint32_t* lh;   // entry j's A part at lh + 2 S j
+  uint32_t* pre;        // prefix product j at pre + S j
+  uint32_t* inv;        // inverse j at inv + S j
+  uint32_t* cval;
+  __device__ FbpInvChain(const FbpHalf* H, int K, int W) {
+    const int c0 = blockIdx.x * blockDim.x + threadIdx.x;
+    valid = c0 < 2 * K;
+    const int c = valid ? c0 : 0, k = c >> 1, sp = c & 1;
+    const int LO = W / 2, HI = W - LO, EM = 1 << (HI > LO ? HI : LO);
+    E = 1 << (sp ? HI : LO);
+    lh = H->lohi + ((size_t)k * 2 + sp) * FB_LO * 2 * S;
+    pre = H->pre + (size_t)c * EM * S;
+    inv = H->inv + ((size_t)k * 2 + sp) * FB_LO * S;
+    cval = H->cval + (size_t)c * S;
+  }
+};
+
+template <int S>
+__global__ __launch_bounds__(64) void k_fbp_inv_fwd(const FbpHalf* halves, int K, int W) {
+  const FbpHalf* H = halves + blockIdx.y;
+  const FbpInvChain<S> ch(H, K, W);
+  if (!ch.valid) return;
+  uint32_t m[S], acc[S], x[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    m[i] = H->p[i];
+    acc[i] = ch.lh[i];
+    ch.pre[i] = acc[i];
+  }
+  for (int j = 1; j < ch.E; ++j) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) x[i] = ch.lh[(size_t)j * 2 * S + i];
+    lane::mont_mul<S>(acc, x, m, H->mprime);
+#pragma unroll
+    for (int i = 0; i < S; ++i) ch.pre[(size_t)j * S + i] = acc[i];
+  }
+  lane::cond_sub<S>(acc, m);
+#pragma unroll
+  for (int i = 0; i < S; ++i) ch.cval[i] = acc[i];
+}
+
+template <int S>
+__global__ __launch_bounds__(64) void k_fbp_inv_bwd(const FbpHalf* halves, int K, int W) {
+  const FbpHalf* H = halves + blockIdx.y;
+  const FbpInvChain<S> ch(H, K, W);
+  if (!ch.valid) return;
+  uint32_t m[S], I[S], x[S], t[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    m[i] = H->p[i];
+    I[i] = ch.cval[i];
+  }
+  for (int j = ch.E - 1; j >= 1; --j) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      t[i] = I[i];
+      x[i] = ch.pre[(size_t)(j - 1) * S + i];
+    }
+    lane::mont_mul<S>(t, x, m, H->mprime);
+    lane::cond_sub<S>(t, m);
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      ch.inv[(size_t)j * S + i] = t[i];
+      x[i] = ch.lh[(size_t)j * 2 * S + i];
+    }
+    lane::mont_mul<S>(I, x, m, H->mprime);
+  }
+  lane::cond_sub<S>(I, m);
+#pragma unroll
+  for (int i = 0; i < S; ++i) ch.inv[i] = I[i];
+}
+
+// T' = lo hi R^-1 = L H R as its canonical pair (A, B), then the factored row (header): a = A, b R = B (L H)^-1 =
+// REDC(B X) with X = REDC(inv_lo inv_hi) = (L H)^-1 R
 template <int S>
 __global__ __launch_bounds__(LANE_BLOCK) void k_fbp_fill(const FbpHalf* halves, int K, int W, uint4* table0, uint4* table1) {
   constexpr int PW = FbpGeom<S>::PW, TQ = 2 * PW / 4;
@@ -395,8 +619,9 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_fbp_fill(const FbpHalf* halves, 
   const FbpHalf* H = halves + half;
   uint4* table = half ? table1 : table0;
   const int LO = W / 2;
-  const uint32_t* lo = H->lohi + (((size_t)k * 2 + 0) * FB_LO + (d & ((1 << LO) - 1))) * 2 * S;
-  const uint32_t* hi = H->lohi + (((size_t)k * 2 + 1) * FB_LO + (d >> LO)) * 2 * S;
+  const int dl = d & ((1 << LO) - 1), dh = d >> LO;
+  const uint32_t* lo = H->lohi + (((size_t)k * 2 + 0) * FB_LO + dl) * 2 * S;
+  const uint32_t* hi = H->lohi + (((size_t)k * 2 + 1) * FB_LO + dh) * 2 * S;
   uint32_t m[S], A[S], B[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) {
@@ -406,6 +631,19 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_fbp_fill(const FbpHalf* halves, 
   }
   pair::mont_mul<S>(A, B, [&](auto J) { return make_uint2(hi[decltype(J)::value], hi[S + decltype(J)::value]); }, m, H->mprime);
   pair::canon<S>(A, B, m);
+  {
+    const uint32_t* il = H->inv + (((size_t)k * 2 + 0) * FB_LO + dl) * S;
+    const uint32_t* ih = H->inv + (((size_t)k * 2 + 1) * FB_LO + dh) * S;
+    uint32_t X[S], Y[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      X[i] = il[i];
+      Y[i] = ih[i];
+    }
+    lane::mont_mul<S>(X, Y, m, H->mprime);
+    lane::mont_mul<S>(B, X, m, H->mprime);
+    lane::cond_sub<S>(B, m);
+  }
   fbp_store_row<S>(table + ((size_t)k * ent + d) * TQ, A, B, std::make_integer_sequence<int, PW / 4>{});
 }
 

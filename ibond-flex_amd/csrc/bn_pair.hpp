@@ -84,7 +84,7 @@ __device__ __forceinline__ void normalize_signed(const uint64_t (&P)[S], uint32_
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     const int64_t v = (int64_t)P[i] + c;
-    r[i] = (uint32_t)v & LMASK;
+    r[i] = lane::limb32((uint64_t)v);
     c = v >> LB;
   }
 }
@@ -189,35 +189,6 @@ __device__ __forceinline__ void a0_pass_b(uint64_t (&P)[S], const uint32_t (&B)[
   (a0_step_b<S, Js>(P, B, get, m, mprime), ...);
 }
 
-// normalisation into 32-bit registers: the limb is cut by an explicit v_and_b32 into a fresh register -- left to
-// LLVM, the mask is applied to the 64-bit sum and the limb stays the low half of a live register pair (every
-// loop-carried limb then holds two VGPRs)
-__device__ __forceinline__ uint32_t limb32(uint64_t v) {
-  uint32_t r;
-  asm("v_and_b32 %0, 0xfffffff, %1" : "=v"(r) : "v"((uint32_t)v));
-  return r;
-}
-template <int S>
-__device__ __forceinline__ void normalize32(const uint64_t (&P)[S], uint32_t (&r)[S]) {
-  uint64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < S; ++i) {
-    const uint64_t v = P[i] + c;
-    r[i] = limb32(v);
-    c = v >> LB;
-  }
-}
-template <int S>
-__device__ __forceinline__ void normalize32_signed(const uint64_t (&P)[S], uint32_t (&r)[S]) {
-  int64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < S; ++i) {
-    const int64_t v = (int64_t)P[i] + c;
-    r[i] = limb32((uint64_t)v);
-    c = v >> LB;
-  }
-}
-
 // (A, B) <- (A, B)(a, 0) R^-1 (above)
 template <int S, class GetU, class Put, class GetB>
 __device__ __forceinline__ void mont_mul_a0(uint32_t (&A)[S], uint32_t (&B)[S], GetU&& ga, Put&& put, GetB&& gb,
@@ -226,11 +197,11 @@ __device__ __forceinline__ void mont_mul_a0(uint32_t (&A)[S], uint32_t (&B)[S], 
 #pragma unroll
   for (int i = 0; i < S; ++i) P[i] = 0;
   a0_pass_u<S>(P, A, ga, put, m, mprime, std::make_integer_sequence<int, S>{});
-  normalize32<S>(P, A);
+  lane::normalize<S>(P, A);
 #pragma unroll
   for (int i = 0; i < S; ++i) P[i] = 0;
   a0_pass_b<S>(P, B, gb, m, mprime, std::make_integer_sequence<int, S>{});
-  normalize32_signed<S>(P, B);
+  normalize_signed<S>(P, B);
 }
 
 // (A, B) with A, B < 2p -> the canonical pair A < p, B < p of the same residue mod p^2

@@ -1456,7 +1456,7 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
   const int gxG = (int)std::max<long long>(1, std::min<long long>(lane_blocks, (long long)occG * c->cus));
   const size_t dbytes = (size_t)2 * c->fb_K * 4, wbytes = (size_t)2 * std::max(SB, 2 * c->fb_pair_s) * 4;   // per element
   int rc;
-  if ((rc = ensure_work(c, (dbytes + wbytes) * chunk))) return rc;
+  if ((rc = ensure_work(c, dbytes * chunk + wbytes * (size_t)fbp_npad(chunk)))) return rc;   // pairs: 64-element tiles
   uint32_t* digits = (uint32_t*)c->d_work;
   uint32_t* w = (uint32_t*)((char*)c->d_work + dbytes * chunk);
   const size_t esz = e.dtype == PAI_F32 ? 4 : 8;
@@ -2943,9 +2943,20 @@ extern "C" int pai_debug_fb_w(pai_ctx* c, uint32_t* out, size_t max_words, long 
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipDeviceSynchronize());
   const int rows = c->fb_pair_s ? 2 * c->fb_pair_s : c->crt_sb;
-  const size_t words = (size_t)2 * rows * c->fb_last_n;
+  const long long ne = c->fb_last_n;
+  const size_t words = (size_t)2 * rows * ne;
   if (words > max_words) return fail(PAI_ERR_ARG, "buffer too small");
-  HIPCHK(hipMemcpy(out, c->fb_last_w, words * 4, hipMemcpyDeviceToHost));
+  if (c->fb_pair_s) {   // 64-element tiles (kernels_fbp.hpp fbp_pair_index) -> [2][2S][n]
+    const long long np = fbp_npad(ne);
+    std::vector<uint32_t> t((size_t)2 * rows * np);
+    HIPCHK(hipMemcpy(t.data(), c->fb_last_w, t.size() * 4, hipMemcpyDeviceToHost));
+    for (int h = 0; h < 2; ++h)
+      for (int j = 0; j < rows; ++j)
+        for (long long i = 0; i < ne; ++i)
+          out[((size_t)h * rows + j) * ne + i] = t[(size_t)h * rows * np + (size_t)(i >> 6) * rows * 64 + (size_t)j * 64 + (i & 63)];
+  } else {
+    HIPCHK(hipMemcpy(out, c->fb_last_w, words * 4, hipMemcpyDeviceToHost));
+  }
   *n = c->fb_last_n;
   *sb = rows;
   return 0;

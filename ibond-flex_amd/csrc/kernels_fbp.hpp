@@ -47,12 +47,21 @@ struct FbpHalf {
   uint32_t* cval;          // [2K][S]: each chain's product, then its inverse R^2 (host)
 };
 
+// The canonical pairs k_fbp leaves for k_fbp_fin, in tiles of 64 elements: [half][i / 64][2S limbs][i % 64] (n
+// rounded up to 64): a wave's limb j is one 256-B line and every limb of an element sits at a compile-time offset
+// from one address.
+__host__ __device__ constexpr long long fbp_npad(long long n) { return (n + 63) & ~63ll; }
+template <int S>
+__device__ __forceinline__ size_t fbp_pair_index(long long i, int half, long long n) {
+  return (size_t)half * 2 * S * fbp_npad(n) + (size_t)(i >> 6) * 2 * S * 64 + (size_t)(i & 63);
+}
+
 struct FbpParams {
   const FbpHalf* halves;   // [2]
   long long n;
   int K, W;
   const uint32_t* digits;  // [2][K][n]
-  uint32_t* out;           // canonical pairs [2][2S][n] (A limbs, then B) for k_fbp_fin
+  uint32_t* out;           // canonical pairs (A limbs, then B) for k_fbp_fin in 64-element tiles (fbp_pair_index)
   const void* x;
   int dtype, exp_mode, fexp;
   int32_t* exp;
@@ -335,15 +344,9 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp(FbpParams p) {
       lane::cond_sub<S>(B, m);                            // B < 4p -> < 2p
       lane::cond_sub<S>(B, m);
       pair::canon<S>(A, B, m);
-      // (opaque base and stride: their 2S addresses must not be hoisted into registers live across the k loop)
-      uint32_t* o = p.out + (size_t)half * 2 * S * p.n + i;
-      long long nn = p.n;
-      asm volatile("" : "+v"(o), "+s"(nn));
+      uint32_t* o = p.out + fbp_pair_index<S>(i, half, p.n);
 #pragma unroll
-      for (int j = 0; j < 2 * S; ++j) {
-        *o = j < S ? A[j] : B[j - S];
-        o += nn;
-      }
+      for (int j = 0; j < 2 * S; ++j) o[j * 64] = j < S ? A[j] : B[j - S];
     }
   }
 }
@@ -359,7 +362,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp(FbpParams p) {
 // (u^ = the pair of u mod p^2.) Bounds: an operand below 5p (4p) keeps REDC's outputs below 2p while
 // R > 10 p^2 / p; every column of the last sum takes at most 3S products < 2^56.
 struct FbpFinParams {
-  const uint32_t* pr;      // [2][2S][n] canonical pairs from k_fbp (half 0: p, half 1: q)
+  const uint32_t* pr;      // canonical pairs from k_fbp in 64-element tiles (fbp_pair_index; half 0: p, half 1: q)
   long long n;
   const uint32_t* p;       // S limbs of p
   const uint32_t* cs;      // 12 S words: (qR)^ [2S], (q^-2 R)^ [2S], q [S], q^2 [2S], p q^2 [3S], 4p [S], 3p [S]
@@ -441,12 +444,13 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
     const long long i = base + threadIdx.x;
     const bool valid = i < p.n;
     const long long ii = valid ? i : p.n - 1;
-    const uint32_t* pr = p.pr + ii;
+    const uint32_t* pp = p.pr + fbp_pair_index<S>(ii, 0, p.n);   // limb j of the pair at pp[64 j]
+    const uint32_t* pq = p.pr + fbp_pair_index<S>(ii, 1, p.n);
     // X = q B_q mod p^2
     uint32_t xa[S], xb[S];
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      xa[j] = pr[(size_t)(3 * S + j) * p.n];
+      xa[j] = pq[(S + j) * 64];
       xb[j] = 0u;
     }
     pair::mont_mul<S>(xa, xb, FbpFinDigits<S>{cs}, m, mprime);
@@ -455,9 +459,8 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
       int64_t ca = 0, cb = 0;
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        const int64_t va = (int64_t)pr[(size_t)j * p.n] + (int64_t)p4[j] - (int64_t)pr[(size_t)(2 * S + j) * p.n] -
-                           (int64_t)xa[j] + ca;
-        const int64_t vb = (int64_t)pr[(size_t)(S + j) * p.n] + (int64_t)p3[j] - (int64_t)xb[j] - (j == 0 ? 4 : 0) + cb;
+        const int64_t va = (int64_t)pp[j * 64] + (int64_t)p4[j] - (int64_t)pq[j * 64] - (int64_t)xa[j] + ca;
+        const int64_t vb = (int64_t)pp[(S + j) * 64] + (int64_t)p3[j] - (int64_t)xb[j] - (j == 0 ? 4 : 0) + cb;
         xa[j] = (uint32_t)va & lane::LMASK;
         xb[j] = (uint32_t)vb & lane::LMASK;
         ca = va >> lane::LB;
@@ -471,8 +474,8 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
     uint32_t a1[S], b1[S];
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      a1[j] = pr[(size_t)(2 * S + j) * p.n];
-      b1[j] = pr[(size_t)(3 * S + j) * p.n];
+      a1[j] = pq[j * 64];
+      b1[j] = pq[(S + j) * 64];
     }
     fbpf_out_all<S, CW>(a1, b1, xa, xb, cs + 4 * S, reinterpret_cast<uint4*>(p.ct + ii * p.ct_words), valid,
                         std::make_integer_sequence<int, NL>{});

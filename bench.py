@@ -164,14 +164,23 @@ def work_add(exps: "torch.Tensor", nb: int) -> float:
     return float((n * (k - 1) + sq) * _M(nb // 16))
 
 
+def lib_sha16() -> str:
+    """sha256 (16 hex digits) of the libflexpai.so this process runs."""
+    from flex.crypto.paillier import _native
+    with open(_native.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def load_traffic(kernel: str, n: int, nb: int, window=None):
     """Measured HBM bytes per launch of `kernel` (profiles/pmc_<kernel>_latest.json, tools/pmc_traffic.py),
-    only when that profile was taken at the same size, key and fixed-base window."""
+    only when that profile was taken at the same size, key and fixed-base window AND of the same library binary
+    (lib_sha16): a profile of an older build is not reported as this build's traffic."""
     path = os.path.join(ROOT, "profiles", f"pmc_{kernel}_latest.json")
     try:
         with open(path) as f:
             pm = json.load(f)
-        if pm.get("n") == n and pm.get("nb") == nb and pm.get("window") == window:
+        if (pm.get("n") == n and pm.get("nb") == nb and pm.get("window") == window
+                and pm.get("lib_sha16") == lib_sha16()):
             return pm.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass

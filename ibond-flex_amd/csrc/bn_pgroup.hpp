@@ -19,13 +19,20 @@
 namespace fpai {
 namespace pgrp {
 
+// a limb cut from a 64-bit sum into a fresh 32-bit register (see bn_lane.hpp limb32)
+__device__ __forceinline__ uint32_t cut28(uint64_t v) {
+  uint32_t r;
+  asm("v_and_b32 %0, 0xfffffff, %1" : "=v"(r) : "v"((uint32_t)v));
+  return r;
+}
+
 template <int TPI, int LL>
 __device__ __forceinline__ void normalize(const uint64_t (&P)[LL], uint32_t (&r)[LL], int lane, int tig) {
   uint64_t c = 0;
 #pragma unroll
   for (int i = 0; i < LL; ++i) {
     const uint64_t v = P[i] + c;
-    r[i] = (uint32_t)v & LMASK;
+    r[i] = cut28(v);
     c = v >> LB;
   }
   uint32_t inlo = dpp_from_prev((uint32_t)c);

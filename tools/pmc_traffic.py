@@ -2,28 +2,33 @@
 """Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE counter CSVs (separate passes) into per-launch HBM
 bytes for one kernel, with the gfx950 correction of MI355X_MICROARCH.md §HBM: FETCH_SIZE reads
 half of the bytes of a wide coalesced stream (so it is doubled); WRITE_SIZE is taken as is. Both are
-in KiB. Writes profiles/pmc_<kernel>_latest.json, which bench.py reports as roofline.traffic.
+in KiB. Writes profiles/pmc_<kernel>_latest.json, which bench.py reports as roofline.traffic -- only while the
+library it loads is the one profiled: the file records the sha256 of libflexpai.so (lib_sha16).
 
     python tools/pmc_traffic.py FETCH.csv WRITE.csv --kernel k_encrypt --n 1048576 --nb 2048 [-o out.json]
 """
 import argparse
 import csv
+import hashlib
 import re
 import json
 import os
 
 
 def per_launch(path, counter, kernel):
-    """Counter of the LARGEST launch of `kernel` (the bench's full-size call; smaller launches of the
-    same kernel come from the host-boundary legs). Rows of one dispatch are summed."""
-    per = {}
+    """Counter of the FIRST of the largest launches of `kernel` (the bench's full-size call on its main context;
+    smaller launches come from the host-boundary legs, a later same-size launch from a second context, e.g. the
+    library-default window). Rows of one dispatch are summed."""
+    per, grid = {}, {}
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter and re.search(r"\b%s\b" % re.escape(kernel), r["Kernel_Name"]):
-            d = r["Dispatch_Id"]
+            d = int(r["Dispatch_Id"])
             per[d] = per.get(d, 0.0) + float(r["Counter_Value"])
+            grid[d] = int(r["Grid_Size"])
     if not per:
         raise SystemExit(f"no {counter} rows for {kernel} in {path}")
-    return max(per.values()), len(per)
+    g = max(grid.values())
+    return per[min(d for d in per if grid[d] == g)], len(per)
 
 
 def main():
@@ -41,7 +46,11 @@ def main():
                            f"pmc_{a.kernel}_latest.json")
     f, nf = per_launch(a.fetch_csv, "FETCH_SIZE", a.kernel)
     w, nw = per_launch(a.write_csv, "WRITE_SIZE", a.kernel)
-    out = {"kernel": a.kernel, "n": a.n, "nb": a.nb, "window": a.window,
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "ibond-flex_amd", "flex", "crypto", "paillier", "_native", "libflexpai.so")
+    with open(lib, "rb") as fh:
+        lib_sha = hashlib.sha256(fh.read()).hexdigest()[:16]
+    out = {"kernel": a.kernel, "n": a.n, "nb": a.nb, "window": a.window, "lib_sha16": lib_sha,
            "fetch_size_kib_raw": f, "write_size_kib_raw": w, "launches": [nf, nw],
            "hbm_read_bytes_per_launch": 2 * f * 1024, "hbm_write_bytes_per_launch": w * 1024,
            "hbm_bytes_per_launch": (2 * f + w) * 1024,

@@ -230,11 +230,136 @@ __device__ __forceinline__ void d4_run(uint32_t (&a)[S], uint32_t* sx, uint32_t*
   }
 }
 
-template <int S>
-__global__ __launch_bounds__(LANE_BLOCK, 1) void k_dec4_pow(Dec4Params p) {
+// ---- k_dec4_pow: the components in registers (round 3)
+// Each lane keeps ITS component of x in registers (the even lane A, the odd lane B), so a square needs no LDS: the
+// digits are the even lane's own limbs, A[j], broadcast to the odd lane by one DPP per digit and doubled there
+// (P_even += A A_j, P_odd += B 2A_j). A product x t (t in the LDS multiplier st = [A_t][B_t]) runs two passes:
+//   pass A: P += a B_t[j] on both lanes; the even lane's z = REDC(A_x B_t) is written over st's B half (the odd
+//           lane's product is discarded);
+//   pass 1: P += a A_t[j] with the split reduction (odd lane: LMASK - q1 and the start X); then the odd lane adds
+//           z, so B' = REDC(B_x A_t - m) + REDC(A_x B_t) < 4p and the even lane's A' = REDC(A_x A_t).
+// Only the multiplier lives in LDS (2S words per lane pair instead of 4S): two blocks of 256 lanes per CU, two
+// waves per SIMD. A multiplier kept across products (LOP_B_READY without a prefetch: the table's x~^2) has its B
+// half clobbered by z: LOP_B_SET also stores it in a spare tile, reloaded before each later product that keeps it.
+constexpr int D4R_SLOT = 2 * D4_S;       // LDS words per element-half: the multiplier [A][B]
+constexpr int D4R_KEPT = LANE_NTILE;     // spare tile (in the lane scratch's stage-A buffer, unused here)
+static_assert((LANE_NTILE + 1) * tile_quads<D4_S>() <= LANE_NTILE * tile_quads<D4_S>() + RBUF_WORDS / 4,
+              "the spare tile fits the lane scratch");
+
+template <int S, int J>
+__device__ __forceinline__ void d4r_sqr_step(uint64_t (&P)[S], const uint32_t (&a)[S], int tig, const uint32_t (&m)[S],
+                                             uint32_t mprime, bool odd) {
+  const uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a[J], 0xA0, 0xF, 0xF, false) << tig;   // 2^tig A_J
+#pragma unroll
+  for (int i = 0; i < S; ++i) P[(i + J) % S] += (uint64_t)a[i] * y;
+  const uint32_t q0 = ((uint32_t)P[J] * mprime) & lane::LMASK;
+  const uint32_t q1 = __builtin_amdgcn_update_dpp(0u, q0, 0xA0, 0xF, 0xF, false);
+  P[J] += odd ? (uint64_t)(lane::LMASK - q1) : 0ull;
+  const uint32_t q = ((uint32_t)P[J] * mprime) & lane::LMASK;
+#pragma unroll
+  for (int i = 0; i < S; ++i) P[(i + J) % S] += (uint64_t)q * m[i];
+  P[(J + 1) % S] += P[J] >> lane::LB;
+  P[J] = 0;
+  lane::pin<S>(P);
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int S, int... Js>
+__device__ __forceinline__ void d4r_sqr_pass(uint64_t (&P)[S], const uint32_t (&a)[S], int tig, const uint32_t (&m)[S],
+                                             uint32_t mprime, bool odd, std::integer_sequence<int, Js...>) {
+  (d4r_sqr_step<S, Js>(P, a, tig, m, mprime, odd), ...);
+}
+
+template <int S, int... Gs>
+__device__ __forceinline__ void d4r_tile_store(const LaneScratch& t, int k, const uint32_t (&x)[S], std::integer_sequence<int, Gs...>) {
+  constexpr int TQ = tile_quads<S>();
+  ((t.quad(k * TQ + Gs) = make_uint4(4 * Gs < S ? x[4 * Gs] : 0u, 4 * Gs + 1 < S ? x[4 * Gs + 1] : 0u,
+                                     4 * Gs + 2 < S ? x[4 * Gs + 2] : 0u, 4 * Gs + 3 < S ? x[4 * Gs + 3] : 0u)),
+   ...);
+}
+template <int S, int... Gs>
+__device__ __forceinline__ void d4r_tile_load(const LaneScratch& t, int k, uint32_t (&x)[S], std::integer_sequence<int, Gs...>) {
+  constexpr int TQ = tile_quads<S>();
+  uint4 v[sizeof...(Gs)];
+  ((v[Gs] = t.quad(k * TQ + Gs)), ...);
+  (((4 * Gs < S ? (x[4 * Gs] = v[Gs].x) : 0u), (4 * Gs + 1 < S ? (x[4 * Gs + 1] = v[Gs].y) : 0u),
+    (4 * Gs + 2 < S ? (x[4 * Gs + 2] = v[Gs].z) : 0u), (4 * Gs + 3 < S ? (x[4 * Gs + 3] = v[Gs].w) : 0u)),
+   ...);
+}
+
+// The op list (kernels_crt.hpp) on register components; st = this pair's multiplier [A][B] in LDS.
+template <int S, class FinalB>
+__device__ __forceinline__ void d4r_run(uint32_t (&a)[S], uint32_t* st, const LaneScratch& tl, const uint32_t* __restrict__ prog,
+                                        int nprog, const uint32_t* x1, const uint32_t (&m)[S], uint32_t mprime, int tig,
+                                        FinalB&& final_b) {
   constexpr int TQ = tile_quads<S>();
   using Q = std::make_integer_sequence<int, TQ>;
-  __shared__ uint32_t lds[D4_PAIRS * D4_SLOT + S];
+  const bool odd = tig != 0;
+  const uint32_t oddmask = odd ? 0xFFFFFFFFu : 0u;
+  bool bclob = false;   // st's B half holds a product's z, not the kept multiplier
+  for (int i = 0; i <= nprog; ++i) {
+    const uint32_t op = (i < nprog) ? lane_op(prog, i) : LOP_B_CONST;
+    if (op & LOP_A_FROM_T) d4r_tile_load<S>(tl, (op >> 16) & 0xFF, a, Q{});
+    const bool sqr = (op & LOP_SQR) != 0;
+    if (sqr && (op & LOP_PREFETCH)) {
+      d4_tile_load<S>(tl, (op >> 8) & 0xFF, st + tig * S, Q{});   // the next MUL's multiplier (B_READY)
+      bclob = false;
+    }
+    uint64_t P[S];
+    if (sqr) {
+#pragma unroll
+      for (int j = 0; j < S; ++j) P[j] = odd ? (uint64_t)x1[j] : 0ull;
+      d4r_sqr_pass<S>(P, a, tig, m, mprime, odd, std::make_integer_sequence<int, S>{});
+      lane::normalize<S>(P, a);
+    } else {
+      if (op & LOP_B_CONST) {
+        d4_fence();
+        final_b(st + tig * S);
+        d4_fence();
+      } else if (!(op & LOP_B_READY)) {
+        d4_tile_load<S>(tl, (op >> 8) & 0xFF, st + tig * S, Q{});
+      } else if (bclob) {
+        d4_tile_load<S>(tl, D4R_KEPT, st + tig * S, Q{});
+      }
+      // pass A: z = REDC(A_x B_t) on the even lane, over st's B half
+#pragma unroll
+      for (int j = 0; j < S; ++j) P[j] = 0;
+      d4_pass<S>(P, a, st + S, 0, m, mprime, false, std::make_integer_sequence<int, S>{});
+      {
+        uint32_t z[S];
+        lane::normalize<S>(P, z);
+        d4_fence();
+        if (!odd) {
+#pragma unroll
+          for (int j = 0; j < S; ++j) st[S + j] = z[j];
+        }
+        d4_fence();
+      }
+      bclob = true;
+      // pass 1: A' = REDC(A_x A_t) (even), REDC(B_x A_t - m) + z (odd)
+#pragma unroll
+      for (int j = 0; j < S; ++j) P[j] = odd ? (uint64_t)x1[j] : 0ull;
+      d4_pass<S>(P, a, st, 0, m, mprime, odd, std::make_integer_sequence<int, S>{});
+#pragma unroll
+      for (int j = 0; j < S; ++j) P[j] += (uint64_t)(st[S + j] & oddmask);
+      lane::normalize<S>(P, a);
+    }
+    if (op & LOP_STORE) d4r_tile_store<S>(tl, op >> 24, a, Q{});
+    if (op & LOP_B_SET) {
+      d4_fence();
+#pragma unroll
+      for (int j = 0; j < S; ++j) st[tig * S + j] = a[j];
+      d4_fence();
+      d4r_tile_store<S>(tl, D4R_KEPT, a, Q{});
+      bclob = false;
+    }
+  }
+}
+
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK, 2) void k_dec4_pow(Dec4Params p) {
+  constexpr int TQ = tile_quads<S>();
+  using Q = std::make_integer_sequence<int, TQ>;
+  __shared__ uint32_t lds[D4_PAIRS * D4R_SLOT + S];
   const int half = blockIdx.y;
   const Dec4Half* H = p.halves + half;
   uint32_t m[S];
@@ -243,35 +368,28 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_dec4_pow(Dec4Params p) {
   const uint32_t mprime = H->mprime;
   const int nprog = H->nprog;
   const uint32_t* prog = H->prog;
-  uint32_t* x1 = lds + D4_PAIRS * D4_SLOT;   // (1 - R) mod p_h: the odd row's start (LDS: no SGPRs)
+  uint32_t* x1 = lds + D4_PAIRS * D4R_SLOT;   // (1 - R) mod p_h: the odd row's start (LDS: no SGPRs)
   for (int i = threadIdx.x; i < S; i += blockDim.x) x1[i] = H->X1[i];
   __syncthreads();
   const int tig = threadIdx.x & 1;
   const int pib = threadIdx.x >> 1;
-  uint32_t* sx = lds + pib * D4_SLOT;
-  uint32_t* st = sx + 2 * S;
+  uint32_t* st = lds + pib * D4R_SLOT;
   const LaneScratch tl = lane_scratch(p.scratch);
   for (long long base = (long long)blockIdx.x * D4_PAIRS; base < p.n; base += (long long)gridDim.x * D4_PAIRS) {
     const long long e = base + pib;
     const bool valid = e < p.n;
     const long long ee = valid ? e : p.n - 1;
     uint32_t a[S];
-    {
-      d4_fence();
 #pragma unroll
-      for (int i = 0; i < S; ++i) sx[tig * S + i] = p.x[((size_t)half * 2 * S + tig * S + i) * p.n + ee];
-      d4_fence();
-      d4_tile_store<S>(tl, 0, sx + tig * S, Q{});
-#pragma unroll
-      for (int i = 0; i < S; ++i) a[i] = sx[i];
-    }
-    d4_run<S>(a, sx, st, tl, prog, nprog, x1, m, mprime, tig, [&](uint32_t* dst) {   // (1, 0): leave Montgomery form
+    for (int i = 0; i < S; ++i) a[i] = p.x[((size_t)half * 2 * S + tig * S + i) * p.n + ee];
+    d4r_tile_store<S>(tl, 0, a, Q{});
+    d4r_run<S>(a, st, tl, prog, nprog, x1, m, mprime, tig, [&](uint32_t* dst) {   // (1, 0): leave Montgomery form
 #pragma unroll
       for (int j = 0; j < S; ++j) dst[j] = (tig == 0 && j == 0) ? 1u : 0u;
     });
     if (valid) {
 #pragma unroll
-      for (int i = 0; i < S; ++i) p.x[((size_t)half * 2 * S + tig * S + i) * p.n + e] = sx[tig * S + i];
+      for (int i = 0; i < S; ++i) p.x[((size_t)half * 2 * S + tig * S + i) * p.n + e] = a[i];
     }
   }
 }

@@ -116,10 +116,10 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_pe_pre(PeParams p) {
 }
 
 template <int S>
-__global__ __launch_bounds__(LANE_BLOCK, 1) void k_pe_pow(PeParams p) {
+__global__ __launch_bounds__(LANE_BLOCK, 2) void k_pe_pow(PeParams p) {
   constexpr int TQ = tile_quads<S>();
   using Q = std::make_integer_sequence<int, TQ>;
-  __shared__ uint32_t lds[D4_PAIRS * D4_SLOT + S];
+  __shared__ uint32_t lds[D4_PAIRS * D4R_SLOT + S];
   const PeConst* K = p.k;
   uint32_t m[S];
 #pragma unroll
@@ -127,31 +127,26 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_pe_pow(PeParams p) {
   const uint32_t mprime = K->mprime;
   const int nprog = K->nprog;
   const uint32_t* prog = K->prog;
-  uint32_t* x1 = lds + D4_PAIRS * D4_SLOT;
+  uint32_t* x1 = lds + D4_PAIRS * D4R_SLOT;
   for (int i = threadIdx.x; i < S; i += blockDim.x) x1[i] = K->X1[i];
   __syncthreads();
   const int tig = threadIdx.x & 1;
   const int pib = threadIdx.x >> 1;
-  uint32_t* sx = lds + pib * D4_SLOT;
-  uint32_t* st = sx + 2 * S;
+  uint32_t* st = lds + pib * D4R_SLOT;
   const LaneScratch tl = lane_scratch(p.scratch);
   for (long long base = (long long)blockIdx.x * D4_PAIRS; base < p.n; base += (long long)gridDim.x * D4_PAIRS) {
     const long long e = base + pib;
     const bool valid = e < p.n;
     const long long ee = valid ? e : p.n - 1;
-    uint32_t a[S];
-    d4_fence();
+    uint32_t a[S];   // this lane's component (kernels_dec4.hpp d4r_run: the even lane A, the odd lane B)
 #pragma unroll
-    for (int i = 0; i < S; ++i) sx[tig * S + i] = p.xw[((size_t)tig * S + i) * p.n + ee];
-    d4_fence();
-    d4_tile_store<S>(tl, 0, sx + tig * S, Q{});
-#pragma unroll
-    for (int i = 0; i < S; ++i) a[i] = sx[i];
+    for (int i = 0; i < S; ++i) a[i] = p.xw[((size_t)tig * S + i) * p.n + ee];
+    d4r_tile_store<S>(tl, 0, a, Q{});
     // the final multiplier: the pair of c0 = 1 + n M = (1, M mod n) (M < 0: n - |M|)
     // (captures by value: a reference to a register array would force it into scratch)
     const int64_t* Mp = p.M;
     const uint32_t* nlp = K->nl;
-    d4_run<S>(a, sx, st, tl, prog, nprog, x1, m, mprime, tig, [=](uint32_t* dst) {
+    d4r_run<S>(a, st, tl, prog, nprog, x1, m, mprime, tig, [=](uint32_t* dst) {
       if (tig == 0) {
 #pragma unroll
         for (int j = 0; j < S; ++j) dst[j] = j == 0 ? 1u : 0u;
@@ -171,7 +166,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_pe_pow(PeParams p) {
     });
     if (valid) {
 #pragma unroll
-      for (int i = 0; i < S; ++i) p.xw[((size_t)tig * S + i) * p.n + e] = sx[tig * S + i];
+      for (int i = 0; i < S; ++i) p.xw[((size_t)tig * S + i) * p.n + e] = a[i];
     }
   }
 }

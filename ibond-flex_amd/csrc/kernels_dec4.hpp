@@ -2,16 +2,18 @@
 //
 // p_h has 2048 bits, S = 74 limbs: a pair (A, B) with v = A + p_h B (mod p_h^2) and its two CIOS rows
 // (2 x 74 64-bit accumulators) do not fit one lane next to the operand, so the rows go to the two lanes of a
-// lane pair (element-half e: lanes 2e, 2e+1). Both lanes hold the same register operand and run the same
-// instruction stream; they differ only in the digits they stream from LDS and in one DPP step:
+// lane pair (element-half e: lanes 2e, 2e+1). Both lanes run the same instruction stream; the even lane computes
+// the A row, the odd lane the B row, taking the even lane's reduction digit q1_j by one DPP step per digit:
 //   even lane: P += a y_j + q1 p           (U = REDC(A1 A2), the A row)
 //   odd lane : P += a y_j + (LMASK - q1) + q2 p, P started at X = (1 - R) mod p_h   (the B row:
-//              REDC(a y - m) with m the even lane's reduction digits q1_j, received by DPP each digit;
-//              the LMASK - q1_j digits and X keep every accumulator non-negative, bn_pair.hpp)
-// A square (A, B)^2 streams A's digits to the even lane and 2B's to the odd one: the pair square costs
-// 2 x 2 S^2 lane-MACs, against 2 (2S)^2 for the Montgomery square over the 148 limbs of p_h^2 that the TPI = 4
-// group engine runs (k_decrypt). A product x t needs A_x B_t + B_x A_t in the B row: a second pass REDC(B_x A_t)
-// (the even lane's copy is discarded) is added to the first (< 4p, a valid operand: R >= 2^24 p_h).
+//              REDC(a y - m) with m the even lane's reduction digits q1_j; the LMASK - q1_j digits and X keep
+//              every accumulator non-negative, bn_pair.hpp)
+// k_dec4_pre (and k_pe_pre) hold the same register operand in both lanes and stream different digits from LDS. The
+// exponentiation (d4r_run, below) keeps each lane's own component in registers: a square (A, B)^2 takes A's digits
+// from the even lane by DPP (P_even += A A_j, P_odd += B 2A_j): 2 x 2 S^2 lane-MACs against 2 (2S)^2 for the
+// Montgomery square over the 148 limbs of p_h^2 that the TPI = 4 group engine runs (k_decrypt); a product x t
+// takes two passes, z = REDC(A_x B_t) on the even lane, then REDC(A_x A_t) | REDC(B_x A_t - m) + z (< 4p, a valid
+// operand: R >= 2^24 p_h).
 //
 //   k_dec4_pre  per element-half: c R as a pair (one split CIOS over the ciphertext's limbs against the
 //               constant pair of R^(K+1))
@@ -134,8 +136,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_dec4_pre(Dec4Params p) {
 // ---------------------------------------------------------------- x_h = c~^(p_h - 1), plain pair
 // The lane machine of kernels_crt.hpp (same op list: SQR, MUL with the multiplier from a tile, the constant,
 // or as set, A_FROM_T, STORE, B_SET) on split pairs. Each lane keeps its own component of every tile (the
-// even lane A, the odd lane B). A square is one split pass; a product two (pass 2 adds REDC(B_x A_t) to the
-// B row). Every pass goes through ONE d4_pass call site.
+// even lane A, the odd lane B).
 template <int S, int... Gs>
 __device__ __forceinline__ void d4_tile_store(const LaneScratch& t, int k, const uint32_t* src, std::integer_sequence<int, Gs...>) {
   constexpr int TQ = tile_quads<S>();
@@ -153,81 +154,6 @@ __device__ __forceinline__ void d4_tile_load(const LaneScratch& t, int k, uint32
     (4 * Gs + 2 < S ? (dst[4 * Gs + 2] = v[Gs].z) : 0u), (4 * Gs + 3 < S ? (dst[4 * Gs + 3] = v[Gs].w) : 0u)),
    ...);
   d4_fence();
-}
-
-// The op list on split pairs: x = (a = A in registers, sx = [A][B] in LDS, each lane's component in its
-// tiles); st = the multiplier. final_b(st + tig S) writes this lane's component of the final multiplier
-// (LOP_B_CONST). Every pass goes through ONE d4_pass call site.
-template <int S, class FinalB>
-__device__ __forceinline__ void d4_run(uint32_t (&a)[S], uint32_t* sx, uint32_t* st, const LaneScratch& tl,
-                                       const uint32_t* __restrict__ prog, int nprog, const uint32_t* x1,
-                                       const uint32_t (&m)[S], uint32_t mprime, int tig, FinalB&& final_b) {
-  constexpr int TQ = tile_quads<S>();
-  using Q = std::make_integer_sequence<int, TQ>;
-  const bool odd = tig != 0;
-  for (int i = 0; i <= nprog; ++i) {
-    const uint32_t op = (i < nprog) ? lane_op(prog, i) : LOP_B_CONST;
-    if (op & LOP_A_FROM_T) {
-      d4_tile_load<S>(tl, (op >> 16) & 0xFF, sx + tig * S, Q{});
-#pragma unroll
-      for (int j = 0; j < S; ++j) a[j] = sx[j];
-    }
-    const bool sqr = (op & LOP_SQR) != 0;
-    if (sqr && (op & LOP_PREFETCH)) d4_tile_load<S>(tl, (op >> 8) & 0xFF, st + tig * S, Q{});   // next MUL's (B_READY)
-    if (!sqr) {   // the multiplier -> st
-      if (op & LOP_B_CONST) {
-        d4_fence();
-        final_b(st + tig * S);
-        d4_fence();
-      } else if (!(op & LOP_B_READY)) {
-        d4_tile_load<S>(tl, (op >> 8) & 0xFF, st + tig * S, Q{});
-      }
-    }
-    for (int ps = 0; ps < (sqr ? 1 : 2); ++ps) {
-      const bool second = ps == 1;
-      uint64_t P[S];
-#pragma unroll
-      for (int j = 0; j < S; ++j) P[j] = (odd && !second) ? (uint64_t)x1[j] : 0ull;
-      const uint32_t* dig = sqr ? sx + tig * S : second ? st : st + tig * S;
-      d4_pass<S>(P, a, dig, sqr ? tig : 0, m, mprime, odd && !second, std::make_integer_sequence<int, S>{});
-      uint32_t y[S];
-      lane::normalize<S>(P, y);
-      if (!second) {
-        d4_fence();
-        if (!sqr) {
-#pragma unroll
-          for (int j = 0; j < S; ++j) a[j] = sx[S + j];   // B_x: pass 2's operand
-        }
-        d4_fence();
-#pragma unroll
-        for (int j = 0; j < S; ++j) sx[tig * S + j] = y[j];
-        d4_fence();
-      } else {
-        uint32_t c = 0;
-#pragma unroll
-        for (int j = 0; j < S; ++j) {   // B row += B_x A_t (< 4p)
-          const uint32_t v = sx[S + j] + y[j] + c;
-          y[j] = v & lane::LMASK;
-          c = v >> lane::LB;
-        }
-        d4_fence();
-        if (odd) {
-#pragma unroll
-          for (int j = 0; j < S; ++j) sx[S + j] = y[j];
-        }
-        d4_fence();
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < S; ++j) a[j] = sx[j];
-    if (op & LOP_STORE) d4_tile_store<S>(tl, op >> 24, sx + tig * S, Q{});
-    if (op & LOP_B_SET) {
-      d4_fence();
-#pragma unroll
-      for (int j = 0; j < S; ++j) st[tig * S + j] = sx[tig * S + j];
-      d4_fence();
-    }
-  }
 }
 
 // ---- k_dec4_pow: the components in registers (round 3)

@@ -139,6 +139,111 @@ static PyObject* g_powmod(PyObject* self, PyObject* const* args, Py_ssize_t narg
   return from_mpz(T);
 }
 
+/* scalar_pow(c, k, m, neg): c^k mod m (neg: (c^k)^-1 mod m == (c^-1)^k, the reference's inverse trick,
+ * encrypted_number.py:99-106) for 0 <= k < 2^SQ_BITS -- the multiplication of a ciphertext by an encoded scalar
+ * (encrypted_number.py:86-113) and the exponent alignment (:115-127). A ciphertext multiplied by several scalars
+ * (HE_OTP_LR's enc.dot(features), he_otp_lr_ft1/train.py:160: every element times six feature columns) keeps the
+ * table of its squarings c^(2^j): from its second multiplication on, c^k costs popcount(k) products instead of an
+ * mpz_powm (~bits(k) squarings). A ciphertext seen once takes mpz_powm: a table would not pay for one use. Keys are
+ * the int objects themselves (a strong reference is held while cached, so an address is never reused by another
+ * int); the modulus is compared by value. Same values as mpz_powm / mpz_invert. */
+#define SQ_BITS 64
+#define SQ_CACHE 64
+#define SQ_SEEN 256
+typedef struct {
+  PyObject* key;
+  mpz_t mod;
+  int nsq;                 /* squarings held: sq[0 .. nsq) = c^(2^j) mod m */
+  mpz_t sq[SQ_BITS];
+  unsigned long long used;
+} SqEntry;
+static SqEntry sqc[SQ_CACHE];
+static const PyObject* sq_seen[SQ_SEEN];
+static int sq_seen_at = 0;
+static unsigned long long sq_clock = 0;
+
+static SqEntry* sq_find(PyObject* key, const mpz_t m) {
+  for (int i = 0; i < SQ_CACHE; ++i)
+    if (sqc[i].key == key && mpz_cmp(sqc[i].mod, m) == 0) return &sqc[i];
+  return NULL;
+}
+static SqEntry* sq_insert(PyObject* key, const mpz_t c, const mpz_t m) {
+  int v = 0;
+  for (int i = 1; i < SQ_CACHE; ++i)
+    if (sqc[i].used < sqc[v].used) v = i;
+  SqEntry* e = &sqc[v];
+  if (!e->key) {
+    mpz_init(e->mod);
+    for (int j = 0; j < SQ_BITS; ++j) mpz_init(e->sq[j]);
+  }
+  Py_XDECREF(e->key);
+  Py_INCREF(key);
+  e->key = key;
+  mpz_set(e->mod, m);
+  mpz_mod(e->sq[0], c, m);
+  e->nsq = 1;
+  return e;
+}
+static int sq_seen_before(const PyObject* key) {
+  for (int i = 0; i < SQ_SEEN; ++i)
+    if (sq_seen[i] == key) return 1;
+  sq_seen[sq_seen_at] = key;
+  sq_seen_at = (sq_seen_at + 1) % SQ_SEEN;
+  return 0;
+}
+
+static PyObject* g_scalar_pow(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  (void)self;
+  if (nargs != 4) {
+    PyErr_SetString(PyExc_TypeError, "scalar_pow(c, k, m, neg)");
+    return NULL;
+  }
+  const int neg = PyObject_IsTrue(args[3]);
+  if (neg < 0) return NULL;
+  if (to_mpz(args[1], B) || to_mpz(args[2], C)) return NULL;
+  if (mpz_sgn(C) <= 0 || mpz_sgn(B) < 0 || mpz_sizeinbase(B, 2) > SQ_BITS) {
+    PyErr_SetString(PyExc_ValueError, "scalar_pow: 0 <= k < 2^64 and m > 0");
+    return NULL;
+  }
+  SqEntry* e = sq_find(args[0], C);
+  if (!e && !sq_seen_before(args[0])) {
+    if (to_mpz(args[0], A)) return NULL;
+    mpz_powm(T, A, B, C);
+  } else {
+    if (!e) {
+      if (to_mpz(args[0], A)) return NULL;
+      e = sq_insert(args[0], A, C);
+    }
+    e->used = ++sq_clock;
+    const int bits = mpz_sgn(B) ? (int)mpz_sizeinbase(B, 2) : 0;
+    for (; e->nsq < bits; ++e->nsq) {
+      mpz_mul(T, e->sq[e->nsq - 1], e->sq[e->nsq - 1]);
+      mpz_mod(e->sq[e->nsq], T, C);
+    }
+    int first = 1;
+    for (int j = 0; j < bits; ++j) {
+      if (!mpz_tstbit(B, j)) continue;
+      if (first) {
+        mpz_set(A, e->sq[j]);
+        first = 0;
+      } else {
+        mpz_mul(T, A, e->sq[j]);
+        mpz_mod(A, T, C);
+      }
+    }
+    if (first) mpz_set_ui(A, 1);
+    mpz_mod(T, A, C);   /* 1 mod 1 == 0, as mpz_powm */
+  }
+  if (neg) {
+    if (!mpz_invert(A, T, C)) {
+      PyErr_SetString(PyExc_ZeroDivisionError, "invert(a, b) no inverse exists");
+      return NULL;
+    }
+    return from_mpz(A);
+  }
+  return from_mpz(T);
+}
+
 /* invert(a, b) (gmpy_math.py:66-74): ZeroDivisionError when no inverse exists */
 static PyObject* g_invert(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
   (void)self;
@@ -497,6 +602,7 @@ static PyMethodDef methods[] = {
     {"mulmod", (PyCFunction)(void (*)(void))g_mulmod, METH_FASTCALL, "(a * b) % c"},
     {"powmod", (PyCFunction)(void (*)(void))g_powmod, METH_FASTCALL, "a ** b % c (GMP mpz_powm)"},
     {"invert", (PyCFunction)(void (*)(void))g_invert, METH_FASTCALL, "a^-1 mod b"},
+    {"scalar_pow", (PyCFunction)(void (*)(void))g_scalar_pow, METH_FASTCALL, "c^k mod m (neg: inverse) with cached squarings"},
     {"mul", (PyCFunction)(void (*)(void))g_mul, METH_FASTCALL, "a * b"},
     {NULL, NULL, 0, NULL}};
 

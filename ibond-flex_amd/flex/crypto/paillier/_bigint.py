@@ -39,6 +39,15 @@ def powmod(a: int, b: int, c: int) -> int:           # gmpy_math.py:51-63
     return pow(a, b, c)
 
 
+def scalar_pow(c: int, k: int, m: int, neg: bool = False) -> int:
+    """c^k mod m, or (c^-1)^k mod m when neg -- powmod(c, k, m) / powmod(invert(c, m), k, m) as
+    encrypted_number.py:99-109 computes them, for 0 < k < 2^64. On the GMP binding a ciphertext that is
+    multiplied again keeps its table of squarings (hostgmp.c scalar_pow): same values, fewer products."""
+    if _gmp is not None and m >= POWMOD_GMP_SIZE and 0 <= k < POWMOD_GMP_SIZE:
+        return _gmp.scalar_pow(c, k, m, neg)
+    return powmod(invert(c, m), k, m) if neg else powmod(c, k, m)
+
+
 def invert(a: int, b: int) -> int:                   # gmpy_math.py:66-74
     if _gmp is not None:
         return _gmp.invert(a, b)

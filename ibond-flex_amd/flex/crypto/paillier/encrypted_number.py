@@ -73,12 +73,13 @@ class PaillierEncryptedNumber(object):
         plaintext = encode.encoding
         if plaintext < 0 or plaintext >= self.public_key.n:
             raise ValueError("Scalar out of bounds: %i" % plaintext)
+        # (c^-1)^(n - plaintext) for the "very large" plaintexts, c^plaintext otherwise; scalar_pow shares the
+        # squarings of a ciphertext multiplied by several scalars (enc.dot(features))
         if plaintext >= self.public_key.n - self.public_key.max_int:
-            neg_c = gmpy_math.invert(self.ciphertext(False), self.public_key.nsquare)
-            neg_scalar = self.public_key.n - plaintext
-            ciphertext = gmpy_math.powmod(neg_c, neg_scalar, self.public_key.nsquare)
+            ciphertext = gmpy_math.scalar_pow(self.ciphertext(False), self.public_key.n - plaintext,
+                                              self.public_key.nsquare, True)
         else:
-            ciphertext = gmpy_math.powmod(self.ciphertext(False), plaintext, self.public_key.nsquare)
+            ciphertext = gmpy_math.scalar_pow(self.ciphertext(False), plaintext, self.public_key.nsquare)
         exponent = self.exponent + encode.exponent
         return PaillierEncryptedNumber(self.public_key, ciphertext, exponent)
 

@@ -207,6 +207,31 @@ def test_host_gmp_binding_matches_python_ints():
             assert _bigint.invert(a, c) == inv
 
 
+def test_scalar_pow_with_cached_squarings():
+    """hostgmp.c scalar_pow (encrypted_number.__mul__): c^k and (c^-1)^k mod m equal Python's pow through the
+    first use (mpz_powm), the table build on the second and the table afterwards, across cache evictions and for
+    one int object under two moduli."""
+    import math
+    import random
+    from flex.crypto.paillier import _bigint, _gmp
+    rnd = random.Random(11)
+    mods = [rnd.getrandbits(b) | 1 | (1 << (b - 1)) for b in (2048, 4096)]
+    cs = [rnd.getrandbits(2040) | 1 for _ in range(80)]       # > the cache's 64 entries: evictions
+    for rep in range(4):
+        for c in cs:
+            for m in mods:
+                k = rnd.getrandbits(rnd.randint(0, 64))
+                assert _gmp.scalar_pow(c, k, m, False) == pow(c, k, m)
+                if k and math.gcd(c, m) == 1:
+                    assert _gmp.scalar_pow(c, k, m, True) == pow(pow(c, -1, m), k, m)
+                assert _bigint.scalar_pow(c, k, m, False) == pow(c, k, m)
+    assert _gmp.scalar_pow(cs[0], 0, mods[0], False) == 1
+    with pytest.raises(ValueError):
+        _gmp.scalar_pow(cs[0], 1 << 64, mods[0], False)
+    with pytest.raises(ZeroDivisionError):
+        _gmp.scalar_pow(mods[0] * 3, 5, mods[0] * 9, True)
+
+
 def test_bulk_word_conversions_and_object_construction():
     """words_to_ints (threaded digit fill), ints_to_words and make_numbers (slots set in C, untracked by the
     cyclic collector) give the same values and objects as int.from_bytes / PaillierEncryptedNumber._make."""

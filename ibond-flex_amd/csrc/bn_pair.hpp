@@ -13,10 +13,12 @@
 // register footprint of a 2S-limb lane product (A, B: 2S; two accumulators: 4S VGPRs).
 //
 // Bounds (checked limb by limb in tools/pair_model.py): with R > 8p and operands < 2p, U < 2p and
-// REDC(.) < (A1 B2 + A2 B1) / R + p < 2p. The second accumulator is SIGNED: subtracting q1_j can take a
-// position below zero, so its carries are arithmetic shifts; its final value is >= 0 because
-// (Z + q2 p) / R > -m / R > -1. It receives per digit at most two a*b products and one q2*p product
-// (< 2^57 + 2^57 + 2^56 for a square's doubled digit), so S * 1.25 * 2^58 < 2^63 for S <= 37.
+// REDC(.) < (A1 B2 + A2 B1) / R + p < 2p. The subtraction of q1_j is never executed: the second row picks q2_j
+// so that its position J becomes q1_j (mod 2^28) instead of 0 -- q2_j = (P2_J - q1_j) mprime -- and the shift
+// that retires position J drops those low 28 bits, which is exactly the subtraction (its value is >= 0 because
+// (Z + q2 p) / R > -m / R > -1). So both rows stay non-negative with unsigned carries, and no 64-bit subtraction
+// (two instructions and a carry hazard) runs per digit. A position receives per digit at most two a*b products
+// and one q2*p product (< 2^57 + 2^57 + 2^56 for a square's doubled digit), so S * 1.25 * 2^58 < 2^64 for S <= 37.
 #pragma once
 #include "bn_lane.hpp"
 
@@ -37,19 +39,18 @@ __device__ __forceinline__ void pin2(uint64_t (&P1)[S], uint64_t (&P2)[S]) {
     if (i != Z) asm volatile("" : "+v"(P1[i]), "+v"(P2[i]));
 }
 
-// reductions of digit J: P1 by q1 (its own digit), P2 by q2 after subtracting q1 at position J
+// reductions of digit J: P1 by q1 (its own digit), P2 by q2 with q1 dropped at position J (above)
 template <int S, int J>
 __device__ __forceinline__ void red2(uint64_t (&P1)[S], uint64_t (&P2)[S], const uint32_t (&m)[S], uint32_t mprime) {
   const uint32_t q1 = ((uint32_t)P1[J] * mprime) & LMASK;
-  P2[J] -= (uint64_t)q1;
-  const uint32_t q2 = ((uint32_t)P2[J] * mprime) & LMASK;
+  const uint32_t q2 = (((uint32_t)P2[J] - q1) * mprime) & LMASK;
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     P1[(i + J) % S] += (uint64_t)q1 * m[i];
     P2[(i + J) % S] += (uint64_t)q2 * m[i];
   }
   P1[(J + 1) % S] += P1[J] >> LB;
-  P2[(J + 1) % S] += (uint64_t)((int64_t)P2[J] >> LB);
+  P2[(J + 1) % S] += P2[J] >> LB;   // its low 28 bits are q1: the subtraction of m
   P1[J] = 0;
   P2[J] = 0;
   pin2<S, J>(P1, P2);
@@ -79,17 +80,6 @@ __device__ __forceinline__ void sqr_digit(uint64_t (&P1)[S], uint64_t (&P2)[S], 
 }
 
 template <int S>
-__device__ __forceinline__ void normalize_signed(const uint64_t (&P)[S], uint32_t (&r)[S]) {
-  int64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < S; ++i) {
-    const int64_t v = (int64_t)P[i] + c;
-    r[i] = lane::limb32((uint64_t)v);
-    c = v >> LB;
-  }
-}
-
-template <int S>
 __device__ __forceinline__ void zero2(uint64_t (&P1)[S], uint64_t (&P2)[S]) {
 #pragma unroll
   for (int i = 0; i < S; ++i) P1[i] = P2[i] = 0;
@@ -107,7 +97,7 @@ __device__ __forceinline__ void mont_sqr(uint32_t (&A)[S], uint32_t (&B)[S], con
   zero2<S>(P1, P2);
   sqr_all<S>(P1, P2, A, B, m, mprime, std::make_integer_sequence<int, S>{});
   lane::normalize<S>(P1, A);
-  normalize_signed<S>(P2, B);
+  lane::normalize<S>(P2, B);
 }
 
 // (A, B) <- (A, B) (A2, B2) R^-1 with the multiplier's digit pair J from get(J) (a uint2: x = A2[J],
@@ -130,7 +120,7 @@ __device__ __forceinline__ void mont_mul(uint32_t (&A)[S], uint32_t (&B)[S], Get
   zero2<S>(P1, P2);
   mul_all<S>(P1, P2, A, B, get, m, mprime, std::make_integer_sequence<int, S>{});
   lane::normalize<S>(P1, A);
-  normalize_signed<S>(P2, B);
+  lane::normalize<S>(P2, B);
 }
 
 // ---- products by a pair (a, 0): a factored table row (kernels_fbp.hpp)
@@ -138,7 +128,7 @@ __device__ __forceinline__ void mont_mul(uint32_t (&A)[S], uint32_t (&B)[S], Get
 // over the digits of a -- U = REDC(A a), handing each reduction digit q1_j to put(j, q1_j), then REDC(B a - m),
 // m = sum q1_j 2^(28 j), with gb(j) returning (a_j, q1_j) -- so that only one 64-bit accumulator row (2S VGPRs)
 // is live at a time; the caller keeps the digits where it has room. Bounds as above (the second pass is the
-// signed row of the lock-step product with one product per position and digit fewer).
+// second row of the lock-step product with one product per position and digit fewer).
 template <int S, int Z>
 __device__ __forceinline__ void pin1(uint64_t (&P)[S]) {
 #pragma unroll
@@ -168,11 +158,10 @@ __device__ __forceinline__ void a0_step_b(uint64_t (&P)[S], const uint32_t (&B)[
   const uint2 d = get(std::integral_constant<int, J>{});   // (a_J, q1_J)
 #pragma unroll
   for (int i = 0; i < S; ++i) P[(i + J) % S] += (uint64_t)B[i] * d.x;
-  P[J] -= (uint64_t)d.y;
-  const uint32_t q2 = ((uint32_t)P[J] * mprime) & LMASK;
+  const uint32_t q2 = (((uint32_t)P[J] - d.y) * mprime) & LMASK;
 #pragma unroll
   for (int i = 0; i < S; ++i) P[(i + J) % S] += (uint64_t)q2 * m[i];
-  P[(J + 1) % S] += (uint64_t)((int64_t)P[J] >> LB);
+  P[(J + 1) % S] += P[J] >> LB;   // its low 28 bits are q1_J: the subtraction of m
   P[J] = 0;
   pin1<S, J>(P);
   __builtin_amdgcn_sched_barrier(0);
@@ -201,7 +190,7 @@ __device__ __forceinline__ void mont_mul_a0(uint32_t (&A)[S], uint32_t (&B)[S], 
 #pragma unroll
   for (int i = 0; i < S; ++i) P[i] = 0;
   a0_pass_b<S>(P, B, gb, m, mprime, std::make_integer_sequence<int, S>{});
-  normalize_signed<S>(P, B);
+  lane::normalize<S>(P, B);
 }
 
 // (A, B) with A, B < 2p -> the canonical pair A < p, B < p of the same residue mod p^2

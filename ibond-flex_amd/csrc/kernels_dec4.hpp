@@ -5,9 +5,8 @@
 // lane pair (element-half e: lanes 2e, 2e+1). Both lanes run the same instruction stream; the even lane computes
 // the A row, the odd lane the B row, taking the even lane's reduction digit q1_j by one DPP step per digit:
 //   even lane: P += a y_j + q1 p           (U = REDC(A1 A2), the A row)
-//   odd lane : P += a y_j + (LMASK - q1) + q2 p, P started at X = (1 - R) mod p_h   (the B row:
-//              REDC(a y - m) with m the even lane's reduction digits q1_j; the LMASK - q1_j digits and X keep
-//              every accumulator non-negative, bn_pair.hpp)
+//   odd lane : P += a y_j + q2 p, q2 = (P_J - q1) mprime   (the B row: REDC(a y - m) with m the even lane's
+//              reduction digits q1_j, which the retiring shift drops instead of subtracting them, bn_pair.hpp)
 // k_dec4_pre (and k_pe_pre) hold the same register operand in both lanes and stream different digits from LDS. The
 // exponentiation (d4r_run, below) keeps each lane's own component in registers: a square (A, B)^2 takes A's digits
 // from the even lane by DPP (P_even += A A_j, P_odd += B 2A_j): 2 x 2 S^2 lane-MACs against 2 (2S)^2 for the
@@ -63,17 +62,16 @@ __device__ __forceinline__ void d4_step(uint64_t (&P)[S], const uint32_t (&a)[S]
   for (int i = 0; i < S; ++i) P[(i + J) % S] += (uint64_t)a[i] * y;
   const uint32_t q0 = ((uint32_t)P[J] * mprime) & lane::LMASK;
   const uint32_t q1 = __builtin_amdgcn_update_dpp(0u, q0, 0xA0, 0xF, 0xF, false);   // quad_perm [0,0,2,2]: even lane's q
-  P[J] += subq ? (uint64_t)(lane::LMASK - q1) : 0ull;
-  const uint32_t q = ((uint32_t)P[J] * mprime) & lane::LMASK;
+  const uint32_t q = (((uint32_t)P[J] - (subq ? q1 : 0u)) * mprime) & lane::LMASK;
 #pragma unroll
   for (int i = 0; i < S; ++i) P[(i + J) % S] += (uint64_t)q * m[i];
-  P[(J + 1) % S] += P[J] >> lane::LB;
+  P[(J + 1) % S] += P[J] >> lane::LB;   // B row: the low 28 bits are q1, dropped (bn_pair.hpp)
   P[J] = 0;
   lane::pin<S>(P);
   __builtin_amdgcn_sched_barrier(0);
 }
 // S digits dig[0..S) (shifted left by sh) against the register operand a; subq: this lane is the B row of a
-// pair pass (it takes LMASK - q1 of its even neighbour at each digit)
+// pair pass (it drops q1 of its even neighbour at each digit)
 template <int S, int... Js>
 __device__ __forceinline__ void d4_pass(uint64_t (&P)[S], const uint32_t (&a)[S], const uint32_t* __restrict__ dig, int sh,
                                         const uint32_t (&m)[S], uint32_t mprime, bool subq, std::integer_sequence<int, Js...>) {
@@ -120,7 +118,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_dec4_pre(Dec4Params p) {
     for (int i = 0; i < S; ++i) a[i] = H->cK[tig * S + i];
     uint64_t P[S];
 #pragma unroll
-    for (int i = 0; i < S; ++i) P[i] = odd ? (uint64_t)H->XK[i] : 0ull;
+    for (int i = 0; i < S; ++i) P[i] = 0;
 #pragma unroll 1
     for (int k = 0; k < p.kchunks; ++k)
       d4_pass<S>(P, a, sx + k * S, 0, m, mprime, odd, std::make_integer_sequence<int, S>{});
@@ -162,7 +160,7 @@ __device__ __forceinline__ void d4_tile_load(const LaneScratch& t, int k, uint32
 // (P_even += A A_j, P_odd += B 2A_j). A product x t (t in the LDS multiplier st = [A_t][B_t]) runs two passes:
 //   pass A: P += a B_t[j] on both lanes; the even lane's z = REDC(A_x B_t) is written over st's B half (the odd
 //           lane's product is discarded);
-//   pass 1: P += a A_t[j] with the split reduction (odd lane: LMASK - q1 and the start X); then the odd lane adds
+//   pass 1: P += a A_t[j] with the split reduction (the odd lane drops the even lane's q1); then the odd lane adds
 //           z, so B' = REDC(B_x A_t - m) + REDC(A_x B_t) < 4p and the even lane's A' = REDC(A_x A_t).
 // Only the multiplier lives in LDS (2S words per lane pair instead of 4S): two blocks of 256 lanes per CU, two
 // waves per SIMD. A multiplier kept across products (LOP_B_READY without a prefetch: the table's x~^2) has its B
@@ -180,7 +178,7 @@ __device__ __forceinline__ void d4r_sqr_step(uint64_t (&P)[S], const uint32_t (&
   for (int i = 0; i < S; ++i) P[(i + J) % S] += (uint64_t)a[i] * y;
   const uint32_t q0 = ((uint32_t)P[J] * mprime) & lane::LMASK;
   const uint32_t q1 = __builtin_amdgcn_update_dpp(0u, q0, 0xA0, 0xF, 0xF, false);
-  P[J] += odd ? (uint64_t)(lane::LMASK - q1) : 0ull;
+  P[J] += odd ? (uint64_t)(lane::LMASK - q1) : 0ull;   // (the odd row started at (1 - R) mod p: non-negative)
   const uint32_t q = ((uint32_t)P[J] * mprime) & lane::LMASK;
 #pragma unroll
   for (int i = 0; i < S; ++i) P[(i + J) % S] += (uint64_t)q * m[i];
@@ -263,7 +261,7 @@ __device__ __forceinline__ void d4r_run(uint32_t (&a)[S], uint32_t* st, const La
       bclob = true;
       // pass 1: A' = REDC(A_x A_t) (even), REDC(B_x A_t - m) + z (odd)
 #pragma unroll
-      for (int j = 0; j < S; ++j) P[j] = odd ? (uint64_t)x1[j] : 0ull;
+      for (int j = 0; j < S; ++j) P[j] = 0;
       d4_pass<S>(P, a, st, 0, m, mprime, odd, std::make_integer_sequence<int, S>{});
 #pragma unroll
       for (int j = 0; j < S; ++j) P[j] += (uint64_t)(st[S + j] & oddmask);
@@ -294,7 +292,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_dec4_pow(Dec4Params p) {
   const uint32_t mprime = H->mprime;
   const int nprog = H->nprog;
   const uint32_t* prog = H->prog;
-  uint32_t* x1 = lds + D4_PAIRS * D4R_SLOT;   // (1 - R) mod p_h: the odd row's start (LDS: no SGPRs)
+  uint32_t* x1 = lds + D4_PAIRS * D4R_SLOT;   // (1 - R) mod p_h: the odd row's start in squares (LDS: no SGPRs)
   for (int i = threadIdx.x; i < S; i += blockDim.x) x1[i] = H->X1[i];
   __syncthreads();
   const int tig = threadIdx.x & 1;

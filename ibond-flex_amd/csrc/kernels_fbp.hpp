@@ -193,6 +193,113 @@ struct FbpAQReader {
   }
 };
 
+// ---- the same two readers on 16-byte LDS reads (ds_read_b128: four words, or four q1 digits, per read)
+typedef uint32_t fbp_u32x4 __attribute__((ext_vector_type(4)));
+template <int OFF>
+__device__ __forceinline__ fbp_u32x4 lds_quad_rd(uint32_t addr) {
+  fbp_u32x4 v;
+  if constexpr (OFF < 65536) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+  else asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr + 65536u), "i"(OFF - 65536) : "memory");
+  return v;
+}
+template <int C>
+__device__ __forceinline__ uint32_t quad_word(const fbp_u32x4& v) {
+  if constexpr (C == 0) return v.x;
+  else if constexpr (C == 1) return v.y;
+  else if constexpr (C == 2) return v.z;
+  else return v.w;
+}
+// 28-bit digit J of the words held in quads qa (digit J needs words lo(J), hi(J))
+template <int PW, int J>
+__device__ __forceinline__ uint32_t fbp_quad_digit(const fbp_u32x4 (&qa)[PW / 4]) {
+  constexpr int l = (28 * J) >> 5, sh = (28 * J) & 31;
+  const uint32_t wl = quad_word<l % 4>(qa[l / 4]);
+  if constexpr (sh + 28 <= 32) return (wl >> sh) & lane::LMASK;
+  else if constexpr (l + 1 < PW) return __builtin_amdgcn_alignbit(quad_word<(l + 1) % 4>(qa[(l + 1) / 4]), wl, sh) & lane::LMASK;
+  else return wl >> sh;
+}
+
+template <int S, int PW, int DQ>
+struct FbpQuadSched {
+  static constexpr int NQA = PW / 4;   // quads of a
+  static constexpr int NQQ = (S + 3) / 4;   // quads of the q1 record
+  static constexpr int hi(int J) { return (28 * J + 27) >> 5 < PW - 1 ? (28 * J + 27) >> 5 : PW - 1; }
+  static constexpr int need(int J) { return hi(J) / 4; }
+  static constexpr int issued(int J) { return J < 0 ? -1 : (need(J) + DQ < NQA - 1 ? need(J) + DQ : NQA - 1); }
+  static constexpr int nA(int J) { return issued(J) - issued(J - 1); }
+  static constexpr int batch_of(int g) {
+    int j = 0;
+    while (issued(j) < g) ++j;
+    return j;
+  }
+};
+
+// pass 1: a quads issued DQ quads ahead; one q1 write per digit (FbpQPut) follows each digit's wait
+template <int S, int PW, int DQ>
+struct FbpAQuadReader {
+  using Sc = FbpQuadSched<S, PW, DQ>;
+  uint32_t addr;
+  fbp_u32x4 qa[PW / 4];
+  static constexpr int before(int J) { return Sc::issued(J - 1) + 1 + J; }
+  static constexpr int pos(int g) { return before(Sc::batch_of(g)) + (g - Sc::issued(Sc::batch_of(g) - 1) - 1); }
+  template <int G0, int... Gs>
+  __device__ __forceinline__ void issue(std::integer_sequence<int, Gs...>) {
+    ((qa[G0 + Gs] = lds_quad_rd<(G0 + Gs) * LANE_BLOCK * 16>(addr)), ...);
+  }
+  template <int J>
+  __device__ __forceinline__ uint32_t operator()(std::integral_constant<int, J>) {
+    constexpr int from = Sc::issued(J - 1) + 1, to = Sc::issued(J);
+    issue<from>(std::make_integer_sequence<int, (to >= from ? to - from + 1 : 0)>{});
+    constexpr int gl = ((28 * J) >> 5) / 4, gh = Sc::need(J);
+    constexpr int pending = before(J) + Sc::nA(J) - 1 - pos(gh);
+    static_assert(pending >= 0 && pending <= 15, "lgkmcnt range");
+    if constexpr (J == 0 || gh > Sc::need(J - 1)) {   // a quad not waited for yet (quads land in order)
+      if constexpr (gl == gh) asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(qa[gl]) : "i"(pending));
+      else asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(qa[gl]), "+v"(qa[gh]) : "i"(pending));
+    }
+    return fbp_quad_digit<PW, J>(qa);
+  }
+};
+
+// pass 2: the a quads as in pass 1, and the q1 record by quads (quad 0 first, quad Q + 1 at digit 4 Q)
+template <int S, int PW, int DQ>
+struct FbpAQQuadReader {
+  using Sc = FbpQuadSched<S, PW, DQ>;
+  uint32_t addr;
+  fbp_u32x4 qa[PW / 4], qq[Sc::NQQ];
+  static constexpr int nq(int J) { return (J == 0 ? 1 : 0) + ((J % 4 == 0 && J / 4 + 1 < Sc::NQQ) ? 1 : 0); }
+  static constexpr int before(int J) {
+    int s = 0;
+    for (int t = 0; t < J; ++t) s += Sc::nA(t) + nq(t);
+    return s;
+  }
+  static constexpr int pos_a(int g) {
+    const int jb = Sc::batch_of(g);
+    return before(jb) + (jb == 0 ? 1 : 0) + (g - Sc::issued(jb - 1) - 1);
+  }
+  static constexpr int pos_q(int Q) { return Q == 0 ? 0 : before(4 * (Q - 1)) + (Q == 1 ? 1 : 0) + Sc::nA(4 * (Q - 1)); }
+  template <int G0, int... Gs>
+  __device__ __forceinline__ void issue(std::integer_sequence<int, Gs...>) {
+    ((qa[G0 + Gs] = lds_quad_rd<(G0 + Gs) * LANE_BLOCK * 16>(addr)), ...);
+  }
+  template <int J>
+  __device__ __forceinline__ uint2 operator()(std::integral_constant<int, J>) {
+    if constexpr (J == 0) qq[0] = lds_quad_rd<FbpLds<S, PW>::q_off(0)>(addr);
+    constexpr int from = Sc::issued(J - 1) + 1, to = Sc::issued(J);
+    issue<from>(std::make_integer_sequence<int, (to >= from ? to - from + 1 : 0)>{});
+    if constexpr (J % 4 == 0 && J / 4 + 1 < Sc::NQQ) qq[J / 4 + 1] = lds_quad_rd<FbpLds<S, PW>::q_off(J + 4)>(addr);
+    constexpr int gl = ((28 * J) >> 5) / 4, gh = Sc::need(J), Q = J / 4;
+    constexpr int need = pos_a(gh) > pos_q(Q) ? pos_a(gh) : pos_q(Q);
+    constexpr int pending = before(J) + Sc::nA(J) + nq(J) - 1 - need;
+    static_assert(pending >= 0 && pending <= 15, "lgkmcnt range");
+    if constexpr (J == 0 || gh > Sc::need(J - 1) || J % 4 == 0) {   // a new a quad or a new q1 quad
+      if constexpr (gl == gh) asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(qa[gl]), "+v"(qq[Q]) : "i"(pending));
+      else asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(qa[gl]), "+v"(qa[gh]), "+v"(qq[Q]) : "i"(pending));
+    }
+    return make_uint2(fbp_quad_digit<PW, J>(qa), quad_word<J % 4>(qq[Q]));
+  }
+};
+
 // the b R words of this lane's row in LDS (quads PW/4 .. PW/2 - 1) into the running sum bs (PW words) + bc
 template <int PW>
 __device__ __forceinline__ void fbp_bsum_add(uint32_t (&bs)[PW], uint32_t& bc, const uint4* lrow) {
@@ -283,6 +390,12 @@ __device__ __forceinline__ void fbp_store_w(const uint32_t (&A)[S], const uint32
 #ifndef FBP_QD
 #define FBP_QD 2   // q1 digits read ahead in the second pass
 #endif
+#ifndef FBP_QUADS
+#define FBP_QUADS 1   // row words and q1 digits by 16-byte reads (FbpAQuadReader), or one word per read
+#endif
+#ifndef FBP_DQ
+#define FBP_DQ 1   // quads read ahead of the quad a digit needs
+#endif
 template <int S>
 __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp(FbpParams p) {
   using G = FbpGeom<S>;
@@ -330,8 +443,13 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp(FbpParams p) {
     for (int k = 0; k < K; ++k) {
       lds_dma_wait();                                     // row k landed, digit k+2 loaded
       fbp_bsum_add<PW>(bs, bc, lbuf + threadIdx.x);
+#if FBP_QUADS
+      pair::mont_mul_a0<S>(A, B, FbpAQuadReader<S, PW, FBP_DQ>{addr0}, FbpQPut<S, PW>{addr0},
+                           FbpAQQuadReader<S, PW, FBP_DQ>{addr0}, m, mprime);
+#else
       pair::mont_mul_a0<S>(A, B, FbpAReader<S, PW, FBP_RD>{addr0}, FbpQPut<S, PW>{addr0},
                            FbpAQReader<S, PW, FBP_RD, FBP_QD>{addr0}, m, mprime);
+#endif
       if (k + 1 < K) {                                    // (every read of the row completed inside)
         const uint32_t dk1 = dn;
         dn = dn2;

@@ -186,7 +186,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_dec_pre_pair(DecPairPreParams p)
     }
     uint32_t xa[S], xb[S];
     lane::normalize<S>(P1, xa);
-    pair::normalize_signed<S>(P2, xb);
+    lane::normalize<S>(P2, xb);
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       p.out[((size_t)half * 2 * S + j) * p.n + i] = xa[j];

@@ -103,7 +103,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_pe_pre(PeParams p) {
     for (int i = 0; i < S; ++i) a[i] = K->cK[tig * S + i];
     uint64_t P[S];
 #pragma unroll
-    for (int i = 0; i < S; ++i) P[i] = odd ? (uint64_t)K->XK[i] : 0ull;
+    for (int i = 0; i < S; ++i) P[i] = 0;
 #pragma unroll 1
     for (int k = 0; k < 2; ++k) d4_pass<S>(P, a, sx + k * S, 0, m, mprime, odd, std::make_integer_sequence<int, S>{});
     uint32_t y[S];
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_pe_pow(PeParams p) {
   const uint32_t mprime = K->mprime;
   const int nprog = K->nprog;
   const uint32_t* prog = K->prog;
-  uint32_t* x1 = lds + D4_PAIRS * D4R_SLOT;
+  uint32_t* x1 = lds + D4_PAIRS * D4R_SLOT;   // (1 - R) mod n: the odd row's start in squares
   for (int i = threadIdx.x; i < S; i += blockDim.x) x1[i] = K->X1[i];
   __syncthreads();
   const int tig = threadIdx.x & 1;

@@ -29,7 +29,9 @@ def wrap64(v):
 
 
 def pair_mul(A1, B1, A2, B2, p, S, sqr=False):
-    """Lockstep CIOS over j: P1 <- A1 A2 (+ q1 p), P2 <- B1 A2 + A1 B2 - q1 (+ q2 p), P2 signed."""
+    """Lockstep CIOS over j: P1 <- A1 A2 (+ q1 p), P2 <- B1 A2 + A1 B2 - q1 (+ q2 p). As the kernels do
+    (bn_pair.hpp red2), q1 is not subtracted: q2 = (P2_J - q1) pinv makes position J equal q1 mod 2^28 and the
+    retiring shift drops it, so P2 stays non-negative (unsigned 64-bit accumulators)."""
     pl = limbs(p, S)
     pinv = (-pow(p, -1, 1 << LB)) % (1 << LB)
     P1 = [0] * S
@@ -53,16 +55,15 @@ def pair_mul(A1, B1, A2, B2, p, S, sqr=False):
         assert P1[J] & MASK == 0
         P1[(J + 1) % S] += P1[J] >> LB
         P1[J] = 0
-        P2[J] -= q1
-        q2 = ((P2[J] & MASK) * pinv) & MASK
+        q2 = ((((P2[J] & 0xFFFFFFFF) - q1) & 0xFFFFFFFF) * pinv) & MASK
         for i in range(S):
             P2[(i + J) % S] += q2 * pl[i]
-        assert P2[J] & MASK == 0
-        P2[(J + 1) % S] += P2[J] >> LB   # arithmetic shift (Python ints are exact)
+        assert P2[J] >= 0 and P2[J] & MASK == q1
+        P2[(J + 1) % S] += P2[J] >> LB   # drops q1: the subtraction of m
         P2[J] = 0
         mx1 = max(mx1, max(P1))
-        mx2 = max(mx2, max(abs(v) for v in P2))
-    assert mx1 < (1 << 64) and mx2 < (1 << 63), (mx1.bit_length(), mx2.bit_length())
+        mx2 = max(mx2, max(P2))
+    assert mx1 < (1 << 64) and mx2 < (1 << 64), (mx1.bit_length(), mx2.bit_length())
 
     def norm(P):
         c, r = 0, []

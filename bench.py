@@ -355,6 +355,7 @@ def main():
     grp_fb = use_fb and not use_crt          # 4096-bit keys: k_fb_digits, k_fbg, k_fbg_garner + k_fbg_fin
     fb_info = None
     fb_pair = 0
+    fb_split = False
     if use_fb:
         ctx.set_fb_window(args.fb_window)     # a dedicated encrypt GPU: the largest tables that fit its HBM
         t0 = time.perf_counter()
@@ -365,6 +366,7 @@ def main():
         setup["fixed_base_build_wall_ms"] = (time.perf_counter() - t0) * 1e3
         use_fb = ctx.fb_ready
         fb_pair = ctx.fb_pair if use_fb else 0
+        fb_split = bool(ctx.split_sampler & 1) if use_fb else False   # k_sgp (kernels_sgp.hpp) for k_fbgp
         if use_fb:
             fb_info = ctx.fixed_base_info()
             h_ms, d_ms, tbytes = ctx.fixed_base_setup()
@@ -830,6 +832,7 @@ def main():
             runs.append((time.perf_counter() - t1, cpub.stage_times()))
         wall, pst = min(runs, key=lambda r: r[0])
         bases, Kp, Wp, K0p = cpub.public_fixed_base_info()
+        pfb_k = "k_sgp" if cpub.split_sampler & 2 else "k_pfb"
         wpfb = work_pfb(nb, Kp)                     # K factored-row products mod n^2 + the correction
         # exact round trip through the key holder's decryption
         valp = torch.empty(N, dtype=torch.float64, device=dev)
@@ -839,8 +842,9 @@ def main():
         okp = bool(torch.equal(valp, x.double())) and int((stp > 1).sum().item()) == 0
         extra["public_key_fixed_base"] = {
             "value": N / wall, "unit": "encrypts/s per GPU", "elements": N,
-            "kernel": "k_pfb_digits + k_pfb + k_pe_fin", "stages_ms": dict(zip(["k_pfb_digits", "k_pfb", "k_pe_fin"], pst)),
+            "kernel": f"k_pfb_digits + {pfb_k} + k_pe_fin", "stages_ms": dict(zip(["k_pfb_digits", pfb_k, "k_pe_fin"], pst)),
             "k_pfb_int_mac_frac": N * wpfb / (pst[1] * 1e-3) / INT_MAC_PEAK if len(pst) > 1 else None,
+            "sampler": pfb_k + (" (split pairs, kernels_sgp.hpp)" if pfb_k == "k_sgp" else " (pair groups, kernels_pfb.hpp)"),
             "work_mac_per_elem": wpfb, "digits": Kp, "window": Wp, "e0_digits": K0p,
             "setup_ms": pfb_setup_ms, "table_bytes": Kp * (1 << Wp) * 512,
             "roundtrip_exact": okp,
@@ -867,6 +871,9 @@ def main():
     else:
         if grp_fb and fb_pair:
             names, works = ["k_fb_digits", "k_fbgp", "k_fbg_fin"], work_fbgp(nb, fb_info[2])
+            if fb_split:   # same tables, same count, the split-pair kernel
+                names[1] = "k_sgp"
+                works["k_sgp"] = works.pop("k_fbgp")
         elif grp_fb:
             names, works = ["k_fb_digits", "k_fbg", "k_fbg_fin"], work_fbg(nb, fb_info[2])
         elif use_crt and use_fb and fb_pair:
@@ -979,13 +986,13 @@ def main():
                    "world_size_seen": dist.get_world_size() if world > 1 else 1},
         "roofline": {"bound": "valu-int-mac", "achieved": achieved / 1e12, "peak": INT_MAC_PEAK / 1e12,
                      "unit": "TMAC/s", "frac": achieved / INT_MAC_PEAK,
-                     "traffic": load_traffic(dom, N, nb, fb_info[3] if (use_fb and dom in ("k_fb", "k_fbp", "k_fbg", "k_fbgp")) else None),
+                     "traffic": load_traffic(dom, N, nb, fb_info[3] if (use_fb and dom in ("k_fb", "k_fbp", "k_fbg", "k_fbgp", "k_sgp")) else None),
                      "kernel": dom, "kernel_ms": dom_ms,
                      "work_per_unit": (f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} products by "
                                        f"factored rows (a, 0) mod p_h^2 per half, 4 s^2 + 2 s each over s = nb/64 32-bit limbs "
                                        f"of p_h, + the c0 sum and the b-sum correction, "
-                                       f"{'kernels_fbp.hpp' if dom == 'k_fbp' else 'kernels_grp_pair.hpp'}), not SURVEY.md §8d's W_enc"
-                                       if dom in ("k_fbp", "k_fbgp") else
+                                       f"{'kernels_fbp.hpp' if dom == 'k_fbp' else 'kernels_sgp.hpp' if dom == 'k_sgp' else 'kernels_grp_pair.hpp'}), not SURVEY.md §8d's W_enc"
+                                       if dom in ("k_fbp", "k_fbgp", "k_sgp") else
                                        f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} table "
                                        f"products per half, 32-bit limbs, kernels_fb.hpp), not SURVEY.md §8d's W_enc"
                                        if dom in ("k_fb", "k_fbg") else f"{dom_work:.4g} canonical 32x32->64 MAC per element (SURVEY.md §8d)")},

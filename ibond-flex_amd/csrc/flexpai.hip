@@ -24,6 +24,7 @@
 #include "engine_grp_pair.hpp"
 #include "engine_pe.hpp"
 #include "engine_pfb.hpp"
+#include "engine_sgp.hpp"
 #include "engine_grp.hpp"
 #include "engine_mul.hpp"
 
@@ -111,6 +112,7 @@ struct pai_ctx {
   int fb_pair_s = 0;            // limbs of p_h of the resident pair tables; 0 = k_fb tables
   FbgpHalf* d_fbgp_halves = nullptr;  // 4096-bit keys: pair-group tables (kernels_grp_pair.hpp)
   bool fb_gpair = false;
+  SgpHalf* d_sgp_fb = nullptr;  // 4096-bit keys: the split-pair sampler over the same tables (kernels_sgp.hpp)
   FbRed* d_fb_red = nullptr;
   uint32_t *d_fb_m8 = nullptr, *d_fb_coefR = nullptr, *d_fb_q2 = nullptr, *d_fb_m0 = nullptr;
   uint32_t* d_fb_q2Rn = nullptr;  // 4096-bit keys: q^2 R mod n^2 (k_fbg_fin)
@@ -130,6 +132,7 @@ struct pai_ctx {
   int pfb_W = 0, pfb_W_used = 0, pfb_K = 0, pfb_K0 = 0, pfb_KS = 0;
   std::vector<HBig> pfb_bases;  // g_0 .. g_PFB_SHORT (chosen at the first build unless set)
   PfbConst* d_pfb = nullptr;
+  SgpHalf* d_sgp_pfb = nullptr;  // the split-pair sampler over the public tables (kernels_sgp.hpp)
   std::vector<void*> pfb_mem;
   long long pfb_seen = 0;
   float pfb_host_ms = 0.f, pfb_dev_ms = 0.f;
@@ -556,6 +559,34 @@ static int upload_fb(pai_ctx* c, const std::vector<T>& v, T** out) {
   return 0;
 }
 
+// Split-pair sampler (kernels_sgp.hpp) over the pair-group tables of modulus P (rows T R, R = 2^(28 FBGP_S)): C =
+// 2^(-56 K) mod P^2 as (C mod P, C div P), the chunk weights w 2^(16 c) C_A mod P of c0 = (1, w |M|), and 2^20 P.
+// FLEXPAI_SGP=0 keeps the group-engine samplers (k_fbgp, k_pfb).
+static bool sgp_enabled() {
+  const char* e = getenv("FLEXPAI_SGP");
+  return !e || atoi(e) != 0;
+}
+
+template <class Upload>
+static int sgp_make_half(const HBig& P, const HBig& w, int K, const void* table, Upload&& up, SgpHalf* out) {
+  const HBig P2 = mul(P, P);
+  const HBig C = inv_mod(mul_pow2_mod(HBig(1), (size_t)LB * (FBGP_S - SGP_S) * K, P2), P2);
+  if (C.is_zero()) return fail(PAI_ERR_KEY, "split-pair sampler: 2 not invertible mod P^2");
+  const HBig cb = div_big(C, P), ca = sub(C, mul(cb, P));
+  std::vector<uint32_t> nmc;
+  for (int k = 0; k < 4; ++k) {
+    const std::vector<uint32_t> v = mod(mul(mul_pow2_mod(mod(w, P), (size_t)16 * k, P), ca), P).limbs(SGP_S, LB);
+    nmc.insert(nmc.end(), v.begin(), v.end());
+  }
+  uint32_t *dp, *dca, *dcb, *dnmc, *dpb;
+  int rc;
+  if ((rc = up(P.limbs(SGP_S, LB), &dp)) || (rc = up(ca.limbs(SGP_S, LB), &dca)) || (rc = up(cb.limbs(SGP_S, LB), &dcb)) ||
+      (rc = up(nmc, &dnmc)) || (rc = up(mul(P, pow2(20)).limbs(SGP_S, LB), &dpb)))
+    return rc;
+  *out = SgpHalf{(const uint4*)table, dp, dca, dcb, dnmc, dpb, mont_prime(P, LB)};
+  return 0;
+}
+
 // Digit windows the table builder supports (lo/hi half-digit tables of at most FB_LO entries)
 static bool fb_window_ok(int w) { return w == 8 || w == 12 || w == 16 || (w >= 20 && w <= 24); }
 
@@ -633,6 +664,7 @@ static void fb_release(pai_ctx* c) {
   c->fb_pair_s = 0;
   c->d_fbgp_halves = nullptr;
   c->fb_gpair = false;
+  c->d_sgp_fb = nullptr;
   c->d_fb_red = nullptr;
 }
 
@@ -737,6 +769,7 @@ static int ensure_fb(pai_ctx* c) {
   const bool gpair_ok = grp && fb_gpair_possible(c);
   const int lohi_limbs = pair_ok ? std::max(sb, 2 * ps) : gpair_ok ? std::max(sb, 2 * FBGP_S) : sb;
   FbgpHalf gv[2];
+  SgpHalf sv[2];
   FbpHalf pv[2];
   FbHalf hv[2];
   FbRed red[2];
@@ -876,6 +909,10 @@ static int ensure_fb(pai_ctx* c) {
       gcval[h] = (uint32_t*)vcv;
       gv[h] = FbgpHalf{(const uint32_t*)t[h], gp, gx, gone, gbases, dlohi, gnm, gpbig, gp2, gpr2, mont_prime(P, LB),
                        mont_prime(m2, LB), (uint32_t*)vinv, (uint32_t*)vpre, (uint32_t*)vcv};
+      if (sgp_enabled() &&
+          (rc = sgp_make_half(P, primes[1 - h], K, t[h],
+                              [&](const std::vector<uint32_t>& v, uint32_t** o) { return upload_fb(c, v, o); }, &sv[h])))
+        return fb_unavailable(c, pai_last_error());
     }
     if (h == 0) {
       c->d_fb_m0 = dm;
@@ -932,6 +969,10 @@ static int ensure_fb(pai_ctx* c) {
   if (gpair_ok) {
     std::vector<FbgpHalf> gvv(gv, gv + 2);
     if ((rc = upload_fb(c, gvv, &c->d_fbgp_halves))) return fb_unavailable(c, pai_last_error());
+    if (sgp_enabled()) {
+      std::vector<SgpHalf> svv(sv, sv + 2);
+      if ((rc = upload_fb(c, svv, &c->d_sgp_fb))) return fb_unavailable(c, pai_last_error());
+    }
   }
   if (gpair_ok || pair_ok) {   // factored rows: the chain products are inverted on the host between the two phases
     const hipError_t e1 = gpair_ok ? fbgp_build_phase1(c->d_fbgp_halves, K, W, nullptr)
@@ -1310,6 +1351,10 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
     case PAI_OPT_FB_PAIR:
       *value = c->fb_state == pai_ctx::FB_READY ? (c->fb_gpair ? FBGP_S : c->fb_pair_s) : 0;
       return 0;
+    case PAI_OPT_SPLIT_SAMPLER:
+      *value = (c->fb_state == pai_ctx::FB_READY && c->d_sgp_fb ? 1 : 0) |
+               (c->pfb_state == pai_ctx::FB_READY && c->d_sgp_pfb ? 2 : 0);
+      return 0;
     case PAI_OPT_PAIR:
       *value = ((c->dec_pair_ok || c->dec4_ok) && c->dec_lane_enabled ? 1 : 0) | (c->crt_pair_ok ? 2 : 0) |
                (c->pe_ok ? 4 : 0);
@@ -1494,11 +1539,15 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
       HIPCHK(fbp_launch(c->fb_pair_s, pp, gF, st));
     } else if (grp && c->fb_gpair) {
       const FbgpParams pg{c->d_fbgp_halves, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
-      HIPCHK(fbgp_launch(pg, gF, st));
-      int occW = 1;
-      grp_fin_occupancy(&occW, &occG);
-      const long long gb4 = (n + BLOCK / 4 - 1) / (BLOCK / 4);
-      HIPCHK(fbgp_launch_w(pg, (int)std::max<long long>(1, std::min<long long>(gb4, (long long)occW * c->cus / 2)), st));
+      if (c->d_sgp_fb) {   // split pairs (kernels_sgp.hpp): SGP_PAIRS elements per block, grid (gx, 2)
+        int occS = 1;
+        sgp_occupancy(&occS);
+        const SgpParams sp{c->d_sgp_fb, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
+        const long long nb = (n + SGP_PAIRS - 1) / SGP_PAIRS;
+        HIPCHK(sgp_launch(sp, (int)std::max<long long>(1, std::min<long long>(nb, (long long)occS * c->cus / 2)), 2, st));
+      } else {
+        HIPCHK(fbgp_launch(pg, gF, st));
+      }
     } else {
       HIPCHK(grp ? grp_launch_fb(pf, gF, st) : fb_launch(SB, pf, gF, st));
     }
@@ -1508,6 +1557,11 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     if (grp) {   // w_h = c0 G_h^(a_h) mod p_h^2 -> Garner: h mod p^2 (S = 148), c = w_q + q^2 h mod n^2 (S = 296)
       int occH = 1, occC = 1;
       grp_fin_occupancy(&occH, &occC);
+      if (c->fb_gpair) {   // the pairs -> w_h = A + p_h B mod p_h^2 (timed with the fin stage)
+        const FbgpParams pg{c->d_fbgp_halves, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
+        const long long gb4 = (n + BLOCK / 4 - 1) / (BLOCK / 4);
+        HIPCHK(fbgp_launch_w(pg, (int)std::max<long long>(1, std::min<long long>(gb4, (long long)occH * c->cus / 2)), st));
+      }
       const long long gb4 = (n + BLOCK / GRP_TPI - 1) / (BLOCK / GRP_TPI), gb8 = (n + BLOCK / 8 - 1) / (BLOCK / 8);
       FbgGarnerParams gh{w, n, c->d_fb_m0, c->d_fb_m8, c->d_fb_coefR, c->fb_mprime0};
       HIPCHK(grp_launch_garner(gh, (int)std::max<long long>(1, std::min<long long>(gb4, (long long)occH * c->cus)), st));
@@ -1573,6 +1627,7 @@ static void pfb_release(pai_ctx* c) {
   for (void* q : c->pfb_mem) (void)hipFree(q);
   c->pfb_mem.clear();
   c->d_pfb = nullptr;
+  c->d_sgp_pfb = nullptr;
 }
 
 static int pfb_unavailable(pai_ctx* c, const std::string& why) {
@@ -1716,6 +1771,15 @@ static int ensure_pfb(pai_ctx* c) {
   std::vector<PfbConst> pv{pc};
   PfbConst* dpc = nullptr;
   if ((rc = upload_pfb(c, pv, &dpc))) return pfb_unavailable(c, pai_last_error());
+  SgpHalf* dsgp = nullptr;
+  if (sgp_enabled()) {
+    SgpHalf sh{};
+    if ((rc = sgp_make_half(n, HBig(1), K, dtab,
+                            [&](const std::vector<uint32_t>& v, uint32_t** o) { return upload_pfb(c, v, o); }, &sh)))
+      return pfb_unavailable(c, pai_last_error());
+    std::vector<SgpHalf> shv{sh};
+    if ((rc = upload_pfb(c, shv, &dsgp))) return pfb_unavailable(c, pai_last_error());
+  }
   const auto t1 = std::chrono::steady_clock::now();
   if (pfb_build_phase1(dpc, pc.nbases, K, W, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return pfb_unavailable(c, "table construction failed");
@@ -1728,6 +1792,7 @@ static int ensure_pfb(pai_ctx* c) {
   }
   const auto t2 = std::chrono::steady_clock::now();
   c->d_pfb = dpc;
+  c->d_sgp_pfb = dsgp;
   c->pfb_host_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
   c->pfb_dev_ms = std::chrono::duration<float, std::milli>(t2 - t1).count();
   c->pfb_table_bytes = pfb_bytes(c, W);
@@ -1788,7 +1853,16 @@ static int launch_pfb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     stage_mark(c, 1, st);
     const PfbParams pp{c->d_pfb, n, digits, (const char*)e.x + (size_t)off * esz, e.dtype, e.exp_mode, e.fexp,
                        e.exp + off, e.status ? e.status + off : nullptr, xw};
-    HIPCHK(pfb_launch(pp, (int)std::min<long long>(gx, (n + GPB - 1) / GPB), st));
+    if (c->d_sgp_pfb) {   // split pairs (kernels_sgp.hpp)
+      int occS = 1;
+      sgp_occupancy(&occS);
+      const SgpParams sp{c->d_sgp_pfb, n, c->pfb_K, c->pfb_W_used, digits, xw, pp.x, pp.dtype, pp.exp_mode, pp.fexp, pp.exp,
+                         pp.status};
+      const long long nb = (n + SGP_PAIRS - 1) / SGP_PAIRS;
+      HIPCHK(sgp_launch(sp, (int)std::max<long long>(1, std::min<long long>(nb, (long long)occS * c->cus)), 1, st));
+    } else {
+      HIPCHK(pfb_launch(pp, (int)std::min<long long>(gx, (n + GPB - 1) / GPB), st));
+    }
     stage_mark(c, 2, st);
     PeParams pf{};
     pf.k = c->d_pe;

@@ -23,6 +23,7 @@ EL_OK, EL_INT, EL_INT_BIG, EL_OVERFLOW, EL_FLOAT_OVF, EL_ENC_RANGE = 0, 1, 2, 3,
 
 PAI_OPT_CRT_ENCRYPT, PAI_OPT_CRT_AVAILABLE, PAI_OPT_STAGE_TIMING, PAI_OPT_LANE_DECRYPT = 1, 2, 3, 4
 PAI_OPT_FIXED_BASE, PAI_OPT_FB_WINDOW, PAI_OPT_FB_READY, PAI_OPT_FB_PAIR, PAI_OPT_PAIR = 5, 6, 7, 8, 9
+PAI_OPT_SPLIT_SAMPLER = 13
 PAI_OPT_PUBLIC_FB, PAI_OPT_PFB_READY, PAI_OPT_PFB_WINDOW = 10, 11, 12
 PFB_NBASES = 33
 
@@ -271,6 +272,11 @@ class Context:
     def fb_pair(self) -> int:
         """Limbs of p_h of the resident pair tables (kernels_fbp.hpp: k_fbp), 0 for k_fb tables or none."""
         return int(self._get_option(PAI_OPT_FB_PAIR))
+
+    @property
+    def split_sampler(self) -> int:
+        """Bit 0: the 4096-bit key-holder tables, bit 1: the public tables are sampled by k_sgp (kernels_sgp.hpp)."""
+        return int(self._get_option(PAI_OPT_SPLIT_SAMPLER))
 
     @property
     def pair_paths(self) -> int:

@@ -112,6 +112,9 @@ typedef struct pai_comm pai_comm;
 #define PAI_OPT_PFB_READY 11     /* read-only: 1 when the public fixed-base tables are resident               */
 #define PAI_OPT_PFB_WINDOW 12    /* digit window of the public tables (as PAI_OPT_FB_WINDOW; default 16:
                                   * 324 rows of 512 B per element, 10.9 GB of tables)                        */
+#define PAI_OPT_SPLIT_SAMPLER 13 /* read-only: bit 0 = the resident 4096-bit key-holder tables, bit 1 = the resident
+                                  * public tables are sampled on split pairs (kernels_sgp.hpp: k_sgp, the default;
+                                  * $FLEXPAI_SGP=0 at table build selects k_fbgp / k_pfb)                      */
 
 /* Number of visible GPUs (0 when there is none or the runtime cannot start). */
 int pai_device_count(int* count);

@@ -5,6 +5,8 @@ engine, recombined by k_crt_fin<8>), SURVEY.md §8 row (f) nb = 4096 / BASELINE 
   (tests/golden/paillier_golden_fb.json, made by tests/golden/make_golden_fb.py) at W = 12, 16 and 21 (the bench's);
 * bit-exact against the CPU restatement (oracle/paillier_oracle.py fb_encrypt_value) at other index
   bases and ragged sizes, identical across windows, decryptable;
+* the split-pair sampler (kernels_sgp.hpp: k_sgp, the default) and the pair-group k_fbgp (FLEXPAI_SGP=0) give
+  identical ciphertexts from the same tables;
 * with the table memory capped, device-RNG encryption falls back to the public-key path (r = the ChaCha20
   stream, bit-identical to the explicit-r reference path) and decryption is unaffected."""
 import numpy as np
@@ -122,3 +124,21 @@ def test_fixed_base_4096_memory_cap_falls_back(golden, monkeypatch):
         assert got[i] == O.encrypt_value(x[i], key, r)[0]
     val, _, _, _ = ctx.decrypt(ct, ex)
     assert np.array_equal(val, x.astype(np.float64))
+
+
+def test_split_sampler_matches_group_engine(ctx4096, golden, monkeypatch):
+    """k_sgp (kernels_sgp.hpp, split pairs: the default) and k_fbgp (pair groups, FLEXPAI_SGP=0) read the same
+    tables and give the same ciphertexts, ragged size, non-zero index base."""
+    N = _native()
+    ctx, key = ctx4096
+    rk = bytes(range(40, 72))
+    x = (np.random.default_rng(21).standard_normal(333) * 1e4).astype(np.float64)
+    x[::5] *= -1.0
+    ct, ex, _ = ctx.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=2 ** 32 - 3)
+    assert ctx.split_sampler & 1
+    monkeypatch.setenv("FLEXPAI_SGP", "0")
+    ref = N.Context(key.n, 0, key.p, key.q)
+    ref.set_fb_window(12)
+    ct2, ex2, _ = ref.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=2 ** 32 - 3)
+    assert ref.fb_ready and not ref.split_sampler & 1
+    assert np.array_equal(ct, ct2) and np.array_equal(ex, ex2)

@@ -8,6 +8,8 @@ hold only the public key (HE_OTP_LR host, he_otp_lr_ft1/train.py:135,164; HE_LR_
 * bit-exact against the oracle's restatement (oracle/paillier_oracle.py pfb_*) with the bases the context drew
   itself (g_0 with Jacobi symbol -1), at ragged sizes and index bases; decryptable; the publicly visible Jacobi
   symbol of c mod n uniform +-1 (as for r uniform in Z_n*);
+* the split-pair sampler (kernels_sgp.hpp: k_sgp, the default) and the pair-group k_pfb (FLEXPAI_SGP=0) give
+  identical ciphertexts;
 * below the break-even count a fresh public key encrypts on k_pe_* (ChaCha20 r, bit-exact vs the explicit-r
   reference path) and builds no tables; 1M elements round-trip exactly."""
 import numpy as np
@@ -146,3 +148,25 @@ def test_public_full_size_roundtrip(drawn):
         assert (got[j], int(ex[i])) == O.pfb_encrypt_value(x[i], key, bases, rk, i, W)
     half, _, _ = ctx.encrypt(x[n // 2:], obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=n // 2)
     assert np.array_equal(half, ct[n // 2:])
+
+
+def test_split_sampler_matches_group_engine(pub, golden_pfb, monkeypatch):
+    """k_sgp (split pairs, the default) and k_pfb (pair groups, FLEXPAI_SGP=0) over the same bases and window:
+    identical ciphertexts."""
+    N = _native()
+    ctx, dec, key, bases = pub
+    rk = b"\x5a" * 32
+    x = np.random.default_rng(33).standard_normal(257).astype(np.float32)
+    outs = []
+    for sgp in ("1", "0"):
+        monkeypatch.setenv("FLEXPAI_SGP", sgp)
+        c = N.Context(key.n, 0)
+        c.set_public_bases(bases)
+        c.set_pfb_window(12)
+        c.prepare_public_fixed_base()
+        assert bool(c.split_sampler & 2) == (sgp == "1")
+        outs.append(c.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=77)[:2])
+        del c
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    val, _, st, _ = dec.decrypt(outs[0][0], outs[0][1])
+    assert np.array_equal(np.asarray(val, dtype=np.float64), x.astype(np.float64))

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 profiles of the committed tree: kernel-trace/stats of the default bench, HBM traffic (separate
 # FETCH_SIZE / WRITE_SIZE passes, tools/pmc_traffic.py) of k_fbp / k_fbp_fin / k_fb_digits (configs[1]) and
-# k_add (configs[2]), k_fbgp (configs[4]), SQ issue counters of the configs[1] kernels, then the default bench line (which now finds the
+# k_add (configs[2]), k_sgp (configs[4]), SQ issue counters of the configs[1] kernels, then the default bench line (which now finds the
 # fresh traffic files of this very library).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -23,7 +23,7 @@ for k in k_fbp_fin k_fb_digits; do
   python3 tools/pmc_traffic.py $O/pmc_FETCH_SIZE/run_counter_collection.csv $O/pmc_WRITE_SIZE/run_counter_collection.csv --kernel $k --n 1048576 --nb 2048 -o profiles/pmc_${k}_latest.json || exit 1
 done
 python3 tools/pmc_traffic.py $O/pmc2_FETCH_SIZE/run_counter_collection.csv $O/pmc2_WRITE_SIZE/run_counter_collection.csv --kernel k_add --n 1048576 --nb 2048 -o profiles/pmc_k_add_latest.json || exit 1
-python3 tools/pmc_traffic.py $O/pmc4_FETCH_SIZE/run_counter_collection.csv $O/pmc4_WRITE_SIZE/run_counter_collection.csv --kernel k_fbgp --n 4194304 --nb 4096 --window 21 -o profiles/pmc_k_fbgp_latest.json || exit 1
+python3 tools/pmc_traffic.py $O/pmc4_FETCH_SIZE/run_counter_collection.csv $O/pmc4_WRITE_SIZE/run_counter_collection.csv --kernel k_sgp --n 4194304 --nb 4096 --window 21 -o profiles/pmc_k_sgp_latest.json || exit 1
 mkdir -p $O/pmcjson && cp profiles/pmc_*_latest.json $O/pmcjson/
 python3 tools/pmc_sq_summary.py $O/pmcsq/run_counter_collection.csv > $O/pmc_sq_summary.txt 2>&1 || true
 head -30 $O/pmc_sq_summary.txt

@@ -259,6 +259,9 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_sgp(SgpParams p) {
       if (k + 1 < K) {   // (after the normalization: the b words do not share registers with P)
         sgp_b_load(table, (size_t)(k + 1), W, dn, tig, bv);
         dn = k + 2 < K ? dg[(size_t)(k + 2) * p.n] : 0u;
+      } else {           // (defined on every path, or bv stays live -- and spilled -- across the product)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) bv[q] = make_uint4(0u, 0u, 0u, 0u);
       }
     }
     // the b sum: lane 1's carry count enters at word 64, lane 0's at word 32 (rippling through lane 1's words)

@@ -550,6 +550,8 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
   constexpr int NL = (32 * CW + 27) / 28;             // limbs that cover them
   static_assert(NL <= 4 * S, "c < n^2 fits 4 S limbs");
   __shared__ uint32_t cs[12 * S];
+  // the waves' 64-element tiles of w_p pairs (2S limbs x 64 elements each), streamed in by DMA during X's product
+  __shared__ __attribute__((aligned(16))) uint32_t wpl[(LANE_BLOCK / 64) * 2 * S * 64];
   for (int j = threadIdx.x; j < 12 * S; j += blockDim.x) cs[j] = p.cs[j];
   __syncthreads();
   uint32_t m[S];
@@ -558,12 +560,31 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
   const uint32_t mprime = p.mprime;
   const uint32_t* p4 = cs + 10 * S;
   const uint32_t* p3 = cs + 11 * S;
+  const int lane = threadIdx.x & 63;
+  uint32_t* wpp = wpl + (threadIdx.x >> 6) * 2 * S * 64;   // limb j of this lane's w_p at wpp[64 j + lane]
   for (long long base = (long long)blockIdx.x * LANE_BLOCK; base < p.n; base += (long long)gridDim.x * LANE_BLOCK) {
     const long long i = base + threadIdx.x;
     const bool valid = i < p.n;
     const long long ii = valid ? i : p.n - 1;
-    const uint32_t* pp = p.pr + fbp_pair_index<S>(ii, 0, p.n);   // limb j of the pair at pp[64 j]
     const uint32_t* pq = p.pr + fbp_pair_index<S>(ii, 1, p.n);
+    {   // the wave's w_p tile (contiguous, 256-B aligned; tiles are padded to 64 elements) -> LDS, 1 KB per DMA
+      long long e0 = base + (threadIdx.x & ~63);
+      if (e0 >= p.n) e0 = (p.n - 1) & ~63ll;
+      uint64_t src = (uint64_t)(reinterpret_cast<const uint4*>(p.pr + fbp_pair_index<S>(e0, 0, p.n)) + lane);
+      typedef __attribute__((address_space(3))) uint32_t lds_u32;
+      const uint32_t lb = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds_u32*)wpp);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous element's reads of the tile are done
+      constexpr int NI = (32 * S + 63) / 64, REM = (32 * S) % 64;
+#pragma unroll
+      for (int g = 0; g < NI; ++g) {
+        uint32_t dst = lb + (uint32_t)(g * 1024);
+        asm volatile("" : "+s"(dst));
+        if (REM == 0 || g + 1 < NI || lane < REM)
+          __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(size_t)dst, 16, 0, 0);
+        src += 1024;
+        asm volatile("" : "+v"(src));   // one address register, advanced per DMA (not 19 precomputed)
+      }
+    }
     // X = q B_q mod p^2
     uint32_t xa[S], xb[S];
 #pragma unroll
@@ -574,11 +595,12 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
     pair::mont_mul<S>(xa, xb, FbpFinDigits<S>{cs}, m, mprime);
     // D = w_p - w_q as a pair with non-negative parts
     {
+      lds_dma_wait();   // the w_p tile landed
       int64_t ca = 0, cb = 0;
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        const int64_t va = (int64_t)pp[j * 64] + (int64_t)p4[j] - (int64_t)pq[j * 64] - (int64_t)xa[j] + ca;
-        const int64_t vb = (int64_t)pp[(S + j) * 64] + (int64_t)p3[j] - (int64_t)xb[j] - (j == 0 ? 4 : 0) + cb;
+        const int64_t va = (int64_t)wpp[j * 64 + lane] + (int64_t)p4[j] - (int64_t)pq[j * 64] - (int64_t)xa[j] + ca;
+        const int64_t vb = (int64_t)wpp[(S + j) * 64 + lane] + (int64_t)p3[j] - (int64_t)xb[j] - (j == 0 ? 4 : 0) + cb;
         xa[j] = (uint32_t)va & lane::LMASK;
         xb[j] = (uint32_t)vb & lane::LMASK;
         ca = va >> lane::LB;

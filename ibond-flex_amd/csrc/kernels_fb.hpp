@@ -114,9 +114,11 @@ struct FbFinParams {
 // Each lane stages its raw stream in its own LDS row (odd stride: conflict-free), reduces it modulo
 // D_h in place and extracts the digits. A kernel of its own: the ChaCha key schedule's registers would
 // otherwise push the modulus out of the SGPRs of k_fb.
-template <int DUMMY = 0>   // (a template only so the header can be included by several units)
+// ROW (odd, >= raw words + 3): LDS words per lane, sized to the key (21 / 37 / 69 at nb = 1024 / 2048 / 4096) so
+// that the LDS of a block does not cap the occupancy (the 83-word rows of every key size allowed 1.5 waves per SIMD).
+template <int ROW>
 __global__ __launch_bounds__(FB_DIG_BLOCK) void k_fb_digits(FbDigitParams p) {
-  constexpr int ROW = FB_RAW_MAX + 3;
+  static_assert(ROW % 2 == 1 && ROW <= FB_RAW_MAX + 3, "row");
   __shared__ uint32_t wb[FB_DIG_BLOCK * ROW];
   uint32_t* a = wb + threadIdx.x * ROW;
   const int half = blockIdx.y;
@@ -132,7 +134,8 @@ __global__ __launch_bounds__(FB_DIG_BLOCK) void k_fb_digits(FbDigitParams p) {
       uint32_t blk[16];
       chacha20_block(p.rng_key, (uint32_t)b, (uint32_t)g, (uint32_t)(g >> 32), FB_NONCE + (uint32_t)half, blk);
 #pragma unroll
-      for (int w = 0; w < 16; ++w) a[16 * b + w] = blk[w];
+      for (int w = 0; w < 16; ++w)
+        if (16 * b + w < rw) a[16 * b + w] = blk[w];   // (the last block's tail would run into the next lane's row)
     }
     if (rb & 31) a[rw - 1] &= (1u << (rb & 31)) - 1u;
     for (int w = rw; w < ROW; ++w) a[w] = 0u;

@@ -584,6 +584,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
         src += 1024;
         asm volatile("" : "+v"(src));   // one address register, advanced per DMA (not 19 precomputed)
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
     // X = q B_q mod p^2
     uint32_t xa[S], xb[S];
@@ -596,11 +597,14 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
     // D = w_p - w_q as a pair with non-negative parts
     {
       lds_dma_wait();   // the w_p tile landed
+      int tx = threadIdx.x;
+      asm volatile("" : "+v"(tx));   // (the tile address is rebuilt here, not held across the products)
+      const uint32_t* wq = wpl + (tx >> 6) * 2 * S * 64 + (tx & 63);
       int64_t ca = 0, cb = 0;
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        const int64_t va = (int64_t)wpp[j * 64 + lane] + (int64_t)p4[j] - (int64_t)pq[j * 64] - (int64_t)xa[j] + ca;
-        const int64_t vb = (int64_t)wpp[(S + j) * 64 + lane] + (int64_t)p3[j] - (int64_t)xb[j] - (j == 0 ? 4 : 0) + cb;
+        const int64_t va = (int64_t)wq[j * 64] + (int64_t)p4[j] - (int64_t)pq[j * 64] - (int64_t)xa[j] + ca;
+        const int64_t vb = (int64_t)wq[(S + j) * 64] + (int64_t)p3[j] - (int64_t)xb[j] - (j == 0 ? 4 : 0) + cb;
         xa[j] = (uint32_t)va & lane::LMASK;
         xb[j] = (uint32_t)vb & lane::LMASK;
         ca = va >> lane::LB;

@@ -291,6 +291,9 @@ __device__ __forceinline__ void fbw_mont_mul(uint32_t (&a)[S], uint32_t addr, co
 // each instruction (M0) is formed right here from one scalar base: left to the compiler, the TQ constant
 // destinations are precomputed once, spilled under the product's register pressure and reloaded with a
 // vmcnt(0) wait before every DMA instruction -- serialising the row stream.
+#ifndef FB_DMA_AUX
+#define FB_DMA_AUX 0   // cache-policy bits of the row DMA (experiments: 2 = nt)
+#endif
 template <int TQ>
 __device__ __forceinline__ void fb_row_to_lds(const uint4* __restrict__ table, size_t row, uint4* wave_row0) {
   typedef __attribute__((address_space(3))) uint4 lds_uint4;
@@ -300,7 +303,8 @@ __device__ __forceinline__ void fb_row_to_lds(const uint4* __restrict__ table, s
   for (int g = 0; g < TQ; ++g) {
     uint32_t dst = lb + (uint32_t)(g * LANE_BLOCK * 16);
     asm volatile("" : "+s"(dst));
-    __builtin_amdgcn_global_load_lds((const void*)(r + g), (__attribute__((address_space(3))) void*)(size_t)dst, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(r + g), (__attribute__((address_space(3))) void*)(size_t)dst, 16, 0,
+                                     FB_DMA_AUX);
   }
 }
 

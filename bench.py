@@ -29,9 +29,11 @@ Rank 0 prints ONE JSON line. `roofline` is for the dominant kernel of the timed 
 timed live with HIP events recorded on the launch stream between the kernels of every timed call; its
 work figure is that kernel's own MAC count (the fixed-base count for k_fb, NOT SURVEY.md §8d's public-
 key W_enc, which is reported beside it as `w_enc_equivalent`). `cpu_baseline` (N = 1 only) is the GMP
-restatement of the reference CPU path (oracle/gmp_oracle.c, threads = os.cpu_count() like the
-reference's Pool(cpu_count())) on a bounded sample of the same workload, which doubles as a bit-exact
-check of the GPU output; `extra.config0_cpu` times configs[0] (nb = 1024, 1k elements) in full.
+restatement of the reference CPU path (oracle/gmp_oracle.c; threads = the process's CPU share -- its
+affinity mask capped by the cgroup CPU quota, which on a shared GPU box is far below os.cpu_count() -- like
+the reference's Pool(cpu_count())) on a bounded sample of the same workload, which doubles as a bit-exact
+check of the GPU output; a one-thread run of the first elements gives the per-core rate and
+`cores_effective` = threaded rate / per-core rate; `extra.config0_cpu` times configs[0] (nb = 1024, 1k elements) in full.
 """
 import argparse
 import hashlib
@@ -198,6 +200,67 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def cpu_quota() -> dict:
+    """The CPU share this process may use: the cgroup CPU quota (v2 cpu.max, or v1 cfs_quota_us /
+    cfs_period_us) of its own cgroup, and the affinity mask. os.cpu_count() counts the whole machine, which on
+    a shared GPU box is many times the process's share (256 threads delivered ~17 cores of work)."""
+    out = {"os_cpu_count": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+           "cgroup_quota_cores": None, "cgroup_quota_source": None}
+    rel = {}
+    try:
+        with open("/proc/self/cgroup") as f:
+            for line in f:
+                _, ctrl, path = line.rstrip("\n").split(":", 2)
+                for c in (ctrl.split(",") if ctrl else [""]):
+                    rel[c] = path
+    except OSError:
+        pass
+    cands = []
+    if "" in rel:                                    # cgroup v2: walk up from our group to the root
+        p = rel[""]
+        while True:
+            cands.append(("v2", os.path.join("/sys/fs/cgroup", p.lstrip("/"), "cpu.max")))
+            if p in ("/", ""):
+                break
+            p = os.path.dirname(p)
+    for key in ("cpu", "cpu,cpuacct"):
+        if key in rel:
+            for base in ("/sys/fs/cgroup/cpu", "/sys/fs/cgroup/cpu,cpuacct"):
+                cands.append(("v1", os.path.join(base, rel[key].lstrip("/"))))
+                cands.append(("v1", base))
+    best = None
+    for kind, path in cands:
+        try:
+            if kind == "v2":
+                with open(path) as f:
+                    q, per = f.read().split()[:2]
+                if q != "max":
+                    v = int(q) / int(per)
+                    best = (v, path) if best is None or v < best[0] else best
+            else:
+                with open(os.path.join(path, "cpu.cfs_quota_us")) as f:
+                    q = int(f.read())
+                with open(os.path.join(path, "cpu.cfs_period_us")) as f:
+                    per = int(f.read())
+                if q > 0:
+                    v = q / per
+                    best = (v, path) if best is None or v < best[0] else best
+        except (OSError, ValueError):
+            continue
+    if best is not None:
+        out["cgroup_quota_cores"], out["cgroup_quota_source"] = round(best[0], 2), best[1]
+    return out
+
+
+def cpu_threads_default() -> int:
+    """Worker threads for the CPU baseline: the affinity mask, capped by the cgroup quota when one is set."""
+    q = cpu_quota()
+    n = q["affinity_cpus"] or 1
+    if q["cgroup_quota_cores"]:
+        n = min(n, max(1, int(q["cgroup_quota_cores"] + 0.5)))
+    return n
+
+
 def _free_port() -> int:
     import socket
     with socket.socket() as s:
@@ -278,11 +341,11 @@ def main():
                          "whose tables fit the free HBM (nb = 2048: W = 23, 45 pair products per half, 2 x 96.6 GB; "
                          "nb = 4096: W = 21, 98 products per half, 2 x 121.7 GB). With the pair sampler W = 23 "
                          "measured 1.8 %% faster than 22 (profiles/r02_window_sweep_pair.txt)")
-    ap.add_argument("--pfb-window", type=int, default=20, choices=(8, 12, 16, 20),
+    ap.add_argument("--pfb-window", type=int, default=20, choices=(12, 16, 20),
                     help="digit window of the public-key fixed-base leg (W = 20: 266 row products per element, "
                          "139 GB of tables; the library default is 16)")
     ap.add_argument("--cpu-sample", type=int, default=16384)
-    ap.add_argument("--cpu-threads", type=int, default=os.cpu_count() or 1,
+    ap.add_argument("--cpu-threads", type=int, default=None,
                     help="threads of the GMP CPU baseline (default os.cpu_count(), like the reference's Pool)")
     ap.add_argument("--deterministic", action="store_true",
                     help="fixed obfuscator key (sha256 constant) instead of os.urandom on rank 0; reproducible runs only")
@@ -550,11 +613,13 @@ def main():
 
     # ---- configs[3] leg (strong scaling): 16M elements over the ranks, every step's ciphertext shards
     # reassembled on every rank by an RCCL all-gather (double-buffered against the next step's encrypt)
+    c3_seams = None
     if cfg_id == 1 and not args.no_strong and nb == 2048:
         tot3 = CONFIGS[3]["total"]
         lo3, hi3 = shard_bounds(tot3, world, rank)
         N3 = -(-tot3 // world)
-        x3 = torch.from_numpy(np.random.default_rng(1000 + rank).standard_normal(N3, dtype=np.float32)).to(dev)
+        x3_host = np.random.default_rng(1000 + rank).standard_normal(N3, dtype=np.float32)
+        x3 = torch.from_numpy(x3_host).to(dev)
         st3 = torch.empty(N3, dtype=torch.int32, device=dev)
         b3 = [(torch.empty((N3, W), dtype=torch.int32, device=dev), torch.empty(N3, dtype=torch.int32, device=dev))
               for _ in range(2 if world > 1 else 1)]
@@ -611,8 +676,43 @@ def main():
             leg["gathered_bytes_per_rank_per_step"] = world * N3 * (W + 1) * 4
             if not same:
                 raise SystemExit("configs[3]: all-gathered shard differs from the local one")
+        # the last timed step's output, checked: this rank's shard decrypted on the device (up to
+        # the 2M elements of one rank's shard at N = 8), the sampler's restatement at the shard's seams, and at
+        # N > 1 a block of the next rank's shard as gathered here, against that rank's regenerated input
+        bl = (args.strong_steps - 1) % len(b3)
+        n3 = hi3 - lo3
+        nchk = min(n3, 2 << 20)
+        v3 = torch.empty(nchk, dtype=torch.float64, device=dev)
+        s3 = torch.empty(nchk, dtype=torch.int32, device=dev)
+        decrypt(b3[bl][0], b3[bl][1], v3, s3, nchk)
+        torch.cuda.synchronize()
+        chk = {"decrypted_own_elements": nchk,
+               "own_roundtrip_exact": bool(torch.equal(v3, x3[:nchk].double())) and int((s3 > 1).sum().item()) == 0}
+        if use_fb and fb_info is not None:
+            # checked against the oracle's restatement in the cpu_baseline leg below (the one place bench.py
+            # runs oracle/ code)
+            seam = [0, n3 - 1]
+            c3_seams = (leg, [lo3 + i for i in seam], [x3_host[i] for i in seam],
+                        _native.words_to_ints(b3[bl][0][seam].cpu().numpy().view(np.uint32)),
+                        [int(v) for v in b3[bl][1][seam].cpu().numpy()])
+        if world > 1:
+            peer = (rank + 1) % world
+            plo, phi = shard_bounds(tot3, world, peer)
+            npe = min(phi - plo, 1 << 16)
+            xp = torch.from_numpy(np.random.default_rng(1000 + peer).standard_normal(N3, dtype=np.float32)[:npe]).to(dev)
+            vp = torch.empty(npe, dtype=torch.float64, device=dev)
+            sp = torch.empty(npe, dtype=torch.int32, device=dev)
+            decrypt(g3[bl][0][peer * N3:], g3[bl][1][peer * N3:], vp, sp, npe)
+            torch.cuda.synchronize()
+            chk["gathered_peer_block"] = {"peer": peer, "elements": npe,
+                                          "roundtrip_exact": bool(torch.equal(vp, xp.double())) and int((sp > 1).sum().item()) == 0}
+        leg["check"] = chk
+        bad = (not chk["own_roundtrip_exact"]
+               or not chk.get("gathered_peer_block", {"roundtrip_exact": True})["roundtrip_exact"])
+        if bad:
+            raise SystemExit(f"configs[3]: last step's output failed its check: {chk}")
         extra["config3_strong"] = leg
-        del x3, st3, b3, g3, w3
+        del x3, st3, b3, g3, w3, v3, s3
         torch.cuda.empty_cache()
 
     solo = world == 1 and rank == 0        # single-GPU legs beside the timed path
@@ -784,6 +884,59 @@ def main():
         hb["python_objects_note"] = (f"PaillierEncryptor.encrypt(ndarray[{hs}]) -> object ndarray of "
                                      "PaillierEncryptedNumber (encryptor.py:99-114 API), incl. materialisation")
         del objs
+        # the drop-in path's own device rate: the runtime's context at the library's default window (callers
+        # of PaillierEncryptor reach this, not the bench's W = 23 context), device-resident input
+        rctx = _runtime.context(pk)
+        ct_r = torch.empty((N, W), dtype=torch.int32, device=dev)
+        ex_r = torch.empty(N, dtype=torch.int32, device=dev)
+        st_r = torch.empty(N, dtype=torch.int32, device=dev)
+        t_r = float("inf")
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            rc = lib.pai_encrypt_dev(rctx.handle, _native.PAI_F32, x.data_ptr(), N, 0, 0, _native.PAI_OBF_RNG, None, 0, 0,
+                                     rng_key, index_base, ct_r.data_ptr(), ex_r.data_ptr(), st_r.data_ptr(),
+                                     stream.cuda_stream)
+            if rc != 0:
+                raise RuntimeError(lib.pai_last_error().decode())
+            torch.cuda.synchronize()
+            t_r = min(t_r, time.perf_counter() - t1)
+        extra["dropin_default_window"] = {
+            "encrypts_per_s": N / t_r, "window_bits": rctx.fb_window, "elements": N,
+            "table_bytes": rctx.fixed_base_setup()[2] if rctx.fb_ready else 0,
+            "note": "_runtime.context(pk) (what PaillierEncryptor.encrypt uses) at the library default window "
+                    "($FLEXPAI_FB_WINDOW unset: 16), device-resident x, best of 3 synchronised calls; "
+                    "FLEXPAI_FB_WINDOW=auto gives a process holding one key the largest window that fits "
+                    "(the bench context's W above)"}
+        del ct_r, ex_r, st_r
+        # a received ciphertext array decrypted through the drop-in API: the reference's plain object-ndarray
+        # pickle (what an unmodified peer sends, ion.py:150-178 -> ion.py:201) into PaillierDecryptor.decrypt
+        # (decryptor.py:114-127), the per-element key check and the packing included
+        import pickle
+        from flex.crypto.paillier.cipher_array import pack_checked
+        from flex.crypto.paillier.decryptor import PaillierDecryptor
+        pdec = PaillierDecryptor(pk, sk)
+        received = pickle.loads(pickle.dumps(enc.encrypt(x_host)))
+        assert type(received) is np.ndarray and received.dtype == object
+        pdec.decrypt(received[:4096])
+        t1 = time.perf_counter()
+        got_vals = pdec.decrypt(received)
+        t_rd = time.perf_counter() - t1
+        t1 = time.perf_counter()
+        pack_checked(received.reshape(-1), pk, W)
+        t_pack = time.perf_counter() - t1
+        hb["received_decrypt_per_s"] = N / t_rd
+        hb["received_decrypt_s"] = t_rd
+        hb["received_check_and_pack_s"] = t_pack
+        hb["received_decrypt_exact"] = bool(np.array_equal(got_vals, x_host.astype(np.float64)))
+        if "decrypt_per_s_per_gpu" in extra:
+            hb["received_decrypt_vs_device_decrypt"] = (N / t_rd) / extra["decrypt_per_s_per_gpu"]
+        hb["received_decrypt_note"] = (f"PaillierDecryptor.decrypt(object ndarray[{N}]) unpickled from the reference's "
+                                       "plain pickle: C key check + word packing (hostgmp.c pack_numbers), host -> "
+                                       "device, decrypt kernels, float64 out")
+        del received, got_vals
+        if not hb["received_decrypt_exact"]:
+            raise SystemExit("decrypting the received object array did not reproduce the input")
         # object-free path (cipher_buffer.py): encrypt into words, serialise, receive without objects
         from flex.crypto.paillier.cipher_array import from_wire
         t1 = time.perf_counter()
@@ -908,19 +1061,34 @@ def main():
     if not args.no_cpu_baseline and world == 1:
         from oracle import gmp_oracle
         if gmp_oracle.available():
-            th = max(1, args.cpu_threads)
-            cores = {"os_cpu_count": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
-                     "cpu_model": cpu_model()}
+            quota = cpu_quota()
+            th = max(1, args.cpu_threads if args.cpu_threads else cpu_threads_default())
+            cores = {**quota, "cpu_model": cpu_model()}
+            # one thread first: the per-core rate, against which the threaded run's parallelism is measured
+            S1 = min(S_chk, 256 if nb <= 2048 else 32)
+            t1 = time.perf_counter()
+            c1, e1 = gmp_oracle.encrypt_f32_chacha(pk.n, x_host[:S1], rng_key, index_base_chk, 1)
+            single = S1 / (time.perf_counter() - t1)
             S = S_chk
             t1 = time.perf_counter()
             cct, cex = gmp_oracle.encrypt_f32_chacha(pk.n, x_host[:S], rng_key, index_base_chk, th)
             cdt = time.perf_counter() - t1
-            same = bool(np.array_equal(ct_host_check[:S], cct) and np.array_equal(ex_host_check[:S], cex))
+            same = bool(np.array_equal(ct_host_check[:S], cct) and np.array_equal(ex_host_check[:S], cex)
+                        and np.array_equal(c1, cct[:S1]) and np.array_equal(e1, cex[:S1]))
+            eff = (S / cdt) / single
+            throttled = eff < 0.7 * th
             cpu = {"value": S / cdt, "unit": "encrypts/s", "cores": th, "kind": "port",
+                   "kind_detail": ("port (oracle/gmp_oracle.c); " +
+                                   (f"THROTTLED: {th} threads delivered {eff:.1f} cores of work" if throttled
+                                    else f"{th} threads delivered {eff:.1f} cores of work")),
+                   "single_thread_per_s": single, "single_thread_sample": S1,
+                   "cores_effective": eff, "throttled": throttled,
                    "sample": f"first {S} elements of the rank-0 vector with the same ChaCha20 obfuscators; "
                              f"GMP 6.2.1 mpz_powm(r, n, n^2) per element (the library gmpy2 2.0.8 wraps, "
-                             f"obfuscator.py:36), {th} worker threads like the reference's Pool(cpu_count())",
+                             f"obfuscator.py:36), {th} worker threads like the reference's Pool(cpu_count()), "
+                             f"capped by the cgroup quota; the first {S1} also on one thread",
                    "extrapolated_full_job_s": N / (S / cdt),
+                   "per_core_extrapolated_full_job_s": N / single,
                    "gpu_bit_exact_on_sample": same, **cores}
             if not same:
                 raise SystemExit("GPU ciphertexts differ from the GMP oracle on the CPU sample")
@@ -935,6 +1103,16 @@ def main():
                 cpu["fixed_base_bit_exact_vs_oracle"] = {"elements": idx, "ok": fb_ok}
                 if not fb_ok:
                     raise SystemExit("fixed-base ciphertexts differ from the oracle restatement")
+            if c3_seams is not None:
+                # the configs[3] leg's last step at its shard seams
+                from oracle import paillier_oracle as O
+                leg3, gidx, xs3, got3, ex3 = c3_seams
+                okey = O.Key(pk.n, sk.p, sk.q)
+                ok3 = all(O.fb_encrypt_value(xv, okey, rng_key, gi, fb_info) == (cv, ev)
+                          for gi, xv, cv, ev in zip(gidx, xs3, got3, ex3))
+                leg3["check"]["seams_vs_oracle"] = {"global_index": gidx, "ok": ok3}
+                if not ok3:
+                    raise SystemExit("configs[3]: seam ciphertexts differ from the oracle restatement")
             if pfb_check is not None:
                 from oracle import paillier_oracle as O
                 bases, Wp, cts, exs = pfb_check

@@ -2,10 +2,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <sys/random.h>
 #include <thread>
@@ -166,6 +168,7 @@ struct pai_ctx {
   static constexpr int EV_CHUNKS = 64;
   hipEvent_t ev[EV_CHUNKS][4] = {};
   int nev = 0, nchunk_ev = 0;
+  float ev_acc[3] = {0.f, 0.f, 0.f};   // stage times of chunks already folded (calls of more than EV_CHUNKS chunks)
   // host-buffer entry points (pai_encrypt / pai_decrypt / pai_add): device copies of the operands, a
   // compute and a copy stream, one event per chunk (host_pipe below)
   void* d_hostio = nullptr;
@@ -174,29 +177,71 @@ struct pai_ctx {
   std::vector<hipEvent_t> hev, pev;   // per chunk: kernels done / staging copy done
   void* h_pin[2] = {nullptr, nullptr};  // pinned staging slots (PCIe at full rate, truly asynchronous)
   size_t pin_bytes = 0;
-  ~pai_ctx() {
-    (void)hipSetDevice(device);
-    for (auto& ch : ev)
-      for (auto& e : ch)
-        if (e) (void)hipEventDestroy(e);
-    for (auto& e : hev) (void)hipEventDestroy(e);
-    for (auto& e : pev) (void)hipEventDestroy(e);
-    for (void* p : h_pin)
-      if (p) (void)hipHostFree(p);
-    if (s_comp) (void)hipStreamDestroy(s_comp);
-    if (s_copy) (void)hipStreamDestroy(s_copy);
-    if (d_hostio) (void)hipFree(d_hostio);
-    for (void* p : allocs) (void)hipFree(p);
-    for (void* p : priv_allocs) (void)hipFree(p);
-    for (void* p : fb_mem) (void)hipFree(p);
-    for (void* p : pfb_mem) (void)hipFree(p);
-    if (d_scratch) (void)hipFree(d_scratch);
-    if (d_work) (void)hipFree(d_work);
-    if (d_mul) (void)hipFree(d_mul);
-    if (d_inv) (void)hipFree(d_inv);
-    if (d_plain) (void)hipFree(d_plain);
-    if (d_seg) (void)hipFree(d_seg);
-    if (d_addplan) (void)hipFree(d_addplan);
+  // thread safety (CtxLock below): one call at a time per context, and the device work of successive calls
+  // ordered through tail_ev even when they come on different streams
+  mutable std::recursive_mutex mu;
+  hipEvent_t tail_ev = nullptr;
+  bool counted = false, holder = false;   // in g_contexts / g_key_holders
+  ~pai_ctx();
+};
+
+static std::atomic<int> g_contexts{0}, g_key_holders{0};
+
+pai_ctx::~pai_ctx() {
+  if (counted) --g_contexts;
+  if (holder) --g_key_holders;
+  (void)hipSetDevice(device);
+  if (tail_ev) {
+    (void)hipEventSynchronize(tail_ev);
+    (void)hipEventDestroy(tail_ev);
+  }
+  for (auto& ch : ev)
+    for (auto& e : ch)
+      if (e) (void)hipEventDestroy(e);
+  for (auto& e : hev) (void)hipEventDestroy(e);
+  for (auto& e : pev) (void)hipEventDestroy(e);
+  for (void* p : h_pin)
+    if (p) (void)hipHostFree(p);
+  if (s_comp) (void)hipStreamDestroy(s_comp);
+  if (s_copy) (void)hipStreamDestroy(s_copy);
+  if (d_hostio) (void)hipFree(d_hostio);
+  for (void* p : allocs) (void)hipFree(p);
+  for (void* p : priv_allocs) (void)hipFree(p);
+  for (void* p : fb_mem) (void)hipFree(p);
+  for (void* p : pfb_mem) (void)hipFree(p);
+  if (d_scratch) (void)hipFree(d_scratch);
+  if (d_work) (void)hipFree(d_work);
+  if (d_mul) (void)hipFree(d_mul);
+  if (d_inv) (void)hipFree(d_inv);
+  if (d_plain) (void)hipFree(d_plain);
+  if (d_seg) (void)hipFree(d_seg);
+  if (d_addplan) (void)hipFree(d_addplan);
+}
+
+// Held by every entry point that takes a context, for the whole call (recursive: the host-buffer entry points
+// call the *_dev ones). A context's device buffers -- scratch, work, fixed-base tables, host-io carve-outs --
+// are shared by all its calls, so a *_dev call's stream first waits for the device work of the context's
+// previous call (whatever stream that was on) and the call's own work becomes the new tail. Two threads may
+// therefore share one context: their calls run one after the other, on the host and on the device (SURVEY.md
+// §8(b)(iv); the reference isolates its state per process instead, encryptor.py:89-96).
+struct CtxLock {
+  pai_ctx* c;
+  hipStream_t st = nullptr;
+  bool dev = false;
+  std::unique_lock<std::recursive_mutex> lk;
+  explicit CtxLock(const pai_ctx* ctx) : c(const_cast<pai_ctx*>(ctx)), lk(ctx->mu) {}
+  CtxLock(pai_ctx* ctx, hipStream_t s) : c(ctx), st(s), dev(true), lk(ctx->mu) {
+    (void)hipSetDevice(c->device);
+    if (c->tail_ev) (void)hipStreamWaitEvent(st, c->tail_ev, 0);
+  }
+  ~CtxLock() {
+    if (!dev) return;
+    if (!c->tail_ev && hipEventCreateWithFlags(&c->tail_ev, hipEventDisableTiming) != hipSuccess) {
+      c->tail_ev = nullptr;
+      (void)hipGetLastError();
+      return;
+    }
+    (void)hipEventRecord(c->tail_ev, st);
   }
 };
 
@@ -363,10 +408,27 @@ static void stage_reset(pai_ctx* c) {
   if (c->stage_keep) return;   // inside a host-buffer call: its entry point reset once for all chunks
   c->nev = 0;
   c->nchunk_ev = 0;
+  for (float& a : c->ev_acc) a = 0.f;
 }
-// The events of a new chunk (nullptr when timing is off or the call has more than EV_CHUNKS chunks)
+// Elapsed times of the recorded chunks into ev_acc, freeing the event slots (waits for the last chunk).
+static void stage_fold(pai_ctx* c) {
+  if (c->nchunk_ev < 1 || c->nev < 2) {
+    c->nchunk_ev = 0;
+    return;
+  }
+  (void)hipEventSynchronize(c->ev[c->nchunk_ev - 1][c->nev - 1]);
+  for (int i = 0; i + 1 < c->nev && i < 3; ++i)
+    for (int ch = 0; ch < c->nchunk_ev; ++ch) {
+      float t = 0.f;
+      if (hipEventElapsedTime(&t, c->ev[ch][i], c->ev[ch][i + 1]) == hipSuccess) c->ev_acc[i] += t;
+    }
+  c->nchunk_ev = 0;
+}
+// The events of a new chunk (nullptr when timing is off); past EV_CHUNKS chunks the recorded ones are folded
+// into ev_acc first, so every chunk of a call is counted
 static hipEvent_t* stage_chunk(pai_ctx* c) {
-  if (!c->timing || c->nchunk_ev >= pai_ctx::EV_CHUNKS) return nullptr;
+  if (!c->timing) return nullptr;
+  if (c->nchunk_ev >= pai_ctx::EV_CHUNKS) stage_fold(c);
   hipEvent_t* e = c->ev[c->nchunk_ev++];
   for (int i = 0; i < 4; ++i)
     if (!e[i]) (void)hipEventCreate(&e[i]);
@@ -423,6 +485,8 @@ int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** ou
   if (!n.is_odd() || n.bits() < 64) return fail(PAI_ERR_KEY, "pai_ctx_create: n must be odd and >= 64 bits");
   auto* c = new pai_ctx();
   c->device = device;
+  c->counted = true;
+  ++g_contexts;
   if (hipSetDevice(device) != hipSuccess) {
     delete c;
     return fail(PAI_ERR_HIP, "pai_ctx_create: hipSetDevice failed");
@@ -590,10 +654,33 @@ static int sgp_make_half(const HBig& P, const HBig& w, int K, const void* table,
 // Digit windows the table builder supports (lo/hi half-digit tables of at most FB_LO entries)
 static bool fb_window_ok(int w) { return w == 8 || w == 12 || w == 16 || (w >= 20 && w <= 24); }
 
+// g_contexts, g_key_holders (above): contexts of this process, and those holding a private key.
+static bool fb_window_auto() {
+  const char* e = getenv("FLEXPAI_FB_WINDOW");
+  return e && strcmp(e, "auto") == 0;
+}
+
+// Window of the key holder's tables: $FLEXPAI_FB_WINDOW, default 16 (2 x 1.07 GB at nb = 2048: a process may hold
+// several keys). "auto": a process whose only private key is this one asks for the largest window (24) and
+// gets the largest whose tables fit auto's share of the free HBM (fb_budget), i.e. W = 23 at nb = 2048 and
+// W = 21 at nb = 4096 on an otherwise empty MI355X; a process holding several keys gets 16.
 static int fb_default_window() {
+  if (fb_window_auto()) return g_key_holders.load() <= 1 ? 24 : 16;
   const char* e = getenv("FLEXPAI_FB_WINDOW");
   const int w = e ? atoi(e) : 16;
   return fb_window_ok(w) ? w : 16;
+}
+
+// Windows of the public-key tables: the ones pinned to reference goldens (12, 16, 20; tests/golden/
+// make_golden_pfb.py). Their K = K0 + 32 KS rows keep k_sgp's b sum within its bound (K <= 512; W = 8 would
+// need 648). "auto": 20 for a process with one context, else 16.
+static bool pfb_window_ok(int w) { return w == 12 || w == 16 || w == 20; }
+
+static int pfb_default_window() {
+  if (fb_window_auto()) return g_contexts.load() <= 1 ? 20 : 16;
+  const char* e = getenv("FLEXPAI_FB_WINDOW");
+  const int w = e ? atoi(e) : 16;
+  return pfb_window_ok(w) ? w : w > 20 ? 20 : 16;
 }
 
 // 32-bit words of one table row: packed words for the lane kernels, S canonical limbs for the group kernel
@@ -628,13 +715,22 @@ static uint64_t fb_bytes(const pai_ctx* c, int W) {
 // max(4 GiB, 1/12 of the device) -- 24 GB on a 288 GB MI355X -- kept for what the context (and others in
 // the process) allocate after the tables: host-pipeline buffers for larger calls, decryption work and
 // scratch, k_add's schedule, a configs[3] shard with its all-gather receive buffers.
+// With FLEXPAI_FB_WINDOW=auto the budget is further capped at $FLEXPAI_FB_AUTO_FRAC (default 0.75) of the free
+// memory, so an automatic choice never takes the whole device (W = 23 at nb = 2048 is 193 GB of 287 GB free).
 static uint64_t fb_budget(const pai_ctx* c) {
   (void)c;
   if (const char* e = getenv("FLEXPAI_FB_MAX_BYTES")) return (uint64_t)strtod(e, nullptr);
   size_t fr = 0, tot = 0;
   if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 0;
   const uint64_t reserve = std::max<uint64_t>(4ull << 30, (uint64_t)tot / 12);
-  return fr > reserve ? fr - reserve : 0;
+  uint64_t b = fr > reserve ? fr - reserve : 0;
+  if (fb_window_auto()) {
+    const char* f = getenv("FLEXPAI_FB_AUTO_FRAC");
+    double frac = f ? atof(f) : 0.75;
+    if (!(frac > 0.0 && frac <= 1.0)) frac = 0.75;
+    b = std::min<uint64_t>(b, (uint64_t)(frac * (double)fr));
+  }
+  return b;
 }
 
 // Fixed-base break-even: the tables cost a one-time build (host bases + k_fb*_lohi/fill over 2 K 2^W rows,
@@ -1227,6 +1323,7 @@ static int set_private_impl(pai_ctx* c, HBig p, HBig q);
 // The fixed-base tables are not built here (ensure_fb, on the first device-RNG encryption).
 int pai_ctx_set_private(pai_ctx* c, const uint8_t* p_le, const uint8_t* q_le, size_t half_bytes) {
   if (!c || !p_le || !q_le) return fail(PAI_ERR_ARG, "pai_ctx_set_private: null argument");
+  CtxLock lk(c);
   HIPCHK(hipSetDevice(c->device));
   HBig p = HBig::from_le_bytes(p_le, half_bytes), q = HBig::from_le_bytes(q_le, half_bytes);
   if (cmp(mul(p, q), c->n) != 0) return fail(PAI_ERR_KEY, "given public key does not match the given p and q");
@@ -1236,6 +1333,10 @@ int pai_ctx_set_private(pai_ctx* c, const uint8_t* p_le, const uint8_t* q_le, si
   c->in_priv = true;
   const int rc = set_private_impl(c, p, q);
   c->in_priv = false;
+  if (!rc && !c->holder) {
+    c->holder = true;
+    ++g_key_holders;
+  }
   if (rc) {
     const std::string msg = g_last_error;
     for (void* a : c->priv_allocs) (void)hipFree(a);
@@ -1304,6 +1405,7 @@ void pai_ctx_destroy(pai_ctx* c) { delete c; }
 
 int pai_ctx_set_option(pai_ctx* c, int option, int value) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c);
   switch (option) {
     case PAI_OPT_CRT_ENCRYPT: c->crt_enabled = value != 0; return 0;
     case PAI_OPT_STAGE_TIMING: c->timing = value != 0; stage_reset(c); return 0;
@@ -1311,7 +1413,7 @@ int pai_ctx_set_option(pai_ctx* c, int option, int value) {
     case PAI_OPT_FIXED_BASE: c->fb_enabled = value != 0; return 0;
     case PAI_OPT_PUBLIC_FB: c->pfb_enabled = value != 0; return 0;
     case PAI_OPT_PFB_WINDOW:
-      if (!fb_window_ok(value)) return fail(PAI_ERR_ARG, "fixed-base window must be 8, 12, 16 or 20 .. 24");
+      if (!pfb_window_ok(value)) return fail(PAI_ERR_ARG, "public fixed-base window must be 12, 16 or 20");
       if (value == c->pfb_W) return 0;
       c->pfb_W = value;
       HIPCHK(hipSetDevice(c->device));
@@ -1332,6 +1434,7 @@ int pai_ctx_set_option(pai_ctx* c, int option, int value) {
 
 int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
   if (!c || !value) return fail(PAI_ERR_ARG, "null argument");
+  CtxLock lk(c);
   switch (option) {
     case PAI_OPT_CRT_ENCRYPT: *value = c->crt_enabled ? 1 : 0; return 0;
     case PAI_OPT_CRT_AVAILABLE: *value = c->crt_ok ? 1 : 0; return 0;
@@ -1347,7 +1450,7 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
       *value = (pfb_supported(c) && c->pfb_enabled && c->pfb_state != pai_ctx::FB_UNAVAILABLE) ? 1 : 0;
       return 0;
     case PAI_OPT_PFB_READY: *value = c->pfb_state == pai_ctx::FB_READY ? 1 : 0; return 0;
-    case PAI_OPT_PFB_WINDOW: *value = c->pfb_W_used ? c->pfb_W_used : c->pfb_W ? c->pfb_W : fb_default_window(); return 0;
+    case PAI_OPT_PFB_WINDOW: *value = c->pfb_W_used ? c->pfb_W_used : c->pfb_W ? c->pfb_W : pfb_default_window(); return 0;
     case PAI_OPT_FB_PAIR:
       *value = c->fb_state == pai_ctx::FB_READY ? (c->fb_gpair ? FBGP_S : c->fb_pair_s) : 0;
       return 0;
@@ -1365,13 +1468,14 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
 
 int pai_ctx_stage_times(pai_ctx* c, float* ms_out, int max_out, int* count) {
   if (!c || !count) return fail(PAI_ERR_ARG, "null argument");
+  CtxLock lk(c);
   *count = 0;
-  if (c->nev < 2 || c->nchunk_ev < 1) return 0;
+  if (c->nev < 2) return 0;
   HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipEventSynchronize(c->ev[c->nchunk_ev - 1][c->nev - 1]));
+  if (c->nchunk_ev > 0) HIPCHK(hipEventSynchronize(c->ev[c->nchunk_ev - 1][c->nev - 1]));
   const int k = std::min(c->nev - 1, max_out);
   for (int i = 0; i < k; ++i) {
-    ms_out[i] = 0.f;
+    ms_out[i] = i < 3 ? c->ev_acc[i] : 0.f;
     for (int ch = 0; ch < c->nchunk_ev; ++ch) {
       float t = 0.f;
       HIPCHK(hipEventElapsedTime(&t, c->ev[ch][i], c->ev[ch][i + 1]));
@@ -1384,6 +1488,7 @@ int pai_ctx_stage_times(pai_ctx* c, float* ms_out, int max_out, int* count) {
 
 int pai_ctx_fixed_base_info(pai_ctx* c, uint32_t* g_p, uint32_t* g_q, int* digits, int* window) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c);
   if (!c->crt_ok && !c->fbg_ok)
     return fail(PAI_ERR_NOPRIV, "fixed-base obfuscation not available (needs the private key)");
   HIPCHK(hipSetDevice(c->device));
@@ -1397,6 +1502,7 @@ int pai_ctx_fixed_base_info(pai_ctx* c, uint32_t* g_p, uint32_t* g_q, int* digit
 
 int pai_ctx_fixed_base_prepare(pai_ctx* c) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c);
   if (!c->crt_ok && !c->fbg_ok)
     return fail(PAI_ERR_NOPRIV, "fixed-base obfuscation not available (needs the private key)");
   HIPCHK(hipSetDevice(c->device));
@@ -1426,6 +1532,7 @@ static bool fb_wanted(pai_ctx* c, long long n) {
 
 int pai_ctx_fixed_base_policy(pai_ctx* c, long long* seen, long long* threshold) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c);
   if (seen) *seen = c->fb_seen;
   if (threshold) *threshold = fb_threshold(c);
   return 0;
@@ -1433,6 +1540,7 @@ int pai_ctx_fixed_base_policy(pai_ctx* c, long long* seen, long long* threshold)
 
 int pai_ctx_fixed_base_setup(const pai_ctx* c, float* host_ms, float* device_ms, uint64_t* table_bytes) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c);
   if (c->fb_state != pai_ctx::FB_READY) return fail(PAI_ERR_KEY, "fixed-base tables are not resident");
   if (host_ms) *host_ms = c->fb_host_ms;
   if (device_ms) *device_ms = c->fb_dev_ms;
@@ -1442,6 +1550,7 @@ int pai_ctx_fixed_base_setup(const pai_ctx* c, float* host_ms, float* device_ms,
 
 int pai_ctx_info(const pai_ctx* c, int* key_bits, int* ct_words, int* pt_words) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c);
   if (key_bits) *key_bits = c->nb;
   if (ct_words) *ct_words = c->ct_words;
   if (pt_words) *pt_words = c->pt_words;
@@ -1616,9 +1725,9 @@ static uint64_t pfb_bytes(const pai_ctx* c, int W) {
 }
 
 static int pfb_choose_window(pai_ctx* c) {
-  if (!c->pfb_W) c->pfb_W = fb_default_window();
+  if (!c->pfb_W) c->pfb_W = pfb_default_window();
   const uint64_t budget = fb_budget(c);
-  for (int w : {24, 23, 22, 21, 20, 16, 12, 8})
+  for (int w : {20, 16, 12})
     if (w <= c->pfb_W && pfb_bytes(c, w) <= budget) return w;
   return 0;
 }
@@ -1878,6 +1987,7 @@ static int launch_pfb(pai_ctx* c, const EncParams& e, hipStream_t st) {
 
 int pai_ctx_public_fb_prepare(pai_ctx* c) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c);
   HIPCHK(hipSetDevice(c->device));
   if (!ensure_pfb(c)) return fail(PAI_ERR_KEY, "public fixed-base obfuscation not available: " + c->pfb_reason);
   return 0;
@@ -1885,11 +1995,19 @@ int pai_ctx_public_fb_prepare(pai_ctx* c) {
 
 int pai_ctx_public_fb_set_bases(pai_ctx* c, const uint8_t* bases_le, size_t base_bytes, int nbases) {
   if (!c || !bases_le || base_bytes == 0) return fail(PAI_ERR_ARG, "pai_ctx_public_fb_set_bases: null argument");
+  CtxLock lk(c);
   if (nbases != PFB_NBASES) return fail(PAI_ERR_ARG, "pai_ctx_public_fb_set_bases: wrong number of bases");
   std::vector<HBig> bs;
   for (int j = 0; j < nbases; ++j) {
     HBig g = HBig::from_le_bytes(bases_le + (size_t)j * base_bytes, base_bytes);
     if (g.bits() < 2 || cmp(g, c->n) >= 0) return fail(PAI_ERR_ARG, "pai_ctx_public_fb_set_bases: need 1 < g < n");
+    // the distribution argument needs units, g_0 with Jacobi symbol -1 (so that (c mod n | n) is
+    // uniform) and distinct bases: reject anything weaker rather than sample a visibly biased r
+    if (inv_mod(g, c->n).is_zero()) return fail(PAI_ERR_ARG, "pai_ctx_public_fb_set_bases: a base is not a unit mod n");
+    for (const HBig& h : bs)
+      if (cmp(h, g) == 0) return fail(PAI_ERR_ARG, "pai_ctx_public_fb_set_bases: repeated base");
+    if (j == 0 && jacobi(g, c->n) != -1)
+      return fail(PAI_ERR_ARG, "pai_ctx_public_fb_set_bases: g_0 must have Jacobi symbol -1 mod n");
     bs.push_back(g);
   }
   HIPCHK(hipSetDevice(c->device));
@@ -1902,6 +2020,7 @@ int pai_ctx_public_fb_set_bases(pai_ctx* c, const uint8_t* bases_le, size_t base
 int pai_ctx_public_fb_info(pai_ctx* c, uint8_t* bases_le, size_t base_bytes, int* nbases, int* digits, int* window,
                            int* e0_digits) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c);
   if (c->pfb_state != pai_ctx::FB_READY) return fail(PAI_ERR_KEY, "public fixed-base tables are not resident");
   if (bases_le) {
     for (size_t j = 0; j < c->pfb_bases.size(); ++j) {
@@ -1919,6 +2038,7 @@ int pai_ctx_public_fb_info(pai_ctx* c, uint8_t* bases_le, size_t base_bytes, int
 
 int pai_ctx_public_fb_policy(pai_ctx* c, long long* seen, long long* threshold) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c);
   if (seen) *seen = c->pfb_seen;
   if (threshold) *threshold = pfb_threshold(c);
   return 0;
@@ -2053,6 +2173,7 @@ int pai_encrypt_dev(pai_ctx* c, int dtype, const void* d_x, size_t N, int exp_mo
                     const uint32_t* d_r_words, size_t r_stride_words, size_t r_words, const uint8_t* rng_key32,
                     uint64_t index_base, uint32_t* d_ct, int32_t* d_exp, int32_t* d_status, void* stream) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c, (hipStream_t)stream);
   if (N == 0) return 0;
   if (dtype < 0 || dtype > 2 || !d_x || !d_ct || !d_exp) return fail(PAI_ERR_ARG, "pai_encrypt_dev: bad arguments");
   if (obf_mode == PAI_OBF_GIVEN && (!d_r_words || r_words == 0 || r_words > (size_t)c->ct_words))
@@ -2165,6 +2286,7 @@ static int add_dev(pai_ctx* c, const uint32_t* cts, const int32_t* exps, int k, 
 int pai_add_dev(pai_ctx* c, const uint32_t* d_cts, const int32_t* d_exps, int k, size_t N, uint32_t* d_out,
                 int32_t* d_exp_out, void* stream) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c, (hipStream_t)stream);
   if (N == 0) return 0;
   if (k < 1 || !d_cts || !d_exps || !d_out || !d_exp_out) return fail(PAI_ERR_ARG, "pai_add_dev: bad arguments");
   HIPCHK(hipSetDevice(c->device));
@@ -2310,6 +2432,7 @@ static int launch_dec_lane(pai_ctx* c, const DecParams& d, hipStream_t st) {
 int pai_decrypt_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t N, double* d_val, int64_t* d_mant,
                     int32_t* d_status, uint32_t* d_raw, void* stream) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c, (hipStream_t)stream);
   if (!c->has_priv) return fail(PAI_ERR_NOPRIV, "pai_decrypt: context has no private key");
   if (N == 0) return 0;
   if (!d_ct || !d_exp || !d_val || !d_status) return fail(PAI_ERR_ARG, "pai_decrypt_dev: bad arguments");
@@ -2464,6 +2587,7 @@ static int add_dev(pai_ctx* c, const uint32_t* cts, const int32_t* exps, int k, 
 int pai_mul_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t N, int dtype, const void* d_x,
                 size_t x_stride, uint32_t* d_out, int32_t* d_exp_out, int32_t* d_status, void* stream) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c, (hipStream_t)stream);
   if (N == 0) return 0;
   if (!d_ct || !d_exp || !d_x || !d_out || !d_exp_out || dtype < 0 || dtype > 2 || x_stride > 1)
     return fail(PAI_ERR_ARG, "pai_mul_dev: bad arguments");
@@ -2494,6 +2618,7 @@ int pai_mul_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t N
 int pai_add_plain_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t N, int dtype, const void* d_x,
                       size_t x_stride, uint32_t* d_out, int32_t* d_exp_out, int32_t* d_status, void* stream) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c, (hipStream_t)stream);
   if (N == 0) return 0;
   if (!d_ct || !d_exp || !d_x || !d_out || !d_exp_out || dtype < 0 || dtype > 2 || x_stride > 1)
     return fail(PAI_ERR_ARG, "pai_add_plain_dev: bad arguments");
@@ -2531,6 +2656,7 @@ constexpr int SEG_CHUNK = 16;
 int pai_segment_add_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t N, const int64_t* index,
                         const int64_t* seg_off, size_t nseg, uint32_t* d_out, int32_t* d_exp_out, void* stream) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c, (hipStream_t)stream);
   if (nseg == 0) return 0;
   if (!d_ct || !d_exp || !seg_off || !d_out || !d_exp_out) return fail(PAI_ERR_ARG, "pai_segment_add_dev: bad arguments");
   if (seg_off[0] != 0) return fail(PAI_ERR_ARG, "pai_segment_add_dev: seg_off[0] must be 0");
@@ -2603,6 +2729,7 @@ constexpr int MATMUL_CHUNK = 16;   // operands per k_add pass of the reduction t
 int pai_matmul_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t m, size_t K, int dtype,
                    const void* d_x, size_t d, uint32_t* d_out, int32_t* d_exp_out, void* stream) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c, (hipStream_t)stream);
   if (m == 0 || d == 0) return 0;
   if (K == 0 || !d_ct || !d_exp || !d_x || !d_out || !d_exp_out || dtype < 0 || dtype > 2)
     return fail(PAI_ERR_ARG, "pai_matmul_dev: bad arguments");
@@ -2662,6 +2789,7 @@ int pai_matmul_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_
 int pai_mul(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, int dtype, const void* x, size_t x_stride,
             uint32_t* ct_out, int32_t* exp_out, int32_t* status_out) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c);
   if (N == 0) return 0;
   if (!ct || !exp || !x || !ct_out || !exp_out || x_stride > 1) return fail(PAI_ERR_ARG, "pai_mul: bad arguments");
   HIPCHK(hipSetDevice(c->device));
@@ -2689,6 +2817,7 @@ int pai_mul(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, int dt
 int pai_add_plain(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, int dtype, const void* x,
                   size_t x_stride, uint32_t* ct_out, int32_t* exp_out, int32_t* status_out) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c);
   if (N == 0) return 0;
   if (!ct || !exp || !x || !ct_out || !exp_out || x_stride > 1) return fail(PAI_ERR_ARG, "pai_add_plain: bad arguments");
   HIPCHK(hipSetDevice(c->device));
@@ -2716,6 +2845,7 @@ int pai_add_plain(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, 
 int pai_segment_add(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, const int64_t* index,
                     const int64_t* seg_off, size_t nseg, uint32_t* ct_out, int32_t* exp_out) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c);
   if (nseg == 0) return 0;
   if ((N && (!ct || !exp)) || !seg_off || !ct_out || !exp_out) return fail(PAI_ERR_ARG, "pai_segment_add: bad arguments");
   HIPCHK(hipSetDevice(c->device));
@@ -2741,6 +2871,7 @@ int pai_segment_add(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N
 int pai_matmul(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t m, size_t K, int dtype, const void* x,
                size_t d, uint32_t* ct_out, int32_t* exp_out) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c);
   if (m == 0 || d == 0) return 0;
   if (K == 0 || !ct || !exp || !x || !ct_out || !exp_out) return fail(PAI_ERR_ARG, "pai_matmul: bad arguments");
   HIPCHK(hipSetDevice(c->device));
@@ -2852,6 +2983,7 @@ int pai_encrypt(pai_ctx* c, int dtype, const void* x, size_t N, int exp_mode, in
                 const uint8_t* r_le, size_t r_stride_bytes, size_t r_bytes, const uint8_t* rng_key32,
                 uint64_t index_base, uint32_t* ct_out, int32_t* exp_out, int32_t* status_out) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c);
   if (N == 0) return 0;
   if (!x || !ct_out || !exp_out) return fail(PAI_ERR_ARG, "pai_encrypt: null buffer");
   if (obf_mode == PAI_OBF_GIVEN && (!r_le || r_bytes == 0)) return fail(PAI_ERR_ARG, "pai_encrypt: r required");
@@ -2923,6 +3055,7 @@ int pai_encrypt(pai_ctx* c, int dtype, const void* x, size_t N, int exp_mode, in
 int pai_add(pai_ctx* c, const uint32_t* const* cts, const int32_t* const* exps, int k, size_t N, uint32_t* ct_out,
             int32_t* exp_out) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c);
   if (N == 0) return 0;
   if (k < 1 || !cts || !exps || !ct_out || !exp_out) return fail(PAI_ERR_ARG, "pai_add: bad arguments");
   for (int j = 0; j < k; ++j)
@@ -2969,6 +3102,7 @@ int pai_add(pai_ctx* c, const uint32_t* const* cts, const int32_t* const* exps, 
 int pai_decrypt(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, double* val_out, int64_t* mant_out,
                 int32_t* status_out, uint32_t* raw_out) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
+  CtxLock lk(c);
   if (!c->has_priv) return fail(PAI_ERR_NOPRIV, "pai_decrypt: context has no private key");
   if (N == 0) return 0;
   if (!ct || !exp || !val_out || !status_out) return fail(PAI_ERR_ARG, "pai_decrypt: null buffer");
@@ -3014,6 +3148,7 @@ int pai_decrypt(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, do
 // (k_fb, k_fbg), or canonical pairs [2][2S][n] with *sb = 2S when the pair tables are resident (k_fbp).
 extern "C" int pai_debug_fb_w(pai_ctx* c, uint32_t* out, size_t max_words, long long* n, int* sb) {
   if (!c || !c->fb_last_w) return fail(PAI_ERR_ARG, "no fixed-base output");
+  CtxLock lk(c);
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipDeviceSynchronize());
   const int rows = c->fb_pair_s ? 2 * c->fb_pair_s : c->crt_sb;
@@ -3054,6 +3189,7 @@ static int launch_debug(pai_ctx* c, DbgParams& p) {
 extern "C" int pai_debug_engine(pai_ctx* c, int op, const uint32_t* a, const uint32_t* b, size_t N, uint32_t* out,
                                 int32_t* flag) {
   if (!c || N == 0) return fail(PAI_ERR_ARG, "pai_debug_engine: bad args");
+  CtxLock lk(c);
   HIPCHK(hipSetDevice(c->device));
   DevScope ds;
   const size_t W = c->ct_words;

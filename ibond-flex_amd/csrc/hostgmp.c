@@ -594,7 +594,188 @@ static PyObject* g_packed_valid(PyObject* self, PyObject* const* args, Py_ssize_
   return PyBool_FromLong(ok);
 }
 
+/* pack_numbers(cls, objs, public_key, nwords, want_words) -> (words, exps, ints) or None
+ *
+ * The received-array half of PaillierDecryptor.decrypt and of the array operators (decryptor.py:53-55 and
+ * cipher_array.pack): for an object array of PaillierEncryptedNumber in one pass
+ *   - the reference's per-element _check (decryptor.py:73-79): every element is a `cls` (subclasses too) and its
+ *     public_key IS `public_key` or compares equal to it (PaillierPublicKey.__eq__; the last equal object is
+ *     remembered, and an unpickled array shares one key object, so this is an identity test per element);
+ *   - the exponents (int32 bytes) and the ciphertext slots (a list of the ints, for the packed cache);
+ *   - with want_words, the ciphertexts as rows of `nwords` little-endian 32-bit words (bytes): the GIL pass
+ *     only collects the int objects; the digit repacking runs on up to 16 threads without the GIL.
+ * Returns None when any element fails a check or a value does not fit (negative, too wide, exponent beyond
+ * int32): the caller then runs the reference's per-element path, which raises the reference's exception. */
+typedef struct {
+  PyObject** ints;
+  unsigned char* out;
+  Py_ssize_t lo, hi, nw;
+  int bad;
+} i2w_job;
+
+static void* i2w_fill(void* arg) {
+  i2w_job* j = (i2w_job*)arg;
+  for (Py_ssize_t i = j->lo; i < j->hi; ++i) {
+    const PyLongObject* l = (const PyLongObject*)j->ints[i];
+    const Py_ssize_t nd = Py_SIZE(l);
+    uint32_t* w = (uint32_t*)(j->out + (size_t)i * 4 * j->nw);
+    memset(w, 0, (size_t)4 * j->nw);
+    if (nd < 0) {
+      j->bad = 1;
+      continue;
+    }
+    uint64_t acc = 0;
+    int have = 0;
+    Py_ssize_t k = 0;
+    for (Py_ssize_t d = 0; d < nd; ++d) {
+      acc |= (uint64_t)l->ob_digit[d] << have;
+      have += PyLong_SHIFT;
+      while (have >= 32) {
+        if (k >= j->nw) {
+          if ((uint32_t)acc) j->bad = 1;
+        } else {
+          w[k] = (uint32_t)acc;
+        }
+        ++k;
+        acc >>= 32;
+        have -= 32;
+      }
+    }
+    if (have > 0 && acc) {
+      if (k >= j->nw) j->bad = 1;
+      else w[k] = (uint32_t)acc;
+    }
+  }
+  return NULL;
+}
+
+static PyObject* g_pack_numbers(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  (void)self;
+  if (nargs != 5 || !PyType_Check(args[0])) {
+    PyErr_SetString(PyExc_TypeError, "pack_numbers(cls, objs, public_key, nwords, want_words)");
+    return NULL;
+  }
+  PyTypeObject* cls = (PyTypeObject*)args[0];
+  const char* cname = cls->tp_name;
+  const char* dot = strrchr(cname, '.');
+  if (dot) cname = dot + 1;
+  char nct[256];
+  snprintf(nct, sizeof nct, "_%s__ciphertext", cname);
+  Py_ssize_t o_pk, o_ex, o_ct;
+  if ((o_pk = slot_offset(args[0], "public_key")) < 0 || (o_ex = slot_offset(args[0], "exponent")) < 0 ||
+      (o_ct = slot_offset(args[0], nct)) < 0)
+    return NULL;
+  const Py_ssize_t nw = PyLong_AsSsize_t(args[3]);
+  if (nw <= 0) {
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "nwords must be positive");
+    return NULL;
+  }
+  const int want = PyObject_IsTrue(args[4]);
+  if (want < 0) return NULL;
+  PyObject* objs = PySequence_Fast(args[1], "pack_numbers: objs must be a sequence");
+  if (!objs) return NULL;
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(objs);
+  PyObject** it = PySequence_Fast_ITEMS(objs);
+  PyObject* key = args[2];
+  PyObject* same_key = key;            /* the last key object found equal to `key` */
+  PyObject *ints = NULL, *exps = NULL, *words = NULL, *res = NULL;
+  int ok = 1;
+  ints = PyList_New(n);
+  exps = PyBytes_FromStringAndSize(NULL, n * 4);
+  if (!ints || !exps) goto done;
+  int32_t* e = (int32_t*)PyBytes_AS_STRING(exps);
+  for (Py_ssize_t i = 0; i < n && ok; ++i) {
+    PyObject* o = it[i];
+    if (!PyObject_TypeCheck(o, cls)) {
+      ok = 0;
+      break;
+    }
+    PyObject* pk = *(PyObject**)((char*)o + o_pk);
+    if (!pk) {
+      ok = 0;
+      break;
+    }
+    if (pk != key && pk != same_key) {
+      const int eq = PyObject_RichCompareBool(pk, key, Py_EQ);
+      if (eq < 0) goto done;
+      if (!eq) {
+        ok = 0;
+        break;
+      }
+      same_key = pk;
+    }
+    PyObject* ct = *(PyObject**)((char*)o + o_ct);
+    PyObject* ex = *(PyObject**)((char*)o + o_ex);
+    if (!ct || !ex || !PyLong_CheckExact(ct) || !PyLong_Check(ex)) {
+      ok = 0;
+      break;
+    }
+    int over = 0;
+    const long long v = PyLong_AsLongLongAndOverflow(ex, &over);
+    if (over || v < INT32_MIN || v > INT32_MAX) {
+      if (PyErr_Occurred()) goto done;
+      ok = 0;
+      break;
+    }
+    e[i] = (int32_t)v;
+    Py_INCREF(ct);
+    PyList_SET_ITEM(ints, i, ct);
+  }
+  if (!ok) {
+    res = Py_None;
+    Py_INCREF(res);
+    goto done;
+  }
+  if (want) {
+    words = PyBytes_FromStringAndSize(NULL, n * 4 * nw);
+    if (!words) goto done;
+    PyObject** iv = ((PyListObject*)ints)->ob_item;
+    long nt = sysconf(_SC_NPROCESSORS_ONLN);
+    if (nt > W2I_THREADS_MAX) nt = W2I_THREADS_MAX;
+    if (nt > n / W2I_ROWS_MIN) nt = (long)(n / W2I_ROWS_MIN);
+    if (nt < 1) nt = 1;
+    i2w_job jobs[W2I_THREADS_MAX];
+    pthread_t th[W2I_THREADS_MAX];
+    int started[W2I_THREADS_MAX] = {0};
+    const Py_ssize_t per = (n + nt - 1) / nt;
+    for (long t = 0; t < nt; ++t) {
+      jobs[t].ints = iv;
+      jobs[t].out = (unsigned char*)PyBytes_AS_STRING(words);
+      jobs[t].lo = t * per < n ? t * per : n;
+      jobs[t].hi = (t + 1) * per < n ? (t + 1) * per : n;
+      jobs[t].nw = nw;
+      jobs[t].bad = 0;
+    }
+    /* the ints are referenced by `ints` (immutable objects): reading their digits needs no GIL */
+    Py_BEGIN_ALLOW_THREADS
+    for (long t = 1; t < nt; ++t) started[t] = pthread_create(&th[t], NULL, i2w_fill, &jobs[t]) == 0;
+    i2w_fill(&jobs[0]);
+    for (long t = 1; t < nt; ++t) {
+      if (started[t]) pthread_join(th[t], NULL);
+      else i2w_fill(&jobs[t]);
+    }
+    Py_END_ALLOW_THREADS
+    for (long t = 0; t < nt; ++t)
+      if (jobs[t].bad) {
+        res = Py_None;
+        Py_INCREF(res);
+        goto done;
+      }
+  } else {
+    words = Py_None;
+    Py_INCREF(words);
+  }
+  res = PyTuple_Pack(3, words, exps, ints);
+done:
+  Py_XDECREF(words);
+  Py_XDECREF(exps);
+  Py_XDECREF(ints);
+  Py_DECREF(objs);
+  return res;
+}
+
 static PyMethodDef methods[] = {
+    {"pack_numbers", (PyCFunction)(void (*)(void))g_pack_numbers, METH_FASTCALL, "checks + words of received numbers"},
     {"packed_valid", (PyCFunction)(void (*)(void))g_packed_valid, METH_FASTCALL, "cached words still match"},
     {"make_numbers", (PyCFunction)(void (*)(void))g_make_numbers, METH_FASTCALL, "bulk slot construction"},
     {"words_to_ints", (PyCFunction)(void (*)(void))g_words_to_ints, METH_FASTCALL, "rows of LE 32-bit words -> ints"},

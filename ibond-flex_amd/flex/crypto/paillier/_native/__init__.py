@@ -55,6 +55,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         if not os.path.exists(path):
             raise NativeError(f"flexpai native library not found at {path}; run __graft_entry__.build() "
                               f"(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        _start_torch_runtime_first()
         lib = ctypes.CDLL(path)
         P, S, I, U64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
         lib.pai_device_count.argtypes = [P]
@@ -101,6 +102,23 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                 getattr(lib, name).restype = ctypes.c_int
         _lib = lib
         return lib
+
+
+def _start_torch_runtime_first() -> None:
+    """PyTorch-ROCm wheels bundle their own HIP and HSA runtimes. In one process only the runtime that opens the
+    GPU first works: once libflexpai's (/opt/rocm) runtime has started, torch.cuda fails with "No HIP GPUs are
+    available". A process that has already imported torch (device buffers for the *_dev entry points, a
+    torch.distributed job) gets torch's runtime started here, before flexpai's first HIP call; torch is never
+    imported by this package. See INTEGRATION.md (PyTorch)."""
+    import sys
+    torch = sys.modules.get("torch")
+    if torch is None or os.environ.get("FLEXPAI_NO_TORCH_INIT"):
+        return
+    try:
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:   # noqa: BLE001 - torch without a usable GPU: flexpai's own runtime still works
+        pass
 
 
 def device_count() -> int:
@@ -260,7 +278,7 @@ class Context:
         return self._get_option(PAI_OPT_FB_WINDOW)
 
     def set_fb_window(self, bits: int):
-        """Digit window of the fixed-base tables (8, 12, 16 or 20); the tables are rebuilt lazily."""
+        """Digit window of the fixed-base tables (8, 12, 16 or 20 .. 24); the tables are rebuilt lazily."""
         _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_FB_WINDOW, int(bits)))
 
     @property
@@ -314,13 +332,15 @@ class Context:
         return bool(self._get_option(PAI_OPT_PFB_READY))
 
     def set_pfb_window(self, bits: int):
+        """Digit window of the public tables: 12, 16 or 20 (the windows pinned to the reference's goldens)."""
         _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_PFB_WINDOW, int(bits)))
 
     def prepare_public_fixed_base(self):
         _check(self.lib.pai_ctx_public_fb_prepare(self._h))
 
     def set_public_bases(self, bases: Sequence[int]):
-        """Fix the 33 bases g_0..g_32 (each 1 < g < n) instead of drawing them (tests, reproducible runs)."""
+        """Fix the 33 bases g_0..g_32 instead of drawing them (tests, reproducible runs). Each must be a unit
+        in (1, n), all distinct, and g_0 must have Jacobi symbol -1 mod n (else NativeError)."""
         nb = (self.n.bit_length() + 7) // 8
         buf = b"".join(int_to_le(g, nb) for g in bases)
         _check(self.lib.pai_ctx_public_fb_set_bases(self._h, buf, nb, len(bases)))

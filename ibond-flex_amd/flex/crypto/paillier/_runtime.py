@@ -52,13 +52,25 @@ def gpu_available() -> bool:
     return _gpus[1] > 0
 
 
+_evict_warned = False
+
+
 def register_private(public_key, private_key) -> None:
     """Remember this process's private key for `public_key` (enables CRT encryption)."""
+    global _evict_warned
     with _lock:
         _private[public_key.n] = private_key
         _private.move_to_end(public_key.n)
         while len(_private) > max_contexts():    # bounded like the contexts (HE_SA_FT re-keys per exchange)
-            _private.popitem(last=False)
+            n_old, _ = _private.popitem(last=False)
+            # a context of that key still cached keeps its private part (set_private is never undone), but a
+            # context created for it later encrypts on the public-key kernels: say so once (ADVICE r3)
+            if not _evict_warned and not os.environ.get("FLEXPAI_QUIET"):
+                import sys
+                print(f"flexpai: more than FLEXPAI_MAX_CONTEXTS={max_contexts()} private keys registered; the least "
+                      "recently registered one is dropped, and a later context for it encrypts through the slower "
+                      "public-key kernels (results unchanged). Raise FLEXPAI_MAX_CONTEXTS to keep it.", file=sys.stderr)
+                _evict_warned = True
 
 
 def _evict_lru() -> None:

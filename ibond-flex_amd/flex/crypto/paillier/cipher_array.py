@@ -46,9 +46,9 @@ from .encrypted_number import PaillierEncryptedNumber
 _CT = "_PaillierEncryptedNumber__ciphertext"
 
 try:                                        # bulk slot construction and checks (csrc/hostgmp.c), when built
-    from ._gmp import make_numbers as _make_numbers, packed_valid as _packed_valid
+    from ._gmp import make_numbers as _make_numbers, packed_valid as _packed_valid, pack_numbers as _pack_numbers
 except ImportError:                         # pragma: no cover - build() always builds it
-    _make_numbers = _packed_valid = None
+    _make_numbers = _packed_valid = _pack_numbers = None
 
 
 class _Packed:
@@ -128,6 +128,8 @@ class PaillierArray(np.ndarray):
         res = NotImplemented
         if _plain_operand(other):
             res = add_plain(self, other * -1)
+        elif _encrypted_like(other):
+            res = sub_encrypted(self, other)
         if res is NotImplemented:
             return np.ndarray.__sub__(np.asarray(self), other)
         return res
@@ -139,6 +141,8 @@ class PaillierArray(np.ndarray):
             neg = mul_plain(self, -1)
             if neg is not NotImplemented:
                 res = add_plain(neg, other)
+        elif _encrypted_like(other):
+            res = sub_encrypted(other, self)
         if res is NotImplemented:
             return np.ndarray.__rsub__(np.asarray(self), other)
         return res
@@ -188,11 +192,29 @@ def pack(arr: np.ndarray, public_key) -> Tuple[np.ndarray, np.ndarray, list]:
         if pk is not None and pk.n == public_key.n:
             return pk.words, pk.exps.astype(np.int32), pk.ints
     flat = np.asarray(arr).reshape(-1)
-    ints = [e.ciphertext(False) for e in flat]
     W = (2 * public_key.n.bit_length() + 31) // 32
+    got = pack_checked(flat, public_key, W)
+    if got is not None:
+        return got
+    ints = [e.ciphertext(False) for e in flat]
     words = _runtime.ints_to_words(ints, W)
     exps = np.fromiter((e.exponent for e in flat), dtype=np.int64, count=flat.size)
     return words, exps.astype(np.int32), ints
+
+
+def pack_checked(flat: np.ndarray, public_key, W: int, want_words: bool = True):
+    """One C pass over a flat object array (csrc/hostgmp.c pack_numbers): the reference's per-element check
+    (every element a PaillierEncryptedNumber under `public_key`, decryptor.py:73-79), the exponents, the
+    ciphertext ints and -- with want_words -- their [N, W] words. None when an element fails a check or does
+    not fit (the caller's per-element path then raises the reference's exception)."""
+    if _pack_numbers is None:
+        return None
+    got = _pack_numbers(PaillierEncryptedNumber, flat, public_key, W, want_words)
+    if got is None:
+        return None
+    words, exps, ints = got
+    w = np.frombuffer(words, dtype="<u4").reshape(len(ints), W) if words is not None else None
+    return w, np.frombuffer(exps, dtype=np.int32), ints
 
 
 def materialize(public_key, words: np.ndarray, exps: np.ndarray, shape, obfuscated) -> PaillierArray:
@@ -271,6 +293,27 @@ def add_encrypted(a, b):
     out, oe = ctx.add([wa, wb], [ea, eb])
     # __raw_add builds fresh, not-yet-obfuscated numbers (encrypted_number.py:180-185)
     return materialize(pk, out, oe, Ab.shape, obfuscated=False)
+
+
+def _encrypted_like(y) -> bool:
+    return isinstance(y, PaillierEncryptedNumber) or (isinstance(y, np.ndarray) and y.dtype == object)
+
+
+def sub_encrypted(a, b):
+    """a - b with both operands encrypted (a PaillierEncryptedNumber or an object array of them, numpy
+    broadcasting): a + (b * -1) per element (encrypted_number.py:74-78) as ONE k_mul by -1 (invert(c), the
+    reference's negative-scalar branch, encrypted_number.py:97-101) and ONE 2-way k_add. The add is order
+    independent, so a scalar left operand is added on the right. NotImplemented when an operand is not
+    entirely PaillierEncryptedNumber (or there is no GPU): the caller falls back to numpy's per-element loop."""
+    if isinstance(b, PaillierEncryptedNumber):
+        neg = b * -1
+    else:
+        neg = mul_plain(b, -1)
+        if neg is NotImplemented:
+            return NotImplemented
+    if isinstance(a, PaillierEncryptedNumber):
+        return add_encrypted(neg, a) if isinstance(neg, np.ndarray) else NotImplemented
+    return add_encrypted(a, neg)
 
 
 # ------------------------------------------------------------------ ciphertext x plaintext

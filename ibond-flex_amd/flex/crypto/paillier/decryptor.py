@@ -44,12 +44,23 @@ class PaillierDecryptor(object):
         return v.item() if isinstance(v, np.generic) else v
 
     def _decrypt_numpy(self, encrypted_number_numpy: np.ndarray) -> np.ndarray:
-        """decryptor.py:91-112, one batched GPU launch."""
-        from .cipher_array import pack
+        """decryptor.py:91-112, one batched GPU launch. The per-element _check and the packing of the
+        ciphertexts run as one C pass (cipher_array.pack_checked; a PaillierArray whose packed words are
+        still valid only checks); the reference's exceptions come from the per-element path when it fails."""
+        from .cipher_array import PaillierArray, pack, pack_checked
         s = encrypted_number_numpy.shape
         flat = np.asarray(encrypted_number_numpy).reshape(-1)
         if flat.size == 0:
             return np.array([]).reshape(s)
+        W = (2 * self.pub_key.n.bit_length() + 31) // 32
+        cached = encrypted_number_numpy._valid_packed() if isinstance(encrypted_number_numpy, PaillierArray) else None
+        if cached is not None and cached.n == self.pub_key.n:
+            if pack_checked(flat, self.pub_key, W, want_words=False) is not None:
+                return self._decrypt_words(cached.words, cached.exps.astype(np.int32), s)
+        else:
+            got = pack_checked(flat, self.pub_key, W)
+            if got is not None:
+                return self._decrypt_words(got[0], got[1], s)
         for e in flat:
             self._check(e)
         words, exps, _ = pack(encrypted_number_numpy, self.pub_key)

@@ -37,6 +37,20 @@
  *   - Return value 0 = success; negative = error, message in pai_last_error() (thread local).
  *   - Per-element outcomes are reported in an int32 status array (PAI_EL_*), mapped by the Python
  *     layer onto the reference's exceptions.
+ *   - Threads: a context may be shared by several threads. Every entry point that takes a pai_ctx holds
+ *     the context's (recursive) mutex for the whole call, and a *_dev call's stream first waits for the
+ *     device work of the context's previous call, whatever stream that was on (the context's scratch,
+ *     work and table buffers are shared by all its calls). Calls on one context therefore run one after
+ *     the other; contexts of different keys run concurrently. pai_ctx_destroy must not race other calls
+ *     on the same context. (The reference never shares this state: it pickles the key into pool
+ *     processes, encryptor.py:89-96.)
+ *   - Reproducibility: PAI_OBF_RNG ciphertexts depend only on (rng_key, global index) for a given sampler,
+ *     but the sampler is chosen per context: the fixed-base tables are built only once a context has seen
+ *     the break-even element count (pai_ctx_fixed_base_policy). Two process layouts (one process vs
+ *     sharded ranks, whose shards may sit below the threshold) give the same bits only when the tables are
+ *     built up front (pai_ctx_fixed_base_prepare / pai_ctx_public_fb_prepare) or $FLEXPAI_FB_MIN_ELEMS /
+ *     $FLEXPAI_PFB_MIN_ELEMS = 0; otherwise the outputs differ in bits but decrypt identically and have
+ *     the same distribution.
  */
 #ifndef FLEXPAI_H
 #define FLEXPAI_H
@@ -95,7 +109,11 @@ typedef struct pai_comm pai_comm;
                                     $FLEXPAI_FB_WINDOW); setting it drops the tables (rebuilt lazily). Read
                                     back: the window of the resident tables, which is the largest one <= the
                                     requested window whose 2 K 2^W rows fit $FLEXPAI_FB_MAX_BYTES (default:
-                                    free device memory less 4 GiB)                                        */
+                                    free device memory less max(4 GiB, 1/12 of the device)).
+                                    $FLEXPAI_FB_WINDOW=auto: a process holding ONE private key asks for 24 and
+                                    gets the largest window whose tables fit $FLEXPAI_FB_AUTO_FRAC (default
+                                    0.75) of the free memory (W = 23 at nb = 2048, 21 at nb = 4096 on an idle
+                                    MI355X); a process holding several keys gets 16                          */
 #define PAI_OPT_FB_READY 7       /* read-only: 1 when the fixed-base tables are resident                    */
 #define PAI_OPT_FB_PAIR 8        /* read-only: limbs of p_h (19, 37; 76 for the 4096-bit pair-group tables)
                                     when the resident tables are pair tables (kernels_fbp.hpp,
@@ -110,8 +128,9 @@ typedef struct pai_comm pai_comm;
                                   * is reached (pai_ctx_public_fb_policy); get: 1 when the path is enabled and not
                                   * known unavailable                                                          */
 #define PAI_OPT_PFB_READY 11     /* read-only: 1 when the public fixed-base tables are resident               */
-#define PAI_OPT_PFB_WINDOW 12    /* digit window of the public tables (as PAI_OPT_FB_WINDOW; default 16:
-                                  * 324 rows of 512 B per element, 10.9 GB of tables)                        */
+#define PAI_OPT_PFB_WINDOW 12    /* digit window of the public tables: 12, 16 or 20 (the windows pinned to the
+                                  * reference's goldens; default 16: 324 rows of 512 B per element, 10.9 GB of
+                                  * tables; $FLEXPAI_FB_WINDOW=auto: 20 for a process with one context)       */
 #define PAI_OPT_SPLIT_SAMPLER 13 /* read-only: bit 0 = the resident 4096-bit key-holder tables, bit 1 = the resident
                                   * public tables are sampled on split pairs (kernels_sgp.hpp: k_sgp, the default;
                                   * $FLEXPAI_SGP=0 at table build selects k_fbgp / k_pfb)                      */
@@ -127,8 +146,9 @@ void pai_ctx_destroy(pai_ctx* ctx);
  * multiply-accumulates); PAI_OPT_CRT_ENCRYPT = 0 forces the public-key kernel. */
 int pai_ctx_set_option(pai_ctx* ctx, int option, int value);
 int pai_ctx_get_option(const pai_ctx* ctx, int option, int* value);
-/* With PAI_OPT_STAGE_TIMING on: kernel durations (ms) of the last encrypt call, summed over its chunks
- * (a host-buffer call's chunks included), in launch order (CRT: stage A, stage B, finish; public key on pairs: k_pe_pre, k_pe_pow, k_pe_fin; other public-key
+/* With PAI_OPT_STAGE_TIMING on: kernel durations (ms) of the last encrypt call, summed over all its chunks
+ * (a host-buffer call's chunks included; past 64 chunks the recorded ones are folded into running sums,
+ * which waits for them), in launch order (CRT: stage A, stage B, finish; public key on pairs: k_pe_pre, k_pe_pow, k_pe_fin; other public-key
  * paths: the one encrypt kernel). Waits for them. */
 int pai_ctx_stage_times(pai_ctx* ctx, float* ms_out, int max_out, int* count);
 /* key bits, 32-bit words per ciphertext (2*key_bits/32), words per plaintext (key_bits/32) */
@@ -166,7 +186,9 @@ int pai_ctx_fixed_base_policy(pai_ctx* ctx, long long* seen, long long* threshol
  * reference's encryption of x under that r.                                                            */
 int pai_ctx_public_fb_prepare(pai_ctx* ctx);
 /* Use these bases (nbases = 33, each base_bytes little-endian, 1 < g < n) instead of random ones; drops
- * resident public tables (rebuilt lazily). For reproducible runs and the parity tests.                  */
+ * resident public tables (rebuilt lazily). For reproducible runs and the parity tests. PAI_ERR_ARG unless
+ * every base is a unit mod n, the bases are distinct and g_0 has Jacobi symbol (g_0 | n) = -1: the
+ * conditions of the distribution argument that a caller can check.                      */
 int pai_ctx_public_fb_set_bases(pai_ctx* ctx, const uint8_t* bases_le, size_t base_bytes, int nbases);
 /* The resident public tables' bases (nbases x base_bytes, nullable), digit count K, window W, and K0.
  * PAI_ERR_KEY when the tables are not resident.                                                        */

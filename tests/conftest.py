@@ -16,6 +16,22 @@ for p in (ROOT, PKG):
 os.environ.setdefault("FLEXPAI_FB_MIN_ELEMS", "0")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first(request):
+    """PyTorch-ROCm ships its own HIP and HSA runtimes; in one process the runtime that opens the device first
+    wins, and torch's fails ("No HIP GPUs are available") once libflexpai's has started. GPU test sessions that
+    use torch buffers therefore start torch's runtime before any flexpai call (PyTorch)."""
+    mark = request.config.getoption("-m") or ""
+    if "gpu" in mark and "not gpu" not in mark:
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except Exception:   # noqa: BLE001 - a session without a usable torch still runs the C-ABI tests
+            pass
+    yield
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through the HIP C-ABI)")
     config.addinivalue_line("markers", "slow: long-running CPU test")

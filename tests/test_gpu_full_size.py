@@ -1,4 +1,5 @@
-"""GPU parity at BASELINE.json's full sizes (configs[1], configs[2]: 1 048 576 elements, nb = 2048),
+"""GPU parity at BASELINE.json's full sizes (configs[1], configs[2]: 1 048 576 elements, nb = 2048; configs[3]:
+16 777 216 elements as 8 shards; configs[4]: one rank's 524 288-element shard at nb = 4096),
 through the C ABI, checked by size-independent properties plus a bit-exact oracle sample:
 
 * decrypt(encrypt(x)) == x exactly for every element (fixed-base key-holder path, the bench's timed
@@ -111,3 +112,91 @@ def test_full_size_4096_sample(golden):
         assert (got[j], int(ex[i])) == O.fb_encrypt_value(x[i], key, rk, 7 + i, params)
     half, _, _ = ctx.encrypt(x[n // 2:], obf_mode=Nn.PAI_OBF_RNG, rng_key=rk, index_base=7 + n // 2)
     assert np.array_equal(half, ct[n // 2:])
+
+
+def _dev_encrypt(lib, Nn, ctx, dx, n, rk, base, ct, ex, st, stream):
+    rc = lib.pai_encrypt_dev(ctx.handle, Nn.PAI_F32, dx, n, 0, 0, Nn.PAI_OBF_RNG, None, 0, 0, rk, base, ct, ex, st, stream)
+    assert rc == 0, lib.pai_last_error().decode()
+
+
+def test_config3_full_size_sharded(ctx2048):
+    """configs[3] at its full size on one GPU: 16 777 216 elements (nb = 2048) at the bench's window W = 23,
+    encrypted as the 8 contiguous shards of an 8-GPU run (index_base = the shard's first global index,
+    sharding.shard_bounds) into one buffer -- the all-gather's output layout -- equal bit for bit to ONE
+    unsharded call; the oracle's restatement of the sampler matches at every shard seam (first and last
+    element of each shard); decryption reproduces all 16M inputs exactly with every status OK. Reference
+    semantics: flex/crypto/paillier/encryptor.py:71-97 (element-wise, order independent), obfuscator.py:35-37."""
+    import torch
+    from flex.crypto.paillier import _native as Nn
+    from flex.crypto.paillier.sharding import shard_bounds
+    ctx, key = ctx2048
+    lib = Nn.load_library()
+    total, world, W = 16 << 20, 8, ctx.ct_words
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    x = np.random.default_rng(33).standard_normal(total, dtype=np.float32)
+    rk = bytes(range(100, 132))
+    try:
+        ctx.set_fb_window(23)
+        ctx.prepare_fixed_base()
+        params = ctx.fixed_base_info()
+        assert params[3] == 23
+        dx = torch.from_numpy(x).to(dev)
+        whole = torch.empty((total, W), dtype=torch.int32, device=dev)
+        wex = torch.empty(total, dtype=torch.int32, device=dev)
+        st = torch.empty(total, dtype=torch.int32, device=dev)
+        _dev_encrypt(lib, Nn, ctx, dx.data_ptr(), total, rk, 0, whole.data_ptr(), wex.data_ptr(), st.data_ptr(), s)
+        assert int(torch.count_nonzero(st).item()) == 0
+        shards = torch.empty_like(whole)
+        sex = torch.empty_like(wex)
+        seams = []
+        for r in range(world):
+            lo, hi = shard_bounds(total, world, r)
+            _dev_encrypt(lib, Nn, ctx, dx[lo:].data_ptr(), hi - lo, rk, lo, shards[lo:].data_ptr(), sex[lo:].data_ptr(),
+                         st[lo:].data_ptr(), s)
+            seams += [lo, hi - 1]
+        assert torch.equal(shards, whole) and torch.equal(sex, wex), "sharded != unsharded"
+        del shards, sex
+        got = Nn.words_to_ints(whole[seams].cpu().numpy().view(np.uint32))
+        gex = wex[seams].cpu().numpy()
+        for j, i in enumerate(seams):
+            assert (got[j], int(gex[j])) == O.fb_encrypt_value(x[i], key, rk, i, params), f"seam element {i}"
+        val = torch.empty(total, dtype=torch.float64, device=dev)
+        rc = lib.pai_decrypt_dev(ctx.handle, whole.data_ptr(), wex.data_ptr(), total, val.data_ptr(), None,
+                                 st.data_ptr(), None, s)
+        assert rc == 0, lib.pai_last_error().decode()
+        assert int(torch.count_nonzero(st).item()) == 0
+        assert torch.equal(val, dx.double()), "16M round trip"
+    finally:
+        torch.cuda.synchronize()
+        ctx.set_fb_window(16)
+        torch.cuda.empty_cache()
+
+
+def test_config4_shard_full_size_4096(golden):
+    """configs[4]'s per-rank shard at N = 8 (4M / 8 = 524 288 elements, nb = 4096) at the bench's window
+    W = 21: exact round trip, every status OK, the oracle's restatement of the sampler on a sample
+    (first, seams, last)."""
+    from flex.crypto.paillier import _native as Nn
+    k = golden["keys"]["4096"]
+    key = O.Key(int(k["n"], 16), int(k["p"], 16), int(k["q"], 16))
+    ctx = Nn.Context(key.n, 0, key.p, key.q)
+    try:
+        ctx.set_fb_window(21)
+        ctx.prepare_fixed_base()
+        params = ctx.fixed_base_info()
+        assert params[3] == 21
+        n = 1 << 19
+        base = 3 * n                                       # rank 3's shard of the 4M vector
+        x = np.random.default_rng(44).standard_normal(n, dtype=np.float32)
+        rk = bytes(range(60, 92))
+        ct, ex, st = ctx.encrypt(x, obf_mode=Nn.PAI_OBF_RNG, rng_key=rk, index_base=base)
+        assert np.all(st == 0)
+        val, _, dst, _ = ctx.decrypt(ct, ex)
+        assert np.all(dst == 0) and np.array_equal(val, x.astype(np.float64))
+        idx = [0, 1, n // 2 - 1, n // 2, n - 1]
+        got = Nn.words_to_ints(ct[idx])
+        for j, i in enumerate(idx):
+            assert (got[j], int(ex[i])) == O.fb_encrypt_value(x[i], key, rk, base + i, params), f"element {i}"
+    finally:
+        ctx.close()

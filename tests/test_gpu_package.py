@@ -222,3 +222,37 @@ def test_context_cache_is_bounded(monkeypatch):
     assert len(_runtime.cached_contexts()) <= 2
     free1, _ = _native.device_mem_info(0)
     assert free0 - free1 < 3 * 600 * 2 ** 20, (free0 - free1) / 2 ** 20
+
+
+def test_encrypted_minus_encrypted_on_the_gpu(pe_pd):
+    """`a - b` with both operands encrypted (encrypted_number.py:74-78, self + (other * -1)) runs as
+    one pai_mul by -1 and one pai_add instead of numpy's per-object loop; bit-identical to the per-element
+    operators (the reference's algorithm on the host) and decrypting to the differences. Also a plain received
+    object ndarray on the left (PaillierArray.__rsub__) and a single PaillierEncryptedNumber on the right."""
+    from flex.crypto.paillier import _runtime
+    from flex.crypto.paillier.cipher_array import PaillierArray
+    pe, pd = pe_pd
+    rng = np.random.default_rng(21)
+    xa = (rng.standard_normal((40, 3)) * 100).astype(np.float32)
+    xb = rng.standard_normal((40, 3)).astype(np.float32)
+    a, b = pe.encrypt(xa), pe.encrypt(xb)
+    ctx = _runtime.context(pe.pub_key)
+    c0 = dict(ctx.calls)
+    d = a - b
+    assert type(d) is PaillierArray
+    assert ctx.calls["pai_mul"] - c0.get("pai_mul", 0) == 1 and ctx.calls["pai_add"] - c0.get("pai_add", 0) == 1
+    fa, fb, fd = a.reshape(-1), b.reshape(-1), d.reshape(-1)
+    for i in range(fa.size):
+        want = fa[i] + (fb[i] * -1)                    # host per-element operators (the reference's code path)
+        assert (fd[i].ciphertext(False), fd[i].exponent) == (want.ciphertext(False), want.exponent), i
+    assert np.array_equal(pd.decrypt(d), xa.astype(np.float64) - xb.astype(np.float64))
+    plain = np.asarray(a).view(np.ndarray).copy()      # an unpickled plain object ndarray minus a PaillierArray
+    e = plain - b
+    assert [(u.ciphertext(False), u.exponent) for u in e.reshape(-1)] == \
+        [(u.ciphertext(False), u.exponent) for u in fd]
+    s = fa[5]
+    f = b - s                                          # array - single number
+    for i in (0, 7, fb.size - 1):
+        w1 = fb[i] + (s * -1)
+        assert (f.reshape(-1)[i].ciphertext(False), f.reshape(-1)[i].exponent) == (w1.ciphertext(False), w1.exponent)
+    assert np.array_equal(pd.decrypt(f), xb.astype(np.float64) - np.float64(xa.reshape(-1)[5]))

@@ -403,3 +403,60 @@ def test_packed_view_check_in_c():
     assert b._valid_packed() is not None
     b[2]._PaillierEncryptedNumber__ciphertext = int("8")    # apply_obfuscation replaces the int the same way
     assert b._valid_packed() is None
+
+
+def test_pack_numbers_checks_and_words_in_c():
+    """a received object array's per-element key check (decryptor.py:73-79) and its packing into
+    device words run as one C pass (hostgmp.c pack_numbers); anything the C pass cannot vouch for returns None
+    and the per-element path raises the reference's exception."""
+    from flex.crypto.paillier import _gmp, _runtime
+    from flex.crypto.paillier import cipher_array as ca
+    from flex.crypto.paillier.decryptor import PaillierDecryptor
+    from flex.crypto.paillier.encrypted_number import PaillierEncryptedNumber
+    from flex.crypto.paillier.keypair import PaillierPrivateKey, PaillierPublicKey
+    rng = np.random.default_rng(11)
+    p, q = 1000003, 1000033
+    pk = PaillierPublicKey(p * q)
+    W = (2 * pk.n.bit_length() + 31) // 32
+    n = 20000                                            # several conversion threads
+    w = rng.integers(0, 2 ** 32, size=(n, W), dtype=np.uint32)
+    w[:, -1] &= 0xff
+    w[::13] = 0
+    ints = _runtime.words_to_ints(w)
+    ex = rng.integers(-40, 40, size=n).astype(np.int32)
+    pk_copy = pickle.loads(pickle.dumps(pk))             # an equal key object, as after unpickling
+    objs = np.array(_gmp.make_numbers(PaillierEncryptedNumber, pk_copy, ints, ex, False), dtype=object)
+    got = ca.pack_checked(objs, pk, W)
+    assert got is not None
+    gw, ge, gi = got
+    same = list(map(id, gi)) == list(map(id, ints))
+    assert np.array_equal(gw, w) and np.array_equal(ge, ex) and same
+    del got, gi
+    chk = ca.pack_checked(objs, pk, W, want_words=False)
+    assert chk[0] is None and np.array_equal(chk[1], ex)
+    # the words agree with the Python packing of the same objects
+    pw, pe, _ = ca.pack(ca.PaillierArray(objs[:50]), pk)
+    assert np.array_equal(pw, w[:50]) and np.array_equal(pe, ex[:50])
+    # every failure falls back (None): another key, a non-number, a value too wide, an exponent beyond int32
+    other = PaillierPublicKey(1000037 * 1000039)
+    bad = objs.copy()
+    bad[7] = PaillierEncryptedNumber._make(other, 5, 0, False)
+    assert ca.pack_checked(bad, pk, W) is None
+    bad = objs.copy()
+    bad[3] = 1.5
+    assert ca.pack_checked(bad, pk, W) is None
+    bad = objs.copy()
+    bad[9] = PaillierEncryptedNumber._make(pk, 1 << (32 * W), 0, False)
+    assert ca.pack_checked(bad, pk, W) is None
+    bad = objs.copy()
+    bad[9] = PaillierEncryptedNumber._make(pk, 3, 1 << 40, False)
+    assert ca.pack_checked(bad, pk, W) is None
+    # the decryptor raises the reference's exceptions before anything reaches the device
+    pd = PaillierDecryptor(pk, PaillierPrivateKey(pk, p, q))
+    bad = objs[:10].copy()
+    bad[4] = PaillierEncryptedNumber._make(other, 5, 0, False)
+    with pytest.raises(ValueError, match="different key"):
+        pd.decrypt(bad)
+    bad[4] = "x"
+    with pytest.raises(TypeError, match="should be an PaillierEncryptedNumber"):
+        pd.decrypt(bad)

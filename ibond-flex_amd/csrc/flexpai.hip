@@ -21,6 +21,7 @@
 #include "engine_lane.hpp"
 #include "engine_fb.hpp"
 #include "engine_fbp.hpp"
+#include "engine_fbs.hpp"
 #include "engine_pair.hpp"
 #include "engine_dec4.hpp"
 #include "engine_grp_pair.hpp"
@@ -112,6 +113,8 @@ struct pai_ctx {
   uint32_t *d_fbp_fin_cs = nullptr, *d_fbp_fin_p = nullptr;   // k_fbp_fin: its 12 S constant words, p
   uint32_t fbp_fin_mprime = 0;
   int fb_pair_s = 0;            // limbs of p_h of the resident pair tables; 0 = k_fb tables
+  bool fb_shoup = false;        // the pair tables hold Shoup rows (kernels_fbs.hpp, k_fbs) instead of Montgomery rows
+  FbsConst* d_fbs_cst = nullptr;   // [2] k_fbs_fill's constants (table construction only)
   FbgpHalf* d_fbgp_halves = nullptr;  // 4096-bit keys: pair-group tables (kernels_grp_pair.hpp)
   bool fb_gpair = false;
   SgpHalf* d_sgp_fb = nullptr;  // 4096-bit keys: the split-pair sampler over the same tables (kernels_sgp.hpp)
@@ -702,13 +705,46 @@ static bool fb_gpair_possible(const pai_ctx* c) {
 
 static int fb_row_words(const pai_ctx* c) { return fb_gpair_possible(c) ? 4 * FBGP_ROW4 : fb_row_words(c->crt_sb); }
 
+// 1024/2048-bit keys: the pair tables (kernels_fbp.hpp) need p_h < 2^(32 PW) and R = 2^(28 S) >= 2^12 p_h (bounds of
+// the first product, kernels_fbp.hpp); $FLEXPAI_FB_PAIR=0 selects k_fb. Returns S (19 or 37), or 0.
+static int fb_pair_possible(const pai_ctx* c) {
+  const int sb = c->crt_sb;
+  const int ps = sb == 37 ? 19 : sb == 74 ? 37 : 0;
+  if (!ps) return 0;
+  if (const char* e = getenv("FLEXPAI_FB_PAIR"))
+    if (atoi(e) == 0) return 0;
+  const int pw = ps == 19 ? FbpGeom<19>::PW : FbpGeom<37>::PW;
+  for (const HBig* h : {&c->fb_p, &c->fb_q})
+    if (h->bits() > (size_t)32 * pw || h->bits() + FBP_PB + 1 > (size_t)LB * ps) return 0;
+  return ps;
+}
+
+// Shoup rows (kernels_fbs.hpp) on the pair path: $FLEXPAI_FBS=1 (default 0: k_fbp's Montgomery rows).
+// Their a' = floor(a R / p_h) < R and k_fbs_fill's mu = floor(R^2 / p_h) must fit S + 1 limbs: p_h > 2^(28 (S - 1)).
+static bool fb_shoup_possible(const pai_ctx* c) {
+  const int ps = fb_pair_possible(c);
+  if (!ps) return false;
+  const char* e = getenv("FLEXPAI_FBS");
+  if (!e || atoi(e) == 0) return false;
+  for (const HBig* h : {&c->fb_p, &c->fb_q})
+    if (h->bits() <= (size_t)LB * (ps - 1)) return false;
+  return true;
+}
+
+// 32-bit words of one resident table row (fb_row_words is the ciphertext half's word count for the Garner
+// kernels; the Shoup rows are longer: a, a', b R)
+static int fb_table_row_words(const pai_ctx* c) {
+  if (fb_shoup_possible(c)) return fbs_row_bytes(fb_pair_possible(c)) / 4;
+  return fb_row_words(c);
+}
+
 static int fb_digit_count(const pai_ctx* c, int W) {
   const size_t kb = std::max(sub(c->fb_p, HBig(1)).bits(), sub(c->fb_q, HBig(1)).bits());
   return (int)((kb + W - 1) / W);
 }
 
 static uint64_t fb_bytes(const pai_ctx* c, int W) {
-  return 2ull * (uint64_t)fb_digit_count(c, W) * (1ull << W) * (uint64_t)fb_row_words(c) * 4ull;
+  return 2ull * (uint64_t)fb_digit_count(c, W) * (1ull << W) * (uint64_t)fb_table_row_words(c) * 4ull;
 }
 
 // Budget for the two tables: $FLEXPAI_FB_MAX_BYTES, else the free device memory less a reserve of
@@ -758,6 +794,8 @@ static void fb_release(pai_ctx* c) {
   c->d_fbp_halves = nullptr;
   c->d_fbp_fin_cs = c->d_fbp_fin_p = nullptr;
   c->fb_pair_s = 0;
+  c->fb_shoup = false;
+  c->d_fbs_cst = nullptr;
   c->d_fbgp_halves = nullptr;
   c->fb_gpair = false;
   c->d_sgp_fb = nullptr;
@@ -853,20 +891,18 @@ static int ensure_fb(pai_ctx* c) {
   // both Garner kernels take w_q < q^2 as an operand mod p^2 (k_fb_fin: w_p + 8 p^2 - w_q > 0; k_fbp_fin:
   // A_q, B_q < 2p): keys with q >= 2p encrypt on the generic CRT path
   if (cmp(primes[1], shl1(primes[0])) >= 0) return fb_unavailable(c, "q >= 2p: fixed-base Garner bounds");
-  // pair products (kernels_fbp.hpp) over the S limbs of p_h: needs p_h < 2^(32 PW) and R = 2^(28 S) >=
-  // 2^12 p_h (bounds of the first product, kernels_fbp.hpp); $FLEXPAI_FB_PAIR=0 selects k_fb
-  const int ps = sb == 37 ? 19 : sb == 74 ? 37 : 0;
-  const int pw = sb == 37 ? FbpGeom<19>::PW : FbpGeom<37>::PW;
-  bool pair_ok = ps && !grp;
-  if (const char* e = getenv("FLEXPAI_FB_PAIR")) pair_ok = pair_ok && atoi(e) != 0;
-  for (int h = 0; h < 2 && pair_ok; ++h)
-    pair_ok = primes[h].bits() <= (size_t)32 * pw && primes[h].bits() + FBP_PB + 1 <= (size_t)LB * ps;
+  // pair products (kernels_fbp.hpp) over the S limbs of p_h (fb_pair_possible), on Shoup rows when
+  // fb_shoup_possible (kernels_fbs.hpp)
+  const int ps = grp ? 0 : fb_pair_possible(c);
+  const bool pair_ok = ps != 0;
+  const bool shoup = pair_ok && fb_shoup_possible(c);
   // 4096-bit keys: pair products on lane groups of 4 x 19 limbs (kernels_grp_pair.hpp), R = 2^(28 76) >= 2^24 p_h
   const bool gpair_ok = grp && fb_gpair_possible(c);
   const int lohi_limbs = pair_ok ? std::max(sb, 2 * ps) : gpair_ok ? std::max(sb, 2 * FBGP_S) : sb;
   FbgpHalf gv[2];
   SgpHalf sv[2];
   FbpHalf pv[2];
+  std::vector<uint32_t> fcst_host[2];   // Shoup rows: mu = floor(R^2 / p_h) (S + 2 limbs), R^2 mod p_h (S limbs)
   FbHalf hv[2];
   FbRed red[2];
   std::memset(red, 0, sizeof(red));
@@ -910,7 +946,7 @@ static int ensure_fb(pai_ctx* c) {
     if (hipMalloc(&lohi[h], (size_t)K * 2 * FB_LO * lohi_limbs * 4) != hipSuccess) return fb_unavailable(c, "table allocation failed");
     c->fb_mem.push_back(lohi[h]);
     dlohi = (uint32_t*)lohi[h];
-    if (hipMalloc(&t[h], ((size_t)K << W) * (TW / 4) * sizeof(uint4)) != hipSuccess)
+    if (hipMalloc(&t[h], ((size_t)K << W) * (fb_table_row_words(c) / 4) * sizeof(uint4)) != hipSuccess)
       return fb_unavailable(c, "table allocation failed");
     c->fb_mem.push_back(t[h]);
     hv[h] = FbHalf{(const uint4*)t[h], dm, dR2, done, dbases, dlohi, dnm, dpbig, mont_prime(m2, LB)};
@@ -958,6 +994,14 @@ static int ensure_fb(pai_ctx* c) {
       pcval[h] = (uint32_t*)vcv;
       pv[h] = FbpHalf{(const uint4*)t[h], pp, pone, pbases, dlohi, pnm, ppbig, mont_prime(P, LB),
                       (uint32_t*)vinv, (uint32_t*)vpre, (uint32_t*)vcv};
+      if (shoup) {
+        const HBig R2 = pow2(2 * RS);
+        const HBig mu = div_big(R2, P);
+        if (mu.bits() > (size_t)LB * (ps + 1)) return fb_unavailable(c, "Shoup rows: mu exceeds S + 1 limbs");
+        fcst_host[h] = mu.limbs(ps + 2, LB);
+        const std::vector<uint32_t> r2 = mod(R2, P).limbs(ps, LB);
+        fcst_host[h].insert(fcst_host[h].end(), r2.begin(), r2.end());
+      }
     }
     if (gpair_ok) {
       // pair-group constants: S = 76 limbs of p_h, R = 2^(28 S); pairs as [A: S][B: S]
@@ -1038,6 +1082,16 @@ static int ensure_fb(pai_ctx* c) {
   if (pair_ok) {
     std::vector<FbpHalf> pvv(pv, pv + 2);
     if ((rc = upload_fb(c, pvv, &c->d_fbp_halves))) return fb_unavailable(c, pai_last_error());
+    if (shoup) {
+      FbsConst fc[2];
+      for (int h = 0; h < 2; ++h) {
+        uint32_t* d;
+        if ((rc = upload_fb(c, fcst_host[h], &d))) return fb_unavailable(c, pai_last_error());
+        fc[h] = FbsConst{d, d + ps + 2};
+      }
+      std::vector<FbsConst> fcv(fc, fc + 2);
+      if ((rc = upload_fb(c, fcv, &c->d_fbs_cst))) return fb_unavailable(c, pai_last_error());
+    }
     // k_fbp_fin (kernels_fbp.hpp): (q R)^, (q^-2 R)^ as pairs over p, then q, q^2, p q^2, 4p, 3p
     const HBig &P = primes[0], &Q = primes[1];
     const size_t RS = (size_t)LB * ps;
@@ -1080,6 +1134,7 @@ static int ensure_fb(pai_ctx* c) {
   }
   const hipError_t be = gpair_ok  ? fbgp_build_phase2(c->d_fbgp_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
                         : grp     ? grp_build_tables(c->d_fb_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
+                        : shoup   ? fbs_build_phase2(ps, c->d_fbp_halves, c->d_fbs_cst, (uint4*)t[0], (uint4*)t[1], K, W, nullptr)
                         : pair_ok ? fbp_build_phase2(ps, c->d_fbp_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr)
                                   : fb_build_tables(sb, c->d_fb_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
   if (be != hipSuccess || hipDeviceSynchronize() != hipSuccess)
@@ -1095,6 +1150,7 @@ static int ensure_fb(pai_ctx* c) {
   c->fb_table_bytes = fb_bytes(c, W);
   c->fb_K = K;
   c->fb_pair_s = pair_ok ? ps : 0;
+  c->fb_shoup = shoup;
   c->fb_gpair = gpair_ok;
   c->fb_W_used = W;
   c->fb_raw_bits = raw_bits;
@@ -1456,7 +1512,8 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
       return 0;
     case PAI_OPT_SPLIT_SAMPLER:
       *value = (c->fb_state == pai_ctx::FB_READY && c->d_sgp_fb ? 1 : 0) |
-               (c->pfb_state == pai_ctx::FB_READY && c->d_sgp_pfb ? 2 : 0);
+               (c->pfb_state == pai_ctx::FB_READY && c->d_sgp_pfb ? 2 : 0) |
+               (c->fb_state == pai_ctx::FB_READY && c->fb_shoup ? 4 : 0);
       return 0;
     case PAI_OPT_PAIR:
       *value = ((c->dec_pair_ok || c->dec4_ok) && c->dec_lane_enabled ? 1 : 0) | (c->crt_pair_ok ? 2 : 0) |
@@ -1519,7 +1576,7 @@ static long long fb_threshold(pai_ctx* c) {
   if (!c->fb_W) c->fb_W = fb_default_window();
   const uint64_t budget = fb_budget(c);
   for (int w : {24, 23, 22, 21, 20, 16, 12, 8})
-    if (w <= c->fb_W && fb_bytes(c, w) <= budget) return fb_break_even(c, w, fb_digit_count(c, w), 4 * TW);
+    if (w <= c->fb_W && fb_bytes(c, w) <= budget) return fb_break_even(c, w, fb_digit_count(c, w), 4 * fb_table_row_words(c));
   return 0;
 }
 
@@ -1602,9 +1659,10 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     else grp_occupancy(&occF);
   }
   else if (fb_occupancy(SB, &occF, &occG)) return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
-  if (c->fb_pair_s && fbp_occupancy(c->fb_pair_s, &occF)) return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
-  // elements per block: one per lane, or one per lane group (grp)
-  const int EPB = grp ? BLOCK / GRP_TPI : LANE_BLOCK;
+  if (c->fb_pair_s && (c->fb_shoup ? fbs_occupancy(c->fb_pair_s, &occF) : fbp_occupancy(c->fb_pair_s, &occF)))
+    return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
+  // elements per block: one per lane, one per lane pair (k_fbs), or one per lane group (grp)
+  const int EPB = grp ? BLOCK / GRP_TPI : c->fb_shoup ? LANE_BLOCK / 2 : LANE_BLOCK;
   const long long lane_blocks = (chunk + EPB - 1) / EPB;
   const int gxF = (int)std::max<long long>(1, std::min<long long>(lane_blocks, (long long)occF * c->cus / 2));
   const int gxG = (int)std::max<long long>(1, std::min<long long>(lane_blocks, (long long)occG * c->cus));
@@ -1645,7 +1703,7 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     const int gF = (int)std::min<long long>(gxF, (n + EPB - 1) / EPB);
     if (c->fb_pair_s) {
       const FbpParams pp{c->d_fbp_halves, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
-      HIPCHK(fbp_launch(c->fb_pair_s, pp, gF, st));
+      HIPCHK(c->fb_shoup ? fbs_launch(c->fb_pair_s, pp, gF, st) : fbp_launch(c->fb_pair_s, pp, gF, st));
     } else if (grp && c->fb_gpair) {
       const FbgpParams pg{c->d_fbgp_halves, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
       if (c->d_sgp_fb) {   // split pairs (kernels_sgp.hpp): SGP_PAIRS elements per block, grid (gx, 2)

@@ -1,0 +1,602 @@
+// Fixed-base obfuscation with Shoup-form rows (round 4): the sampler of kernels_fbp.hpp with each product by a
+// table row done as Shoup's fixed-multiplier product instead of a Montgomery pass. Same distribution, same
+// canonical pairs out, so k_fbp_fin recombines them unchanged and the ciphertexts are bit-identical to k_fbp's.
+//
+// Rows. A table entry T = T_k[d] mod p_h^2 (PLAIN, not Montgomery form) is stored factored as T = a (1 + p_h b),
+// a = T mod p_h, together with Shoup's quotient a' = floor(a R / p_h), R = 2^(28 S) (PWA words): the words of a
+// (PW), of a' (PWA, padded to quads), then of b R mod p_h (PW) -- 400 B per row at nb = 2048 (25 quads). The a
+// and a' quads stream into LDS by DMA one digit ahead, the b R quads into registers (summed into bs at once).
+//
+// Product of the running pair (A, B), V = A + p B (mod p^2), by a (tools/shoup_model.py checks every bound):
+//   V a = A a + p B a = r_A + p (Q_A + B a),   A a = r_A + Q_A p
+// and for each component X in {A, B} two steps:
+//   step 1: Q = floor(X a' / R) from the columns >= S - 1 of X a' only: S (S + 1) / 2 MACs, Q at most S + 1
+//           below the exact floor (the dropped columns are worth < S R);
+//   step 2: X' = init + X a - Q p from the columns 0 .. S - 1 (signed 64-bit accumulators: + X_i a_j and
+//           + (-Q_i) p_j), exact because the true value lies in [0, R): S (S + 1) MACs.
+// Shoup's bound A a / p - A a' / R in [0, A / R) keeps A < (S + 3) p and B < 2 (S + 3) p, far below R.
+// 3 S^2 + 3 S MACs per product against 4 S^2 for the Montgomery pass pair (and no q_j multiplications).
+// After the K products the b sum is applied once (fbp_apply_bsum), then the pair is reduced to canonical.
+#pragma once
+#include "kernels_fbp.hpp"
+
+namespace fpai {
+
+template <int S>
+struct FbsGeom;
+template <>
+struct FbsGeom<19> {   // 1024-bit keys: p_h < 2^512, R = 2^532
+  static constexpr int PW = 16, PWA = 17, QA = 4, QAP = 5, QB = 4;
+};
+template <>
+struct FbsGeom<37> {   // 2048-bit keys: p_h < 2^1024, R = 2^1036
+  static constexpr int PW = 32, PWA = 33, QA = 8, QAP = 9, QB = 8;
+};
+// row quads: a [0, QA), a' [QA, QA + QAP), b R [QA + QAP, QA + QAP + QB)
+template <int S>
+constexpr int fbs_row_quads() { return FbsGeom<S>::QA + FbsGeom<S>::QAP + FbsGeom<S>::QB; }
+template <int S>
+constexpr int fbs_lds_quads() { return FbsGeom<S>::QA + FbsGeom<S>::QAP; }
+
+template <int C>
+__device__ __forceinline__ uint32_t fb_quad_word(const uint4& v) {
+  if constexpr (C == 0) return v.x;
+  else if constexpr (C == 1) return v.y;
+  else if constexpr (C == 2) return v.z;
+  else return v.w;
+}
+template <int OFF>
+__device__ __forceinline__ void lds_quad_wr(uint32_t addr, const fbp_u32x4& v) {
+  if constexpr (OFF < 65536) asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "v"(v), "i"(OFF) : "memory");
+  else asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr + 65536u), "v"(v), "i"(OFF - 65536) : "memory");
+}
+
+// Digits J of a number held as NQ quads at quad Q0 of this lane's LDS row ([quad][lane] layout), consumed in
+// the order J = S-1 .. 0 (DESC) or 0 .. S-1. Quads are read DQ quads ahead of the first digit that needs them,
+// in consumption order, and every wait names the exact count of reads issued after the ones it needs (the only
+// LDS operations in flight in a step are these reads).
+template <int S, int NQ, int Q0, bool DESC, int DQ>
+struct FbsReader {
+  uint32_t addr;
+  fbp_u32x4 q[NQ];
+  static constexpr int dig(int t) { return DESC ? S - 1 - t : t; }
+  static constexpr int wlo(int J) { return (28 * J) >> 5; }
+  static constexpr int whi(int J) { return (28 * J + 27) >> 5 < 4 * NQ - 1 ? (28 * J + 27) >> 5 : 4 * NQ - 1; }
+  static constexpr int rank(int qd) { return DESC ? NQ - 1 - qd : qd; }   // issue position of quad qd
+  static constexpr int quad_at(int r) { return DESC ? NQ - 1 - r : r; }
+  static constexpr int cmax(int a, int b) { return a > b ? a : b; }
+  static constexpr int need(int t) {   // highest issue position needed by the digits of steps 0 .. t
+    int m = -1;
+    for (int u = 0; u <= t; ++u) m = cmax(m, cmax(rank(wlo(dig(u)) / 4), rank(whi(dig(u)) / 4)));
+    return m;
+  }
+  static constexpr int issued(int t) { return t < 0 ? -1 : (need(t) + DQ < NQ - 1 ? need(t) + DQ : NQ - 1); }
+  template <int R0, int... Rs>
+  __device__ __forceinline__ void issue(std::integer_sequence<int, Rs...>) {
+    ((q[quad_at(R0 + Rs)] = lds_quad_rd<(Q0 + quad_at(R0 + Rs)) * LANE_BLOCK * 16>(addr)), ...);
+  }
+  template <int T>
+  __device__ __forceinline__ uint32_t operator()(std::integral_constant<int, T>) {
+    constexpr int from = issued(T - 1) + 1, to = issued(T);
+    issue<from>(std::make_integer_sequence<int, (to >= from ? to - from + 1 : 0)>{});
+    constexpr int J = dig(T), l = wlo(J), h = whi(J), gl = l / 4, gh = h / 4;
+    if constexpr (T == 0 || need(T) > need(T - 1)) {
+      constexpr int pending = to - need(T);
+      static_assert(pending >= 0 && pending <= 15, "lgkmcnt range");
+      if constexpr (gl == gh) asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(q[gl]) : "i"(pending));
+      else asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(q[gl]), "+v"(q[gh]) : "i"(pending));
+    }
+    constexpr int sh = (28 * J) & 31;
+    const uint32_t wl = quad_word<l % 4>(q[gl]);
+    if constexpr (sh + 28 <= 32) return (wl >> sh) & lane::LMASK;
+    else if constexpr (l + 1 < 4 * NQ) return __builtin_amdgcn_alignbit(quad_word<(l + 1) % 4>(q[(l + 1) / 4]), wl, sh) & lane::LMASK;
+    else return wl >> sh;   // past the stored words: zero bits
+  }
+};
+
+// step 1, digit J of a' (columns >= S - 1): P[k - (S - 1)] for k = i + J >= S - 1
+template <int S, int T, class Rd>
+__device__ __forceinline__ void fbs_q_digit(uint64_t (&P)[S + 1], const uint32_t (&X)[S], Rd& rd) {
+  constexpr int J = S - 1 - T;
+  const uint32_t d = rd(std::integral_constant<int, T>{});
+#pragma unroll
+  for (int i = S - 1 - J; i < S; ++i) P[i + J - (S - 1)] += (uint64_t)X[i] * d;
+#pragma unroll
+  for (int i = 0; i <= S; ++i) asm volatile("" : "+v"(P[i]));
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int S, class Rd, int... Ts>
+__device__ __forceinline__ void fbs_q_all(uint64_t (&P)[S + 1], const uint32_t (&X)[S], Rd& rd, std::integer_sequence<int, Ts...>) {
+  (fbs_q_digit<S, Ts>(P, X, rd), ...);
+}
+// -Q: the negated limbs of floor(X a' / R) (truncated, above); rd yields the digits of a', J = S-1 .. 0
+template <int S, class Rd>
+__device__ __forceinline__ void fbs_quotient(const uint32_t (&X)[S], Rd& rd, int32_t (&nq)[S]) {
+  uint64_t P[S + 1];
+#pragma unroll
+  for (int i = 0; i <= S; ++i) P[i] = 0;
+  fbs_q_all<S>(P, X, rd, std::make_integer_sequence<int, S>{});
+  uint64_t c = P[0] >> lane::LB;
+#pragma unroll
+  for (int i = 1; i <= S; ++i) {
+    const uint64_t v = P[i] + c;
+    nq[i - 1] = -(int32_t)lane::limb32(v);
+    c = v >> lane::LB;
+  }
+}
+
+// Digits J = 0 .. S-1 of a, read from the row in global memory (a is not in LDS), NQ quads, two quads ahead of the
+// digit that first needs them. The loads are inline asm, so that they stay where they are issued (left to the
+// compiler, all NQ quads were hoisted to the start and kept live, 32 VGPRs), with exact vmcnt waits: in a step 2
+// the only vector-memory operations in flight are these loads and, from digit XD on, the XN operations the caller's
+// hook issues there (the next row's). Quads 0 and 1 are loaded by the caller (EXT: already waited for) or by
+// start() (issue order = quad order either way).
+template <int OFF>
+__device__ __forceinline__ fbp_u32x4 fbs_gload(const uint4* base) {
+  fbp_u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(v) : "v"(base), "i"(OFF) : "memory");
+  return v;
+}
+struct FbsNoHook {
+  template <int J>
+  __device__ __forceinline__ void operator()(std::integral_constant<int, J>) {}
+};
+template <int S, int NQ, int Q0, bool DESC, bool EXT, int XN, class Hook>
+struct FbsGlobalReader {
+  const uint4* row;
+  Hook hook;
+  fbp_u32x4 q[NQ];
+  static constexpr int dig(int t) { return DESC ? S - 1 - t : t; }
+  static constexpr int wlo(int J) { return (28 * J) >> 5; }
+  static constexpr int whi(int J) { return (28 * J + 27) >> 5 < 4 * NQ - 1 ? (28 * J + 27) >> 5 : 4 * NQ - 1; }
+  static constexpr int rank(int qd) { return DESC ? NQ - 1 - qd : qd; }   // issue position of quad qd
+  static constexpr int quad_at(int r) { return DESC ? NQ - 1 - r : r; }
+  static constexpr int cmax(int a, int b) { return a > b ? a : b; }
+  static constexpr int need(int t) {   // highest issue position needed by steps 0 .. t
+    int m = -1;
+    for (int u = 0; u <= t; ++u) m = cmax(m, cmax(rank(wlo(dig(u)) / 4), rank(whi(dig(u)) / 4)));
+    return m;
+  }
+  static constexpr int top(int t) { return need(t) + 2 < NQ - 1 ? need(t) + 2 : NQ - 1; }   // positions issued by step t
+  static constexpr int xd() {   // the step that issues the last quad: the hook runs there
+    int t = 0;
+    while (top(t) < NQ - 1) ++t;
+    return t;
+  }
+  // positions 0 and 1 (EXT: loaded and waited for by the caller)
+  __device__ __forceinline__ void start() {
+    q[quad_at(0)] = fbs_gload<(Q0 + quad_at(0)) * 16>(row);
+    q[quad_at(1)] = fbs_gload<(Q0 + quad_at(1)) * 16>(row);
+  }
+  template <int R0, int... Rs>
+  __device__ __forceinline__ void issue(std::integer_sequence<int, Rs...>) {
+    ((q[quad_at(R0 + Rs)] = fbs_gload<(Q0 + quad_at(R0 + Rs)) * 16>(row)), ...);
+  }
+  template <int T>
+  __device__ __forceinline__ uint32_t operator()(std::integral_constant<int, T>) {
+    constexpr int from = T == 0 ? 2 : top(T - 1) + 1, to = top(T);
+    issue<from>(std::make_integer_sequence<int, (to >= from ? to - from + 1 : 0)>{});
+    if constexpr (T == xd()) hook(std::integral_constant<int, T>{});
+    constexpr int J = dig(T), l = wlo(J), gl = l / 4, gh = whi(J) / 4;
+    constexpr bool fresh = T == 0 || need(T) > need(T - 1);
+    if constexpr (fresh && (!EXT || need(T) >= 2)) {
+      constexpr int pending = to - need(T) + (T >= xd() ? XN : 0);
+      static_assert(pending >= 0 && pending <= 63, "vmcnt range");
+      if constexpr (gl == gh) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(q[gh]) : "i"(pending));
+      else asm volatile("s_waitcnt vmcnt(%2)" : "+v"(q[gl]), "+v"(q[gh]) : "i"(pending));
+    }
+    constexpr int sh = (28 * J) & 31;
+    const uint32_t wl = quad_word<l % 4>(q[gl]);
+    if constexpr (sh + 28 <= 32) return (wl >> sh) & lane::LMASK;
+    else if constexpr (l + 1 < 4 * NQ) return __builtin_amdgcn_alignbit(quad_word<(l + 1) % 4>(q[(l + 1) / 4]), wl, sh) & lane::LMASK;
+    else return wl >> sh;
+  }
+};
+template <int S>
+using FbsAReader = FbsGlobalReader<S, FbsGeom<S>::QAP, FbsGeom<S>::QA, true, true, 0, FbsNoHook>;     // A1: a' (8, 7 given)
+template <int S>
+using FbsBReader = FbsGlobalReader<S, FbsGeom<S>::QAP, FbsGeom<S>::QA, true, false, 0, FbsNoHook>;    // B1: a'
+template <int S>
+using FbsA2Reader = FbsGlobalReader<S, FbsGeom<S>::QA, 0, false, true, 0, FbsNoHook>;                  // A2: a (0, 1 given)
+
+// step 2, digit J of a: P[i + J] += X_i a_J - Q_i p_J for i + J < S
+template <int S, int J, class Rd>
+__device__ __forceinline__ void fbs_r_digit(int64_t (&P)[S], const uint32_t (&X)[S], const int32_t (&nq)[S],
+                                            const uint32_t (&m)[S], Rd& rd) {
+  const uint32_t d = rd(std::integral_constant<int, J>{});
+  const int32_t mj = (int32_t)m[J];
+#pragma unroll
+  for (int i = 0; i + J < S; ++i) {
+    P[i + J] = (int64_t)((uint64_t)P[i + J] + (uint64_t)X[i] * d);
+    P[i + J] += (int64_t)nq[i] * mj;
+  }
+#pragma unroll
+  for (int i = J; i < S; ++i) asm volatile("" : "+v"(P[i]));
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int S, class Rd, int... Js>
+__device__ __forceinline__ void fbs_r_all(int64_t (&P)[S], const uint32_t (&X)[S], const int32_t (&nq)[S], const uint32_t (&m)[S],
+                                          Rd& rd, std::integer_sequence<int, Js...>) {
+  (fbs_r_digit<S, Js>(P, X, nq, m, rd), ...);
+}
+// X <- init + X a - Q p (exact, in [0, R)); INIT: the magnitudes of the negated limbs in ni are added first (a
+// compile-time choice: a pointer here made the array a stack object in scratch memory)
+template <int S, bool INIT, class Rd>
+__device__ __forceinline__ void fbs_remainder(uint32_t (&X)[S], const int32_t (&nq)[S], const uint32_t (&m)[S], Rd& rd,
+                                              const int32_t (&ni)[S]) {
+  int64_t P[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) P[i] = INIT ? (int64_t)(-ni[i]) : 0;
+  fbs_r_all<S>(P, X, nq, m, rd, std::make_integer_sequence<int, S>{});
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const int64_t v = P[i] + c;
+    X[i] = lane::limb32((uint64_t)v);
+    c = v >> lane::LB;   // arithmetic: the low part of a signed sum
+  }
+}
+
+// x <- x - 2^e m while x >= 2^e m, e = E .. 0 (x < 2^(E+1) m on entry -> x < m), counting the multiples into t;
+// 2^e m is formed from m in the loop (one shift per limb), not held
+template <int S, int E>
+__device__ __forceinline__ void fbs_reduce(uint32_t (&x)[S], const uint32_t (&m)[S], uint32_t& t) {
+#pragma unroll 1
+  for (int e = E; e >= 0; --e) {
+    int32_t c = 0;
+    uint32_t d[S];
+    uint32_t sc = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      const uint64_t me = ((uint64_t)m[i] << e) + sc;
+      sc = (uint32_t)(me >> lane::LB);
+      const int32_t v = (int32_t)x[i] - (int32_t)((uint32_t)me & lane::LMASK) + c;
+      d[i] = (uint32_t)v & lane::LMASK;
+      c = v >> lane::LB;
+    }
+    const bool lt = c != 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) x[i] = lt ? x[i] : d[i];
+    t += lt ? 0u : (1u << e);
+  }
+}
+
+// ---------------------------------------------------------------- the sampler on split pairs
+// Element-half e on lanes 2e, 2e+1 (kernels_sgp.hpp's layout): the even lane keeps A, the odd lane B, and both run
+// the same Shoup pass on their own component at once -- step 1 (their quotient), then step 2, the odd lane's
+// accumulator starting at the even lane's Q_A (one DPP per limb). Per lane: the component, -Q and one accumulator
+// row (148 VGPRs in step 2) and half of the b sum (16 words + a carry).
+//
+// Rows in LDS, double-buffered (product k reads buffer k & 1 while row k+1 streams into the other): DMA instruction
+// g of a wave fetches quad 2g + t of pair p's row on lane 2p + t, landing at [g][lane] (1 KB per instruction), so
+// quad Q of the pair's row sits at (Q / 2) KB + (Q & 1) 16 B from the pair's base: both lanes of a pair read the same
+// addresses (a broadcast), consecutive pairs consecutive 32 B. The b R quads go to registers (4 per lane).
+template <int S>
+constexpr int fbs_dma_insts() { return (FbsGeom<S>::QA + FbsGeom<S>::QAP + 1) / 2; }   // 9 at S = 37
+template <int S>
+constexpr int fbs_wave_buf_bytes() { return fbs_dma_insts<S>() * 1024; }
+template <int Q>
+constexpr int fbs_pair_off() { return (Q >> 1) * 1024 + (Q & 1) * 16; }
+
+// digits of a' (quads QA .. QA+QAP-1 of the row, consumed J = S-1 .. 0) or of a (quads 0 .. QA-1, J = 0 .. S-1) from
+// the pair's row in LDS; reads DQ quads ahead in consumption order, exact lgkmcnt waits (only these reads in flight)
+template <int S, int NQ, int Q0, bool DESC, int DQ>
+struct FbsPairReader {
+  uint32_t addr;
+  fbp_u32x4 q[NQ];
+  static constexpr int dig(int t) { return DESC ? S - 1 - t : t; }
+  static constexpr int wlo(int J) { return (28 * J) >> 5; }
+  static constexpr int whi(int J) { return (28 * J + 27) >> 5 < 4 * NQ - 1 ? (28 * J + 27) >> 5 : 4 * NQ - 1; }
+  static constexpr int rank(int qd) { return DESC ? NQ - 1 - qd : qd; }
+  static constexpr int quad_at(int r) { return DESC ? NQ - 1 - r : r; }
+  static constexpr int cmax(int a, int b) { return a > b ? a : b; }
+  static constexpr int need(int t) {
+    int m = -1;
+    for (int u = 0; u <= t; ++u) m = cmax(m, cmax(rank(wlo(dig(u)) / 4), rank(whi(dig(u)) / 4)));
+    return m;
+  }
+  static constexpr int issued(int t) { return t < 0 ? -1 : (need(t) + DQ < NQ - 1 ? need(t) + DQ : NQ - 1); }
+  template <int R0, int... Rs>
+  __device__ __forceinline__ void issue(std::integer_sequence<int, Rs...>) {
+    ((q[quad_at(R0 + Rs)] = lds_quad_rd<fbs_pair_off<Q0 + quad_at(R0 + Rs)>()>(addr)), ...);
+  }
+  template <int T>
+  __device__ __forceinline__ uint32_t operator()(std::integral_constant<int, T>) {
+    constexpr int from = issued(T - 1) + 1, to = issued(T);
+    issue<from>(std::make_integer_sequence<int, (to >= from ? to - from + 1 : 0)>{});
+    constexpr int J = dig(T), l = wlo(J), h = whi(J), gl = l / 4, gh = h / 4;
+    if constexpr (T == 0 || need(T) > need(T - 1)) {
+      constexpr int pending = to - need(T);
+      static_assert(pending >= 0 && pending <= 15, "lgkmcnt range");
+      if constexpr (gl == gh) asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(q[gl]) : "i"(pending));
+      else asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(q[gl]), "+v"(q[gh]) : "i"(pending));
+    }
+    constexpr int sh = (28 * J) & 31;
+    const uint32_t wl = quad_word<l % 4>(q[gl]);
+    if constexpr (sh + 28 <= 32) return (wl >> sh) & lane::LMASK;
+    else if constexpr (l + 1 < 4 * NQ) return __builtin_amdgcn_alignbit(quad_word<(l + 1) % 4>(q[(l + 1) / 4]), wl, sh) & lane::LMASK;
+    else return wl >> sh;
+  }
+};
+
+// row `row` (this pair's) -> the wave's LDS buffer at lb (wave-uniform): quads 2g + t on lane 2p + t; and this lane's
+// half of the b R quads (QB / 2: lane t takes words t PW / 2 .. (t + 1) PW / 2 - 1) into bv
+template <int S>
+__device__ __forceinline__ void fbs_row_fetch(const uint4* row, uint32_t lb, int tig, fbp_u32x4 (&bv)[FbsGeom<S>::QB / 2]) {
+  using G = FbsGeom<S>;
+  const uint4* src = row + tig;
+#pragma unroll
+  for (int g = 0; g < fbs_dma_insts<S>(); ++g) {
+    uint32_t dst = lb + (uint32_t)(g * 1024);
+    asm volatile("" : "+s"(dst));
+    __builtin_amdgcn_global_load_lds((const void*)(src + 2 * g), (__attribute__((address_space(3))) void*)(size_t)dst, 16, 0, 0);
+  }
+  constexpr int QH = G::QB / 2;
+  const fbp_u32x4* b = reinterpret_cast<const fbp_u32x4*>(row + G::QA + G::QAP + QH * tig);
+#pragma unroll
+  for (int q = 0; q < QH; ++q) bv[q] = b[q];
+}
+
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbs(FbpParams p) {
+  using G = FbsGeom<S>;
+  constexpr int PW = G::PW, TQ = fbs_row_quads<S>(), WB = fbs_wave_buf_bytes<S>();
+  static_assert(PW == 32 || PW == 16, "b sum halves");
+  constexpr int HW = PW / 2;   // b sum words per lane
+  __shared__ __attribute__((aligned(16))) uint8_t lbuf[(LANE_BLOCK / 64) * 2 * WB];
+  const int half = blockIdx.y;
+  const FbpHalf* H = p.halves + half;
+  uint32_t m[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) m[j] = H->p[j];
+  const uint32_t mprime = H->mprime;
+  const uint4* table = H->table;
+  const int K = p.K, W = p.W;
+  const int lane = threadIdx.x & 63;
+  const int tig = threadIdx.x & 1;
+  const bool odd = tig != 0;
+  const int pib = threadIdx.x >> 1;
+  typedef __attribute__((address_space(3))) uint8_t lds_u8;
+  const uint32_t wbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds_u8*)(lbuf + (threadIdx.x >> 6) * 2 * WB));
+  const uint32_t pbase = wbase + (uint32_t)((lane >> 1) * 32);   // this pair's quad 0 in buffer 0
+  constexpr int PAIRS = LANE_BLOCK / 2;
+  for (long long base = (long long)blockIdx.x * PAIRS; base < p.n; base += (long long)gridDim.x * PAIRS) {
+    const long long e = base + pib;
+    const bool valid = e < p.n;
+    const long long ee = valid ? e : p.n - 1;
+    int64_t M = 0;
+    int ex = 0, stt;
+    const bool fixed = p.exp_mode != 0;
+    if (p.dtype == 0) stt = encode_float((double)((const float*)p.x)[ee], fixed, p.fexp, M, ex);
+    else if (p.dtype == 1) stt = encode_float(((const double*)p.x)[ee], fixed, p.fexp, M, ex);
+    else stt = encode_int(((const int64_t*)p.x)[ee], fixed, p.fexp, M, ex);
+    if (half == 0 && valid && !odd) {
+      p.exp[e] = ex;
+      if (p.status) p.status[e] = stt;
+    }
+    uint32_t X[S];   // even lane: A; odd lane: B (the start c0 = (1, gamma))
+    {
+      uint32_t A0[S], B0[S];
+      fbp_c0<S>(M, H, A0, B0);
+#pragma unroll
+      for (int j = 0; j < S; ++j) X[j] = odd ? B0[j] : A0[j];
+    }
+    const uint32_t* dg = p.digits + (size_t)half * K * p.n + ee;
+    uint32_t bsw[HW], bcc = 0;
+#pragma unroll
+    for (int j = 0; j < HW; ++j) bsw[j] = 0;
+    static_assert(G::QB / 2 == HW / 4, "b R quads per lane");
+    fbp_u32x4 bv[G::QB / 2];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous element's reads of both buffers are done
+    fbs_row_fetch<S>(table + (size_t)dg[0] * TQ, wbase, tig, bv);
+    uint32_t dn = K > 1 ? dg[(size_t)p.n] : 0u;
+    for (int k = 0; k < K; ++k) {
+      lds_dma_wait();                                     // row k in buffer k & 1, its b R in bv, digit k+1 in dn
+      {                                                   // this lane's half of the b sum
+        unsigned int c = 0;
+#pragma unroll
+        for (int q = 0; q < HW / 4; ++q) {
+          bsw[4 * q] = __builtin_addc(bsw[4 * q], bv[q].x, c, &c);
+          bsw[4 * q + 1] = __builtin_addc(bsw[4 * q + 1], bv[q].y, c, &c);
+          bsw[4 * q + 2] = __builtin_addc(bsw[4 * q + 2], bv[q].z, c, &c);
+          bsw[4 * q + 3] = __builtin_addc(bsw[4 * q + 3], bv[q].w, c, &c);
+        }
+        bcc += c;
+      }
+      const uint32_t cur = pbase + (uint32_t)((k & 1) * WB);
+      if (k + 1 < K) {                                    // row k+1 -> the other buffer (read two products ago: done)
+        fbs_row_fetch<S>(table + (((size_t)(k + 1) << W) + dn) * TQ, wbase + (uint32_t)(((k + 1) & 1) * WB), tig, bv);
+        dn = k + 2 < K ? dg[(size_t)(k + 2) * p.n] : 0u;
+      } else {
+#pragma unroll
+        for (int q = 0; q < G::QB / 2; ++q) bv[q] = fbp_u32x4{0u, 0u, 0u, 0u};
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      int32_t nq[S];
+      {
+        FbsPairReader<S, G::QAP, G::QA, true, 1> r1{cur};
+        fbs_quotient<S>(X, r1, nq);
+      }
+      {   // step 2; the odd lane's accumulator starts at the even lane's Q_A
+        int64_t P[S];
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+          const int32_t qa = __builtin_amdgcn_update_dpp(0, nq[i], 0xA0, 0xF, 0xF, false);   // quad_perm [0,0,2,2]
+          P[i] = odd ? (int64_t)(-qa) : 0;
+        }
+        FbsPairReader<S, G::QA, 0, false, 1> r2{cur};
+        fbs_r_all<S>(P, X, nq, m, r2, std::make_integer_sequence<int, S>{});
+        int64_t c = 0;
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+          const int64_t v = P[i] + c;
+          X[i] = lane::limb32((uint64_t)v);
+          c = v >> lane::LB;
+        }
+      }
+    }
+    // the even lane: A < (S + 3) p to canonical (its multiples of p move into B), B from the odd lane, the b sum
+    // (its high half from the odd lane), B + REDC(A bs R), B to canonical
+    uint32_t B[S], bs[PW], bc;
+#pragma unroll
+    for (int j = 0; j < S; ++j) B[j] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)X[j], 0xF5, 0xF, 0xF, false);   // [1,1,3,3]
+    {
+      uint32_t c = 0;   // bs = lo + 2^(32 HW) (hi + c_lo) + 2^(32 PW) c_hi
+#pragma unroll
+      for (int j = 0; j < HW; ++j) {
+        bs[j] = bsw[j];
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)bsw[j], 0xF5, 0xF, 0xF, false);
+        const uint64_t v = (uint64_t)hi + (j == 0 ? bcc : 0u) + c;
+        bs[HW + j] = (uint32_t)v;
+        c = (uint32_t)(v >> 32);
+      }
+      bc = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)bcc, 0xF5, 0xF, 0xF, false) + c;
+    }
+    if (!odd && valid) {
+      uint32_t t = 0;
+      fbs_reduce<S, 5>(X, m, t);                          // (S + 3) p < 64 p
+      {
+        uint32_t c = t;
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+          const uint32_t v = B[j] + c;
+          B[j] = v & lane::LMASK;
+          c = v >> lane::LB;
+        }
+      }
+      fbp_apply_bsum<S, PW>(X, B, bs, bc, m, mprime);     // B + REDC(A bs R) < 2 (S + 3) p + 64 + 2 p < 128 p
+      uint32_t tb = 0;
+      fbs_reduce<S, 6>(B, m, tb);
+      uint32_t* o = p.out + fbp_pair_index<S>(e, half, p.n);
+#pragma unroll
+      for (int j = 0; j < 2 * S; ++j) o[j * 64] = j < S ? X[j] : B[j - S];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- Shoup-form rows from the pair tables' lo/hi
+// entries and inverses (k_fbp_lohi, k_fbp_inv_fwd/bwd): per entry T R = lo hi R^-1 as a pair, T = (T R)(1, 0) R^-1
+// canonical (A_T, B_T); a = A_T; b = B_T A_T^-1 = REDC(B_T X) with X = REDC(inv_lo inv_hi) = A_T^-1 R (the lo/hi
+// entries and their inverses are R-forms of l_lo, l_hi and their inverses, A_T = l_lo l_hi mod p), b R =
+// REDC(b R^2); a' = floor(a R / p) from floor(a mu / R), mu = floor(R^2 / p), raised by one when a R - a' p >= p.
+struct FbsConst {
+  const uint32_t* mu;      // floor(R^2 / p_h): S + 1 limbs (+ 1 spare)
+  const uint32_t* r2;      // R^2 mod p_h, S limbs
+};
+
+template <int S, int... Gs>
+__device__ __forceinline__ void fbs_store_words(uint4* __restrict__ dst, const uint32_t (&x)[S], std::integer_sequence<int, Gs...>) {
+  ((dst[Gs] = make_uint4(fb_word<S, 4 * Gs>(x), fb_word<S, 4 * Gs + 1>(x), fb_word<S, 4 * Gs + 2>(x), fb_word<S, 4 * Gs + 3>(x))),
+   ...);
+}
+
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK) void k_fbs_fill(const FbpHalf* halves, const FbsConst* cst, int K, int W, uint4* table0,
+                                                         uint4* table1) {
+  using G = FbsGeom<S>;
+  constexpr int TQ = fbs_row_quads<S>();
+  const int ent = 1 << W;
+  const int per = (ent + LANE_BLOCK - 1) / LANE_BLOCK;
+  const int k = blockIdx.x / per;
+  const int d = (blockIdx.x % per) * LANE_BLOCK + threadIdx.x;
+  if (d >= ent) return;
+  const int half = blockIdx.y;
+  const FbpHalf* H = halves + half;
+  const FbsConst* C = cst + half;
+  uint4* table = half ? table1 : table0;
+  const int LO = W / 2;
+  const int dl = d & ((1 << LO) - 1), dh = d >> LO;
+  const uint32_t* lo = H->lohi + (((size_t)k * 2 + 0) * FB_LO + dl) * 2 * S;
+  const uint32_t* hi = H->lohi + (((size_t)k * 2 + 1) * FB_LO + dh) * 2 * S;
+  uint32_t m[S], A[S], B[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    m[i] = H->p[i];
+    A[i] = lo[i];
+    B[i] = lo[S + i];
+  }
+  pair::mont_mul<S>(A, B, [&](auto J) { return make_uint2(hi[decltype(J)::value], hi[S + decltype(J)::value]); }, m, H->mprime);
+  pair::mont_mul<S>(A, B, [&](auto J) { return make_uint2(decltype(J)::value == 0 ? 1u : 0u, 0u); }, m, H->mprime);   // T R -> T
+  pair::canon<S>(A, B, m);
+  uint32_t bR[S];
+  {
+    const uint32_t* il = H->inv + (((size_t)k * 2 + 0) * FB_LO + dl) * S;
+    const uint32_t* ih = H->inv + (((size_t)k * 2 + 1) * FB_LO + dh) * S;
+    uint32_t X[S], Y[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      X[i] = il[i];
+      Y[i] = ih[i];
+      bR[i] = B[i];
+    }
+    lane::mont_mul<S>(X, Y, m, H->mprime);               // A_T^-1 R
+    lane::mont_mul<S>(bR, X, m, H->mprime);              // b = B_T A_T^-1
+#pragma unroll
+    for (int i = 0; i < S; ++i) Y[i] = C->r2[i];
+    lane::mont_mul<S>(bR, Y, m, H->mprime);              // b R
+    lane::cond_sub<S>(bR, m);
+  }
+  // a' = floor(a R / p): the high part of a mu, then one correction
+  uint32_t ap[S + 1];
+  {
+    uint64_t P[2 * S + 2];
+#pragma unroll
+    for (int c = 0; c < 2 * S + 2; ++c) P[c] = 0;
+#pragma unroll
+    for (int j = 0; j < S + 1; ++j) {
+      const uint32_t mj = C->mu[j];
+#pragma unroll
+      for (int i = 0; i < S; ++i) P[i + j] += (uint64_t)A[i] * mj;
+      if ((j & 7) == 7) {   // keep the columns below 2^63: carry the finished low columns up
+#pragma unroll
+        for (int c = 0; c + 1 < 2 * S + 2; ++c) {
+          P[c + 1] += P[c] >> lane::LB;
+          P[c] &= lane::LMASK;
+        }
+      }
+    }
+    uint64_t c = 0;
+#pragma unroll
+    for (int t = 0; t < 2 * S + 2; ++t) {
+      const uint64_t v = P[t] + c;
+      if (t >= S && t - S < S + 1) ap[t - S] = (uint32_t)v & lane::LMASK;
+      c = v >> lane::LB;
+    }
+    // t = a R - a' p over the low S + 1 limbs (exact: 0 <= t < 2 p); a' += 1 when t >= p
+    int64_t T[S + 1];
+#pragma unroll
+    for (int t2 = 0; t2 < S + 1; ++t2) T[t2] = t2 == S ? (int64_t)A[0] : 0;
+#pragma unroll
+    for (int j = 0; j < S; ++j)
+#pragma unroll
+      for (int i = 0; i + j < S + 1; ++i) T[i + j] -= (int64_t)((uint64_t)ap[i] * m[j]);
+    uint32_t tl[S + 1];
+    int64_t cc = 0;
+#pragma unroll
+    for (int t2 = 0; t2 < S + 1; ++t2) {
+      const int64_t v = T[t2] + cc;
+      tl[t2] = (uint32_t)v & lane::LMASK;
+      cc = v >> lane::LB;
+    }
+    // t >= p ?
+    int32_t bw = 0;
+#pragma unroll
+    for (int t2 = 0; t2 < S + 1; ++t2) {
+      const int32_t v = (int32_t)tl[t2] - (int32_t)(t2 < S ? m[t2] : 0u) + bw;
+      bw = v >> lane::LB;
+    }
+    uint32_t inc = bw == 0 ? 1u : 0u;
+#pragma unroll
+    for (int t2 = 0; t2 < S + 1; ++t2) {
+      const uint32_t v = ap[t2] + inc;
+      ap[t2] = v & lane::LMASK;
+      inc = v >> lane::LB;
+    }
+  }
+  uint4* dst = table + ((size_t)k * ent + d) * TQ;
+  fbs_store_words<S>(dst, A, std::make_integer_sequence<int, G::QA>{});
+  fbs_store_words<S + 1>(dst + G::QA, ap, std::make_integer_sequence<int, G::QAP>{});
+  fbs_store_words<S>(dst + G::QA + G::QAP, bR, std::make_integer_sequence<int, G::QB>{});
+}
+
+}  // namespace fpai

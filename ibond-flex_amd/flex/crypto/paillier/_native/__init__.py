@@ -293,7 +293,8 @@ class Context:
 
     @property
     def split_sampler(self) -> int:
-        """Bit 0: the 4096-bit key-holder tables, bit 1: the public tables are sampled by k_sgp (kernels_sgp.hpp)."""
+        """Bit 0: the 4096-bit key-holder tables, bit 1: the public tables are sampled by k_sgp (kernels_sgp.hpp);
+        bit 2: the 1024/2048-bit key-holder tables hold Shoup rows sampled by k_fbs (kernels_fbs.hpp)."""
         return int(self._get_option(PAI_OPT_SPLIT_SAMPLER))
 
     @property

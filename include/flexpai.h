@@ -133,7 +133,9 @@ typedef struct pai_comm pai_comm;
                                   * tables; $FLEXPAI_FB_WINDOW=auto: 20 for a process with one context)       */
 #define PAI_OPT_SPLIT_SAMPLER 13 /* read-only: bit 0 = the resident 4096-bit key-holder tables, bit 1 = the resident
                                   * public tables are sampled on split pairs (kernels_sgp.hpp: k_sgp, the default;
-                                  * $FLEXPAI_SGP=0 at table build selects k_fbgp / k_pfb)                      */
+                                  * $FLEXPAI_SGP=0 at table build selects k_fbgp / k_pfb); bit 2 = the resident
+                                  * 1024/2048-bit key-holder tables hold Shoup rows sampled on split pairs
+                                  * (kernels_fbs.hpp: k_fbs; $FLEXPAI_FBS at table build)                      */
 
 /* Number of visible GPUs (0 when there is none or the runtime cannot start). */
 int pai_device_count(int* count);

@@ -359,6 +359,8 @@ def main():
     ap.add_argument("--no-strong", action="store_true",
                     help="skip the configs[3] leg (16M elements sharded over the ranks + RCCL all-gather)")
     ap.add_argument("--strong-steps", type=int, default=3, help="timed steps of the configs[3] leg")
+    ap.add_argument("--no-contention", action="store_true",
+                    help="skip the one-GPU rehearsal of the N = 8 all-gather's HBM contention")
     ap.add_argument("--selftest-cpu", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -610,6 +612,53 @@ def main():
         if not ok:
             raise SystemExit("decrypt(encrypt(x)) != x on the device")
         del val, stt
+
+    # ---- HBM contention of the N = 8 all-gather, rehearsed on one GPU: at N = 8 a rank
+    # receives 7 shards (7 x N x W words, 3.8 GB) per step while it encrypts the next one. A device-to-device copy
+    # of that size on a side stream stands in for the RCCL receive writes (pessimistic: a copy also reads the
+    # bytes from HBM, the xGMI receive only writes them); reported: each alone, and both at once.
+    if cfg_id == 1 and world == 1 and not args.no_contention:
+        nbytes = 7 * N * W * 4
+        try:
+            src = torch.empty(nbytes // 4, dtype=torch.int32, device=dev)
+            dst = torch.empty_like(src)
+        except RuntimeError:
+            src = dst = None
+        if src is not None:
+            side = torch.cuda.Stream(dev)
+
+            def timed(run_copy, run_enc):
+                ev = {k: torch.cuda.Event(enable_timing=True) for k in ("c0", "c1", "e0", "e1")}
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                if run_copy:
+                    with torch.cuda.stream(side):
+                        ev["c0"].record(side)
+                        dst.copy_(src, non_blocking=True)
+                        ev["c1"].record(side)
+                if run_enc:
+                    ev["e0"].record(stream)
+                    encrypt(x, ct, ex, index_base)
+                    ev["e1"].record(stream)
+                torch.cuda.synchronize()
+                wall = (time.perf_counter() - t0) * 1e3
+                return (ev["c0"].elapsed_time(ev["c1"]) if run_copy else None,
+                        ev["e0"].elapsed_time(ev["e1"]) if run_enc else None, wall)
+
+            timed(True, True)
+            c_alone = min(timed(True, False)[0] for _ in range(3))
+            e_alone = min(timed(False, True)[1] for _ in range(3))
+            both = [timed(True, True) for _ in range(3)]
+            c_both, e_both, w_both = min(both, key=lambda t: t[2])
+            extra["allgather_contention_1gpu"] = {
+                "received_bytes_per_step_at_n8": nbytes, "copy_alone_ms": c_alone,
+                "copy_alone_gb_s": nbytes / (c_alone * 1e-3) / 1e9, "encrypt_alone_ms": e_alone,
+                "encrypt_with_copy_ms": e_both, "copy_with_encrypt_ms": c_both, "both_wall_ms": w_both,
+                "encrypt_slowdown": e_both / e_alone,
+                "note": "a 3.8 GB device-to-device copy on a side stream (reads + writes HBM) stands in for the N = 8 "
+                        "all-gather's receive writes into this rank's HBM during the next step's encrypt"}
+            del src, dst
+            torch.cuda.empty_cache()
 
     # ---- configs[3] leg (strong scaling): 16M elements over the ranks, every step's ciphertext shards
     # reassembled on every rank by an RCCL all-gather (double-buffered against the next step's encrypt)

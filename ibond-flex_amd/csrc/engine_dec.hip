@@ -1,8 +1,12 @@
 // Lane-engine CRT decryption: kernel instantiations and launch geometry (own translation unit so
 // the engine builds in parallel; the context and the C ABI live in flexpai.hip).
 #include "engine_dec.hpp"
+#ifndef FLEXPAI_XCHECK
+#define FLEXPAI_XCHECK 0   // 1: the test-only library (flexpai.hip: xcheck_env)
+#endif
 
 namespace fpai {
+#if FLEXPAI_XCHECK
 
 template <typename K>
 static int occupancy(K kernel) {
@@ -54,4 +58,5 @@ hipError_t dec_lane_launch(int sa, const DecPreParams& pre, const CrtParams& pw,
   return hipErrorInvalidValue;
 }
 
+#endif
 }  // namespace fpai

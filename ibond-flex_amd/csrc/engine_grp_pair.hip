@@ -1,5 +1,8 @@
 // Pair-group fixed-base kernels for 4096-bit keys (kernels_grp_pair.hpp): instantiations and launches.
 #include "engine_grp_pair.hpp"
+#ifndef FLEXPAI_XCHECK
+#define FLEXPAI_XCHECK 0   // 1: the test-only library (flexpai.hip: xcheck_env)
+#endif
 
 namespace fpai {
 
@@ -7,17 +10,21 @@ static size_t pg_lds() { return ((size_t)(BLOCK / FBGP_TPI) * 2 * FBGP_S + FBGP_
 static size_t main_lds() { return pg_lds(); }   // + the static row staging (pair_table_products)
 static size_t w_lds() { return (size_t)(BLOCK / 4) * 4 * L * 4; }
 
+#if FLEXPAI_XCHECK
 int fbgp_occupancy(int* occ) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, k_fbgp<FBGP_TPI, FBGP_LL>, BLOCK, main_lds()) != hipSuccess ||
       *occ < 1)
     *occ = 1;
   return 0;
 }
+#endif
 
+#if FLEXPAI_XCHECK
 hipError_t fbgp_launch(const FbgpParams& p, int gx, hipStream_t st) {
   hipLaunchKernelGGL((k_fbgp<FBGP_TPI, FBGP_LL>), dim3(gx, 2), dim3(BLOCK), main_lds(), st, p);
   return hipGetLastError();
 }
+#endif
 
 hipError_t fbgp_launch_w(const FbgpParams& p, int gx, hipStream_t st) {
   hipLaunchKernelGGL(k_fbgp_w<4>, dim3(gx, 2), dim3(BLOCK), w_lds(), st, p);

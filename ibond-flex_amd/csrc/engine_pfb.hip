@@ -1,17 +1,22 @@
 // Public-key fixed-base kernels (kernels_pfb.hpp): instantiations and launches.
 #include "engine_pfb.hpp"
+#ifndef FLEXPAI_XCHECK
+#define FLEXPAI_XCHECK 0   // 1: the test-only library (flexpai.hip: xcheck_env)
+#endif
 
 namespace fpai {
 
 static size_t pg_lds() { return ((size_t)(BLOCK / PFB_TPI) * 2 * PFB_S + PFB_S) * 4; }
 static size_t main_lds() { return pg_lds(); }   // + the static row staging (kernels_grp_pair.hpp)
 
+#if FLEXPAI_XCHECK
 int pfb_occupancy(int* occ) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, k_pfb<PFB_TPI, PFB_LL>, BLOCK, main_lds()) != hipSuccess ||
       *occ < 1)
     *occ = 1;
   return 0;
 }
+#endif
 
 hipError_t pfb_build_phase1(const PfbConst* d_c, int nbases, int K, int W, hipStream_t st) {
   constexpr int GPB = BLOCK / PFB_TPI;
@@ -45,9 +50,11 @@ hipError_t pfb_launch_digits(const PfbDigitParams& p, int gx, hipStream_t st) {
   return hipGetLastError();
 }
 
+#if FLEXPAI_XCHECK
 hipError_t pfb_launch(const PfbParams& p, int gx, hipStream_t st) {
   hipLaunchKernelGGL((k_pfb<PFB_TPI, PFB_LL>), dim3(gx), dim3(BLOCK), main_lds(), st, p);
   return hipGetLastError();
 }
+#endif
 
 }  // namespace fpai

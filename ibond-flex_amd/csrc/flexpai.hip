@@ -22,6 +22,22 @@
 #include "engine_fb.hpp"
 #include "engine_fbp.hpp"
 #include "engine_fbs.hpp"
+
+// FLEXPAI_XCHECK (the test-only library libflexpai_xcheck.so, __graft_entry__.build): the kernel generations the
+// pair kernels replaced -- k_fb/k_fb_fin, k_fbg, k_fbgp, k_pfb, the 2S-limb k_dec_* and k_crt_b -- and k_debug,
+// selected by $FLEXPAI_FB_PAIR=0 / $FLEXPAI_SGP=0 / $FLEXPAI_PAIR=0, so that the tests can cross-check the shipping
+// kernels against them. The product library (FLEXPAI_XCHECK 0) does not contain them and ignores those variables.
+#ifndef FLEXPAI_XCHECK
+#define FLEXPAI_XCHECK 0
+#endif
+static const char* xcheck_env(const char* name) {
+#if FLEXPAI_XCHECK
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 #include "engine_pair.hpp"
 #include "engine_dec4.hpp"
 #include "engine_grp_pair.hpp"
@@ -592,7 +608,7 @@ static HBig div_big(const HBig& a, const HBig& m) {
 // 2^(28 S) >= 2^24 n. Constants: n, (1 - R) and (1 - R^2) mod n, the pair of R^3 mod n^2, the op list for n.
 static int setup_pe(pai_ctx* c, const HBig& n) {
   bool pair = true;
-  if (const char* e = getenv("FLEXPAI_PAIR")) pair = atoi(e) != 0;
+  if (const char* e = xcheck_env("FLEXPAI_PAIR")) pair = atoi(e) != 0;
   const size_t RS = (size_t)LB * D4_S;
   if (!pair || n.bits() + 24 > RS || n.bits() <= 1536) return 0;
   std::vector<uint32_t> prog;
@@ -630,7 +646,7 @@ static int upload_fb(pai_ctx* c, const std::vector<T>& v, T** out) {
 // 2^(-56 K) mod P^2 as (C mod P, C div P), the chunk weights w 2^(16 c) C_A mod P of c0 = (1, w |M|), and 2^20 P.
 // FLEXPAI_SGP=0 keeps the group-engine samplers (k_fbgp, k_pfb).
 static bool sgp_enabled() {
-  const char* e = getenv("FLEXPAI_SGP");
+  const char* e = xcheck_env("FLEXPAI_SGP");
   return !e || atoi(e) != 0;
 }
 
@@ -695,7 +711,7 @@ static int fb_row_words(int sb) {
 // R >= 2^24 p_h ($FLEXPAI_FB_PAIR=0 selects k_fbg); its rows are the canonical pair as 2 x 64 words
 static bool fb_gpair_possible(const pai_ctx* c) {
   if (c->crt_sb != GRP_TPI * L) return false;
-  if (const char* e = getenv("FLEXPAI_FB_PAIR"))
+  if (const char* e = xcheck_env("FLEXPAI_FB_PAIR"))
     if (atoi(e) == 0) return false;
   for (const HBig* h : {&c->fb_p, &c->fb_q})
     if (h->bits() + 24 > (size_t)LB * FBGP_S || h->bits() > (size_t)LB * FBGP_SP || h->bits() > (size_t)32 * FBGP_PW)
@@ -711,7 +727,7 @@ static int fb_pair_possible(const pai_ctx* c) {
   const int sb = c->crt_sb;
   const int ps = sb == 37 ? 19 : sb == 74 ? 37 : 0;
   if (!ps) return 0;
-  if (const char* e = getenv("FLEXPAI_FB_PAIR"))
+  if (const char* e = xcheck_env("FLEXPAI_FB_PAIR"))
     if (atoi(e) == 0) return 0;
   const int pw = ps == 19 ? FbpGeom<19>::PW : FbpGeom<37>::PW;
   for (const HBig* h : {&c->fb_p, &c->fb_q})
@@ -896,8 +912,14 @@ static int ensure_fb(pai_ctx* c) {
   const int ps = grp ? 0 : fb_pair_possible(c);
   const bool pair_ok = ps != 0;
   const bool shoup = pair_ok && fb_shoup_possible(c);
+#if !FLEXPAI_XCHECK
+  if (!grp && !pair_ok) return fb_unavailable(c, "key outside the pair sampler's bounds");
+#endif
   // 4096-bit keys: pair products on lane groups of 4 x 19 limbs (kernels_grp_pair.hpp), R = 2^(28 76) >= 2^24 p_h
   const bool gpair_ok = grp && fb_gpair_possible(c);
+#if !FLEXPAI_XCHECK
+  if (grp && !(gpair_ok && sgp_enabled())) return fb_unavailable(c, "key outside the split-pair sampler's bounds");
+#endif
   const int lohi_limbs = pair_ok ? std::max(sb, 2 * ps) : gpair_ok ? std::max(sb, 2 * FBGP_S) : sb;
   FbgpHalf gv[2];
   SgpHalf sv[2];
@@ -1132,11 +1154,17 @@ static int ensure_fb(pai_ctx* c) {
       if (pair_host_invert(primes[h], gpair_ok ? gcval[h] : pcval[h], 2 * K, gpair_ok ? FBGP_S : ps))
         return fb_unavailable(c, pai_last_error());
   }
+#if FLEXPAI_XCHECK
   const hipError_t be = gpair_ok  ? fbgp_build_phase2(c->d_fbgp_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
                         : grp     ? grp_build_tables(c->d_fb_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
                         : shoup   ? fbs_build_phase2(ps, c->d_fbp_halves, c->d_fbs_cst, (uint4*)t[0], (uint4*)t[1], K, W, nullptr)
                         : pair_ok ? fbp_build_phase2(ps, c->d_fbp_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr)
                                   : fb_build_tables(sb, c->d_fb_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
+#else
+  const hipError_t be = gpair_ok ? fbgp_build_phase2(c->d_fbgp_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
+                        : shoup  ? fbs_build_phase2(ps, c->d_fbp_halves, c->d_fbs_cst, (uint4*)t[0], (uint4*)t[1], K, W, nullptr)
+                                 : fbp_build_phase2(ps, c->d_fbp_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
+#endif
   if (be != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return fb_unavailable(c, "table construction failed");
   for (void* p : lohi) fb_scratch.push_back(p);
@@ -1178,7 +1206,7 @@ static int setup_fbg(pai_ctx* c, const HBig& p, const HBig& q) {
   // split-pair decryption (kernels_dec4.hpp): p_h of at most 28 * 74 - 24 bits (R >= 2^24 p_h), the ciphertext
   // in at most 4 chunks of 74 limbs; $FLEXPAI_PAIR=0 keeps the group engine's k_decrypt
   bool pair = true;
-  if (const char* e = getenv("FLEXPAI_PAIR")) pair = atoi(e) != 0;
+  if (const char* e = xcheck_env("FLEXPAI_PAIR")) pair = atoi(e) != 0;
   const size_t RS = (size_t)LB * D4_S;
   const int kp = (int)((32 * (size_t)c->ct_words + RS - 1) / RS);
   if (pair && pb + 24 <= RS && kp <= 4 && c->tpi_d == 4) {
@@ -1322,7 +1350,7 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
   }
   // pair kernels: residues mod p_h^2 as (A, B) over the sa limbs of p_h, R = 2^(28 sa) >= 2^12 p_h
   bool pair = true;
-  if (const char* e = getenv("FLEXPAI_PAIR")) pair = atoi(e) != 0;
+  if (const char* e = xcheck_env("FLEXPAI_PAIR")) pair = atoi(e) != 0;
   if (pair && (size_t)LB * sa >= pb + 12) {
     const int S2 = 2 * sa;
     auto split = [&](const HBig& v, const HBig& P) {   // canonical pair of v < P^2
@@ -1454,6 +1482,13 @@ static int set_private_impl(pai_ctx* c, HBig p, HBig q) {
   c->n_limbs = (int)((c->n.bits() + LB - 1) / LB);
   c->has_priv = true;
   if ((rc = setup_crt(c, p, q))) return rc;
+#if !FLEXPAI_XCHECK
+  // a key outside the pair kernels' bounds (R = 2^(28 S) >= 2^12 p_h): CRT encryption and lane decryption would
+  // need the 2S-limb kernels of the test build; it encrypts on the public-key kernels and decrypts on the group
+  // engine instead
+  if (c->crt_ok && !c->crt_pair_ok) c->crt_ok = false;
+  if (c->dec_lane_ok && !c->dec_pair_ok) c->dec_lane_ok = false;
+#endif
   return 0;
 }
 
@@ -1654,11 +1689,17 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
   const long long N = e.n;
   const long long chunk = std::min(N, CRT_CHUNK);
   int occF = 1, occG = 1;
+#if FLEXPAI_XCHECK
   if (grp) {
     if (c->fb_gpair) fbgp_occupancy(&occF);
     else grp_occupancy(&occF);
+  } else if (!c->fb_pair_s && fb_occupancy(SB, &occF, &occG)) {
+    return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
   }
-  else if (fb_occupancy(SB, &occF, &occG)) return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
+#else
+  if (grp && !(c->fb_gpair && c->d_sgp_fb)) return fail(PAI_ERR_KEY, "fixed-base encrypt: no split-pair tables");
+  if (!grp && !c->fb_pair_s) return fail(PAI_ERR_KEY, "fixed-base encrypt: no pair tables");
+#endif
   if (c->fb_pair_s && (c->fb_shoup ? fbs_occupancy(c->fb_pair_s, &occF) : fbp_occupancy(c->fb_pair_s, &occF)))
     return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
   // elements per block: one per lane, one per lane pair (k_fbs), or one per lane group (grp)
@@ -1713,10 +1754,14 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
         const long long nb = (n + SGP_PAIRS - 1) / SGP_PAIRS;
         HIPCHK(sgp_launch(sp, (int)std::max<long long>(1, std::min<long long>(nb, (long long)occS * c->cus / 2)), 2, st));
       } else {
+#if FLEXPAI_XCHECK
         HIPCHK(fbgp_launch(pg, gF, st));
+#endif
       }
     } else {
+#if FLEXPAI_XCHECK
       HIPCHK(grp ? grp_launch_fb(pf, gF, st) : fb_launch(SB, pf, gF, st));
+#endif
     }
     stage_mark(c, 2, st);
     c->fb_last_w = w;
@@ -1747,6 +1792,7 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
       stage_mark(c, 3, st);
       continue;
     }
+#if FLEXPAI_XCHECK
     FbFinParams pg{};
     pg.w = w;
     pg.n = n;
@@ -1759,6 +1805,9 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     pg.ct_words = c->ct_words;
     HIPCHK(fb_launch_fin(SB, pg, (int)std::min<long long>(gxG, (n + LANE_BLOCK - 1) / LANE_BLOCK), st));
     stage_mark(c, 3, st);
+#else
+    (void)gxG;
+#endif
   }
   return 0;
 }
@@ -1995,10 +2044,14 @@ static bool pfb_wanted(pai_ctx* c, long long n) {
 static int launch_pfb(pai_ctx* c, const EncParams& e, hipStream_t st) {
   const long long N = e.n;
   const long long chunk = std::min(N, CRT_CHUNK);
+#if FLEXPAI_XCHECK
   int occ = 1;
   pfb_occupancy(&occ);
   constexpr int GPB = BLOCK / PFB_TPI;
   const int gx = (int)std::max<long long>(1, std::min<long long>((chunk + GPB - 1) / GPB, (long long)occ * c->cus));
+#else
+  if (!c->d_sgp_pfb) return fail(PAI_ERR_KEY, "public fixed-base encrypt: no split-pair tables");
+#endif
   const size_t dbytes = (size_t)c->pfb_K * 4, xbytes = (size_t)2 * PFB_SP * 4;
   int rc;
   if ((rc = ensure_work(c, (dbytes + xbytes) * chunk))) return rc;
@@ -2028,7 +2081,9 @@ static int launch_pfb(pai_ctx* c, const EncParams& e, hipStream_t st) {
       const long long nb = (n + SGP_PAIRS - 1) / SGP_PAIRS;
       HIPCHK(sgp_launch(sp, (int)std::max<long long>(1, std::min<long long>(nb, (long long)occS * c->cus)), 1, st));
     } else {
+#if FLEXPAI_XCHECK
       HIPCHK(pfb_launch(pp, (int)std::min<long long>(gx, (n + GPB - 1) / GPB), st));
+#endif
     }
     stage_mark(c, 2, st);
     PeParams pf{};
@@ -2156,6 +2211,9 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
   int occA = 1, occB = 1;
   if (crt_lane_occupancy(SA, &occA, &occB)) return fail(PAI_ERR_KEY, "CRT encrypt: unsupported size");
   const bool bpair = c->crt_pair_ok;   // stage B on pairs (kernels_pair.hpp)
+#if !FLEXPAI_XCHECK
+  if (!bpair) return fail(PAI_ERR_KEY, "CRT encrypt: no pair constants");
+#endif
   if (bpair && crt_b_pair_occupancy(SA, &occB)) return fail(PAI_ERR_KEY, "CRT encrypt: unsupported size");
   const long long lanes_blocks = (chunk + LANE_BLOCK - 1) / LANE_BLOCK;
   const int gxA = (int)std::max<long long>(1, std::min<long long>(lanes_blocks, (long long)occA * c->cus / 2));
@@ -2196,7 +2254,9 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
     pb.scratch = (uint32_t*)c->d_scratch;
     const int gB = (int)std::min<long long>(gxB, (n + LANE_BLOCK - 1) / LANE_BLOCK);
     if (bpair) HIPCHK(crt_b_pair_launch(SA, pb, gB, st));
+#if FLEXPAI_XCHECK
     else HIPCHK(crt_launch_b(SA, pb, gB, st));
+#endif
     HIPCHK(hipGetLastError());
     stage_mark(c, 2, st);
     CrtFinParams f{};
@@ -2444,6 +2504,7 @@ static int launch_dec4(pai_ctx* c, const DecParams& d, hipStream_t st) {
   return 0;
 }
 
+#if FLEXPAI_XCHECK
 // lane-engine decryption (kernels_dec.hpp, engine_dec.hip), in chunks of CRT_CHUNK elements
 static int launch_dec_lane(pai_ctx* c, const DecParams& d, hipStream_t st) {
   const long long N = d.n;
@@ -2486,6 +2547,7 @@ static int launch_dec_lane(pai_ctx* c, const DecParams& d, hipStream_t st) {
   }
   return 0;
 }
+#endif
 
 int pai_decrypt_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t N, double* d_val, int64_t* d_mant,
                     int32_t* d_status, uint32_t* d_raw, void* stream) {
@@ -2517,7 +2579,9 @@ int pai_decrypt_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size
   hipStream_t st = (hipStream_t)stream;
   if (c->dec_pair_ok && c->dec_lane_enabled) return launch_dec_pair(c, p, st);
   if (c->dec4_ok && c->dec_lane_enabled) return launch_dec4(c, p, st);
+#if FLEXPAI_XCHECK
   if (c->dec_lane_ok && c->dec_lane_enabled) return launch_dec_lane(c, p, st);
+#endif
   switch (c->tpi_d) {
     case 1: return launch_decrypt<1>(c, p, st);
     case 2: return launch_decrypt<2>(c, p, st);
@@ -3229,7 +3293,8 @@ extern "C" int pai_debug_fb_w(pai_ctx* c, uint32_t* out, size_t max_words, long 
   return 0;
 }
 
-// ------------------------------------------------------------------ engine unit-test hook
+// ------------------------------------------------------------------ engine unit-test hook (test build only)
+#if FLEXPAI_XCHECK
 template <int TPI>
 static int launch_debug(pai_ctx* c, DbgParams& p) {
   constexpr int S = TPI * L;
@@ -3244,8 +3309,14 @@ static int launch_debug(pai_ctx* c, DbgParams& p) {
   return 0;
 }
 
+#endif
+
 extern "C" int pai_debug_engine(pai_ctx* c, int op, const uint32_t* a, const uint32_t* b, size_t N, uint32_t* out,
                                 int32_t* flag) {
+#if !FLEXPAI_XCHECK
+  (void)c, (void)op, (void)a, (void)b, (void)N, (void)out, (void)flag;
+  return fail(PAI_ERR_ARG, "pai_debug_engine: in the test build (libflexpai_xcheck.so) only");
+#else
   if (!c || N == 0) return fail(PAI_ERR_ARG, "pai_debug_engine: bad args");
   CtxLock lk(c);
   HIPCHK(hipSetDevice(c->device));
@@ -3270,4 +3341,5 @@ extern "C" int pai_debug_engine(pai_ctx* c, int op, const uint32_t* a, const uin
   HIPCHK(hipMemcpy(out, dout, N * W * 4, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(flag, dflag, N * 4, hipMemcpyDeviceToHost));
   return 0;
+#endif
 }

@@ -15,6 +15,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FLEXPAI_LIB") or os.path.join(_HERE, "libflexpai.so")   # override: experiments only
+# the test-only build (FLEXPAI_XCHECK): also holds the kernel generations the pair kernels replaced, selected by
+# $FLEXPAI_FB_PAIR=0 / $FLEXPAI_SGP=0 / $FLEXPAI_PAIR=0, for the tests that cross-check against them
+XCHECK_LIB_PATH = os.path.join(_HERE, "libflexpai_xcheck.so")
 
 PAI_F32, PAI_F64, PAI_I64 = 0, 1, 2
 PAI_OBF_NONE, PAI_OBF_GIVEN, PAI_OBF_RNG = 0, 1, 2
@@ -39,6 +42,7 @@ EXPORTED = ("pai_device_count", "pai_device_mem_info", "pai_ctx_create", "pai_ct
 PAI_COMM_ID_BYTES = 128
 
 _lib = None
+_libs = {}
 _lib_lock = threading.Lock()
 
 
@@ -47,11 +51,12 @@ class NativeError(RuntimeError):
 
 
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load libflexpai.so and declare the C signatures. Raises if the library is absent."""
+    """Load libflexpai.so (or another build of the C ABI, e.g. XCHECK_LIB_PATH) and declare the C signatures.
+    Raises if the library is absent."""
     global _lib
     with _lib_lock:
-        if _lib is not None:
-            return _lib
+        if path in _libs:
+            return _libs[path]
         if not os.path.exists(path):
             raise NativeError(f"flexpai native library not found at {path}; run __graft_entry__.build() "
                               f"(hipcc --offload-arch=gfx950). There is no CPU fallback.")
@@ -100,7 +105,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         for name in EXPORTED:
             if name not in ("pai_ctx_destroy", "pai_last_error", "pai_comm_destroy"):
                 getattr(lib, name).restype = ctypes.c_int
-        _lib = lib
+        _libs[path] = lib
+        if path == LIB_PATH:
+            _lib = lib
         return lib
 
 
@@ -145,18 +152,21 @@ class Comm:
         _check(load_library().pai_comm_unique_id(buf))
         return bytes(buf)
 
+    def _chk(self, rc: int):
+        _check(rc, self.lib)
+
     def __init__(self, uid: bytes, world: int, rank: int, device: int = 0):
         if len(uid) != PAI_COMM_ID_BYTES:
             raise ValueError("communicator id must be %d bytes" % PAI_COMM_ID_BYTES)
         self.lib = load_library()
         h = ctypes.c_void_p()
-        _check(self.lib.pai_comm_create(uid, world, rank, device, ctypes.byref(h)))
+        self._chk(self.lib.pai_comm_create(uid, world, rank, device, ctypes.byref(h)))
         self._h, self.world, self.rank = h, world, rank
 
     def allgather_shards(self, d_ct: int, d_exp: int, n_per_rank: int, ct_words: int, d_ct_all: int,
                          d_exp_all: int, stream: int = 0):
         """Device pointers (e.g. torch tensor .data_ptr()); asynchronous on `stream`."""
-        _check(self.lib.pai_allgather_shards_dev(self._h, d_ct, d_exp, n_per_rank, ct_words, d_ct_all, d_exp_all,
+        self._chk(self.lib.pai_allgather_shards_dev(self._h, d_ct, d_exp, n_per_rank, ct_words, d_ct_all, d_exp_all,
                                                  stream or None))
 
     def close(self):
@@ -171,9 +181,9 @@ class Comm:
             pass
 
 
-def _check(rc: int):
+def _check(rc: int, lib=None):
     if rc != 0:
-        msg = load_library().pai_last_error().decode(errors="replace")
+        msg = (lib or load_library()).pai_last_error().decode(errors="replace")
         if rc == -5:
             raise ZeroDivisionError(msg)          # gmpy_math.invert (gmpy_math.py:71-72)
         if rc == -4 and ("does not match" in msg or "have to be different" in msg):
@@ -192,21 +202,25 @@ def int_to_le(v: int, nbytes: int) -> bytes:
 class Context:
     """One key on one GPU. Created lazily by the Python layer (never pickled, never forked)."""
 
-    def __init__(self, n: int, device: int = 0, p: Optional[int] = None, q: Optional[int] = None):
-        self.lib = load_library()
+    def __init__(self, n: int, device: int = 0, p: Optional[int] = None, q: Optional[int] = None, lib=None):
+        """lib: another build of the C ABI (load_library(XCHECK_LIB_PATH) in the cross-check tests)."""
+        self.lib = lib or load_library()
         self.n = n
         nbytes = (n.bit_length() + 7) // 8
         buf = int_to_le(n, nbytes)
         h = ctypes.c_void_p()
-        _check(self.lib.pai_ctx_create(buf, nbytes, device, ctypes.byref(h)))
+        self._chk(self.lib.pai_ctx_create(buf, nbytes, device, ctypes.byref(h)))
         self._h = h
         kb, cw, pw = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        _check(self.lib.pai_ctx_info(h, ctypes.byref(kb), ctypes.byref(cw), ctypes.byref(pw)))
+        self._chk(self.lib.pai_ctx_info(h, ctypes.byref(kb), ctypes.byref(cw), ctypes.byref(pw)))
         self.key_bits, self.ct_words, self.pt_words = kb.value, cw.value, pw.value
         self.has_private = False
         self.calls = collections.Counter()     # C-ABI entry points this context has run (tests, stats)
         if p is not None:
             self.set_private(p, q)
+
+    def _chk(self, rc: int):
+        _check(rc, self.lib)
 
     @property
     def handle(self):
@@ -214,14 +228,14 @@ class Context:
 
     def set_private(self, p: int, q: int):
         hb = max(p.bit_length(), q.bit_length()) // 8 + 1
-        _check(self.lib.pai_ctx_set_private(self._h, int_to_le(p, hb), int_to_le(q, hb), hb))
+        self._chk(self.lib.pai_ctx_set_private(self._h, int_to_le(p, hb), int_to_le(q, hb), hb))
         self.has_private = True
         if os.environ.get("FLEXPAI_CRT", "1").strip() == "0":
             self.set_crt(False)
 
     def _get_option(self, opt: int) -> int:
         v = ctypes.c_int()
-        _check(self.lib.pai_ctx_get_option(self._h, opt, ctypes.byref(v)))
+        self._chk(self.lib.pai_ctx_get_option(self._h, opt, ctypes.byref(v)))
         return v.value
 
     @property
@@ -234,19 +248,19 @@ class Context:
         return bool(self._get_option(PAI_OPT_CRT_ENCRYPT))
 
     def set_stage_timing(self, enabled: bool):
-        _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_STAGE_TIMING, 1 if enabled else 0))
+        self._chk(self.lib.pai_ctx_set_option(self._h, PAI_OPT_STAGE_TIMING, 1 if enabled else 0))
 
     def stage_times(self):
         """Kernel durations (ms) of the last encrypt call (needs set_stage_timing(True))."""
         buf = (ctypes.c_float * 8)()
         cnt = ctypes.c_int()
-        _check(self.lib.pai_ctx_stage_times(self._h, buf, 8, ctypes.byref(cnt)))
+        self._chk(self.lib.pai_ctx_stage_times(self._h, buf, 8, ctypes.byref(cnt)))
         return [float(buf[i]) for i in range(cnt.value)]
 
     def set_crt(self, enabled: bool):
         """Encrypt through the private-key CRT kernels (default when available) or the public-key one.
         The ciphertext bits are identical either way."""
-        _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_CRT_ENCRYPT, 1 if enabled else 0))
+        self._chk(self.lib.pai_ctx_set_option(self._h, PAI_OPT_CRT_ENCRYPT, 1 if enabled else 0))
 
     @property
     def lane_decrypt(self) -> bool:
@@ -254,7 +268,7 @@ class Context:
         return bool(self._get_option(PAI_OPT_LANE_DECRYPT))
 
     def set_lane_decrypt(self, enabled: bool):
-        _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_LANE_DECRYPT, 1 if enabled else 0))
+        self._chk(self.lib.pai_ctx_set_option(self._h, PAI_OPT_LANE_DECRYPT, 1 if enabled else 0))
 
     @property
     def fixed_base(self) -> bool:
@@ -262,13 +276,13 @@ class Context:
         return bool(self._get_option(PAI_OPT_FIXED_BASE))
 
     def set_fixed_base(self, enabled: bool):
-        _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_FIXED_BASE, 1 if enabled else 0))
+        self._chk(self.lib.pai_ctx_set_option(self._h, PAI_OPT_FIXED_BASE, 1 if enabled else 0))
 
     def fixed_base_info(self):
         """(g_p, g_q, K, W): the generators, the exponent digit count and the digit window (bits) of
         the fixed-base path."""
         gp, gq, k, w = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int(), ctypes.c_int()
-        _check(self.lib.pai_ctx_fixed_base_info(self._h, ctypes.byref(gp), ctypes.byref(gq), ctypes.byref(k),
+        self._chk(self.lib.pai_ctx_fixed_base_info(self._h, ctypes.byref(gp), ctypes.byref(gq), ctypes.byref(k),
                                                 ctypes.byref(w)))
         return gp.value, gq.value, k.value, w.value
 
@@ -279,7 +293,7 @@ class Context:
 
     def set_fb_window(self, bits: int):
         """Digit window of the fixed-base tables (8, 12, 16 or 20 .. 24); the tables are rebuilt lazily."""
-        _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_FB_WINDOW, int(bits)))
+        self._chk(self.lib.pai_ctx_set_option(self._h, PAI_OPT_FB_WINDOW, int(bits)))
 
     @property
     def fb_ready(self) -> bool:
@@ -304,19 +318,19 @@ class Context:
 
     def prepare_fixed_base(self):
         """Build the fixed-base tables now (NativeError with the reason when unavailable)."""
-        _check(self.lib.pai_ctx_fixed_base_prepare(self._h))
+        self._chk(self.lib.pai_ctx_fixed_base_prepare(self._h))
 
     def fixed_base_setup(self):
         """(host_ms, device_ms, table_bytes) of the last table build."""
         hm, dm, tb = ctypes.c_float(), ctypes.c_float(), ctypes.c_uint64()
-        _check(self.lib.pai_ctx_fixed_base_setup(self._h, ctypes.byref(hm), ctypes.byref(dm), ctypes.byref(tb)))
+        self._chk(self.lib.pai_ctx_fixed_base_setup(self._h, ctypes.byref(hm), ctypes.byref(dm), ctypes.byref(tb)))
         return float(hm.value), float(dm.value), int(tb.value)
 
     def fixed_base_policy(self):
         """(seen, threshold): device-RNG elements encrypted under this key so far, and the count at which
         the fixed-base tables get built (0 once resident or unavailable); include/flexpai.h."""
         seen, thr = ctypes.c_longlong(), ctypes.c_longlong()
-        _check(self.lib.pai_ctx_fixed_base_policy(self._h, ctypes.byref(seen), ctypes.byref(thr)))
+        self._chk(self.lib.pai_ctx_fixed_base_policy(self._h, ctypes.byref(seen), ctypes.byref(thr)))
         return int(seen.value), int(thr.value)
 
     # ------------------------------------------------------ public-key fixed bases (kernels_pfb.hpp)
@@ -326,7 +340,7 @@ class Context:
         return bool(self._get_option(PAI_OPT_PUBLIC_FB))
 
     def set_public_fixed_base(self, enabled: bool):
-        _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_PUBLIC_FB, 1 if enabled else 0))
+        self._chk(self.lib.pai_ctx_set_option(self._h, PAI_OPT_PUBLIC_FB, 1 if enabled else 0))
 
     @property
     def pfb_ready(self) -> bool:
@@ -334,24 +348,24 @@ class Context:
 
     def set_pfb_window(self, bits: int):
         """Digit window of the public tables: 12, 16 or 20 (the windows pinned to the reference's goldens)."""
-        _check(self.lib.pai_ctx_set_option(self._h, PAI_OPT_PFB_WINDOW, int(bits)))
+        self._chk(self.lib.pai_ctx_set_option(self._h, PAI_OPT_PFB_WINDOW, int(bits)))
 
     def prepare_public_fixed_base(self):
-        _check(self.lib.pai_ctx_public_fb_prepare(self._h))
+        self._chk(self.lib.pai_ctx_public_fb_prepare(self._h))
 
     def set_public_bases(self, bases: Sequence[int]):
         """Fix the 33 bases g_0..g_32 instead of drawing them (tests, reproducible runs). Each must be a unit
         in (1, n), all distinct, and g_0 must have Jacobi symbol -1 mod n (else NativeError)."""
         nb = (self.n.bit_length() + 7) // 8
         buf = b"".join(int_to_le(g, nb) for g in bases)
-        _check(self.lib.pai_ctx_public_fb_set_bases(self._h, buf, nb, len(bases)))
+        self._chk(self.lib.pai_ctx_public_fb_set_bases(self._h, buf, nb, len(bases)))
 
     def public_fixed_base_info(self):
         """(bases, K, W, K0) of the resident public tables."""
         nb = (self.n.bit_length() + 7) // 8
         buf = (ctypes.c_uint8 * (nb * PFB_NBASES))()
         nbs, k, w, k0 = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        _check(self.lib.pai_ctx_public_fb_info(self._h, buf, nb, ctypes.byref(nbs), ctypes.byref(k), ctypes.byref(w),
+        self._chk(self.lib.pai_ctx_public_fb_info(self._h, buf, nb, ctypes.byref(nbs), ctypes.byref(k), ctypes.byref(w),
                                                ctypes.byref(k0)))
         raw = bytes(buf)
         bases = [int.from_bytes(raw[j * nb:(j + 1) * nb], "little") for j in range(nbs.value)]
@@ -359,7 +373,7 @@ class Context:
 
     def public_fixed_base_policy(self):
         seen, thr = ctypes.c_longlong(), ctypes.c_longlong()
-        _check(self.lib.pai_ctx_public_fb_policy(self._h, ctypes.byref(seen), ctypes.byref(thr)))
+        self._chk(self.lib.pai_ctx_public_fb_policy(self._h, ctypes.byref(seen), ctypes.byref(thr)))
         return int(seen.value), int(thr.value)
 
     def close(self):
@@ -417,7 +431,7 @@ class Context:
                 r_stride = r_bytes
         key = rng_key if rng_key is not None else os.urandom(32)
         self.calls["pai_encrypt"] += 1
-        _check(self.lib.pai_encrypt(self._h, dt, _ptr(x), N, exp_mode, fixed_exp, obf_mode,
+        self._chk(self.lib.pai_encrypt(self._h, dt, _ptr(x), N, exp_mode, fixed_exp, obf_mode,
                                     _ptr(r_buf) if r_buf is not None else None, r_stride, r_bytes,
                                     key, index_base, _ptr(ct), _ptr(ex), _ptr(st)))
         return ct, ex, st
@@ -434,7 +448,7 @@ class Context:
         ex_ptrs = (ctypes.c_void_p * k)(*[_ptr(e) for e in exps])
         out = np.empty((N, self.ct_words), dtype=np.uint32)
         oe = np.empty(N, dtype=np.int32)
-        _check(self.lib.pai_add(self._h, ct_ptrs, ex_ptrs, k, N, _ptr(out), _ptr(oe)))
+        self._chk(self.lib.pai_add(self._h, ct_ptrs, ex_ptrs, k, N, _ptr(out), _ptr(oe)))
         return out, oe
 
     def mul(self, ct: np.ndarray, exp: np.ndarray, x: np.ndarray):
@@ -451,7 +465,7 @@ class Context:
         out = np.empty((N, self.ct_words), dtype=np.uint32)
         oe = np.empty(N, dtype=np.int32)
         st = np.empty(N, dtype=np.int32)
-        _check(self.lib.pai_mul(self._h, _ptr(ct), _ptr(exp), N, scalar_dtype(x), _ptr(x), 1 if x.size == N and N > 1 else 0,
+        self._chk(self.lib.pai_mul(self._h, _ptr(ct), _ptr(exp), N, scalar_dtype(x), _ptr(x), 1 if x.size == N and N > 1 else 0,
                                 _ptr(out), _ptr(oe), _ptr(st)))
         return out, oe, st
 
@@ -469,7 +483,7 @@ class Context:
         out = np.empty((N, self.ct_words), dtype=np.uint32)
         oe = np.empty(N, dtype=np.int32)
         st = np.empty(N, dtype=np.int32)
-        _check(self.lib.pai_add_plain(self._h, _ptr(ct), _ptr(exp), N, scalar_dtype(x), _ptr(x),
+        self._chk(self.lib.pai_add_plain(self._h, _ptr(ct), _ptr(exp), N, scalar_dtype(x), _ptr(x),
                                       1 if x.size == N and N > 1 else 0, _ptr(out), _ptr(oe), _ptr(st)))
         return out, oe, st
 
@@ -487,7 +501,7 @@ class Context:
         oe = np.empty(max(nseg, 0), dtype=np.int32)
         if nseg <= 0:
             return out, oe
-        _check(self.lib.pai_segment_add(self._h, _ptr(ct), _ptr(exp), exp.size, _ptr(index), _ptr(seg_off), nseg,
+        self._chk(self.lib.pai_segment_add(self._h, _ptr(ct), _ptr(exp), exp.size, _ptr(index), _ptr(seg_off), nseg,
                                         _ptr(out), _ptr(oe)))
         return out, oe
 
@@ -502,7 +516,7 @@ class Context:
         self.calls["pai_matmul"] += 1
         out = np.empty((m * d, self.ct_words), dtype=np.uint32)
         oe = np.empty(m * d, dtype=np.int32)
-        _check(self.lib.pai_matmul(self._h, _ptr(ct), _ptr(exp), m, K, scalar_dtype(x), _ptr(x), d, _ptr(out), _ptr(oe)))
+        self._chk(self.lib.pai_matmul(self._h, _ptr(ct), _ptr(exp), m, K, scalar_dtype(x), _ptr(x), d, _ptr(out), _ptr(oe)))
         return out, oe
 
     def decrypt(self, ct: np.ndarray, exp: np.ndarray, want_raw: bool = False):
@@ -515,7 +529,7 @@ class Context:
         mant = np.empty(N, dtype=np.int64)
         st = np.empty(N, dtype=np.int32)
         raw = np.empty((N, self.pt_words), dtype=np.uint32) if want_raw else None
-        _check(self.lib.pai_decrypt(self._h, _ptr(ct), _ptr(exp), N, _ptr(val), _ptr(mant), _ptr(st),
+        self._chk(self.lib.pai_decrypt(self._h, _ptr(ct), _ptr(exp), N, _ptr(val), _ptr(mant), _ptr(st),
                                     _ptr(raw) if raw is not None else None))
         return val, mant, st, raw
 

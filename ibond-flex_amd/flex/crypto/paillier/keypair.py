@@ -1,3 +1,8 @@
+#  Portions of this file (the seeded key-generation loop of generate_paillier_keypair and the classes' slot
+#  lists) follow flex/crypto/paillier/keypair.py of iBond-flex so that seeded keys and pickles match it bit
+#  for bit: Copyright 2020 The FLEX Authors, licensed under the Apache License, Version 2.0
+#  (http://www.apache.org/licenses/LICENSE-2.0). Distributed on an "AS IS" BASIS, WITHOUT WARRANTIES OR
+#  CONDITIONS OF ANY KIND, either express or implied.
 """Paillier keys — same classes, slots and behaviour as flex/crypto/paillier/keypair.py:20-127.
 
 Key generation is host-side and one-time; the seeded path reproduces the

@@ -56,3 +56,12 @@ def golden_pfb():
     import json
     with open(os.path.join(ROOT, "tests", "golden", "paillier_golden_pfb.json")) as f:
         return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def xlib():
+    """The test-only build of the C ABI (libflexpai_xcheck.so, __graft_entry__.build): the product kernels plus the
+    generations they replaced, selected by $FLEXPAI_FB_PAIR=0 / $FLEXPAI_SGP=0 / $FLEXPAI_PAIR=0, for the
+    cross-checks. Contexts on it: _native.Context(..., lib=xlib)."""
+    from flex.crypto.paillier import _native
+    return _native.load_library(_native.XCHECK_LIB_PATH)

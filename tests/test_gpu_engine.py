@@ -1,4 +1,5 @@
-"""Unit tests of the lane-group big-number engine (bn_group.hpp) through pai_debug_engine."""
+"""Unit tests of the lane-group big-number engine (bn_group.hpp) through pai_debug_engine (k_debug), which is in
+the test build (libflexpai_xcheck.so) only; the product library refuses the call."""
 import ctypes
 import random
 
@@ -10,7 +11,7 @@ pytestmark = pytest.mark.gpu
 
 def _run(ctx, op, a_vals, b_vals):
     from flex.crypto.paillier import _native as N
-    lib = N.load_library()
+    lib = ctx.lib
     lib.pai_debug_engine.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
     A = N.ints_to_words(a_vals, ctx.ct_words)
@@ -24,11 +25,11 @@ def _run(ctx, op, a_vals, b_vals):
 
 
 @pytest.fixture(scope="module", params=[1024, 2048, 4096])
-def setup(request, golden):
+def setup(request, golden, xlib):
     from flex.crypto.paillier import _native as N
     k = golden["keys"][str(request.param)]
     n = int(k["n"], 16)
-    ctx = N.Context(n, 0)
+    ctx = N.Context(n, 0, lib=xlib)
     S = 37 * {1024: 2, 2048: 4, 4096: 8}[request.param]   # L = 37 limbs per lane (bn_group.hpp)
     return ctx, n, n * n, 28 * S
 
@@ -102,3 +103,16 @@ def test_modexp_n(setup):
     a = [rnd.randrange(1, n) for _ in range(11)]
     got, _ = _run(ctx, 4, a, a)
     assert got == [pow(x, n, N2) for x in a]
+
+
+def test_product_library_refuses_the_debug_hook(golden):
+    from flex.crypto.paillier import _native as N
+    ctx = N.Context(int(golden["keys"]["1024"]["n"], 16), 0)
+    lib = N.load_library()
+    lib.pai_debug_engine.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]
+    A = N.ints_to_words([5], ctx.ct_words)
+    out = np.zeros_like(A)
+    flag = np.zeros(1, dtype=np.int32)
+    assert lib.pai_debug_engine(ctx.handle, 1, A.ctypes.data, A.ctypes.data, 1, out.ctypes.data, flag.ctypes.data) != 0
+    assert b"test build" in lib.pai_last_error()

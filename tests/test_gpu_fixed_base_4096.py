@@ -126,9 +126,9 @@ def test_fixed_base_4096_memory_cap_falls_back(golden, monkeypatch):
     assert np.array_equal(val, x.astype(np.float64))
 
 
-def test_split_sampler_matches_group_engine(ctx4096, golden, monkeypatch):
-    """k_sgp (kernels_sgp.hpp, split pairs: the default) and k_fbgp (pair groups, FLEXPAI_SGP=0) read the same
-    tables and give the same ciphertexts, ragged size, non-zero index base."""
+def test_split_sampler_matches_group_engine(ctx4096, golden, monkeypatch, xlib):
+    """k_sgp (kernels_sgp.hpp, split pairs: the default) and k_fbgp (pair groups, FLEXPAI_SGP=0 in the test build)
+    read the same tables and give the same ciphertexts, ragged size, non-zero index base."""
     N = _native()
     ctx, key = ctx4096
     rk = bytes(range(40, 72))
@@ -137,7 +137,7 @@ def test_split_sampler_matches_group_engine(ctx4096, golden, monkeypatch):
     ct, ex, _ = ctx.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=2 ** 32 - 3)
     assert ctx.split_sampler & 1
     monkeypatch.setenv("FLEXPAI_SGP", "0")
-    ref = N.Context(key.n, 0, key.p, key.q)
+    ref = N.Context(key.n, 0, key.p, key.q, lib=xlib)
     ref.set_fb_window(12)
     ct2, ex2, _ = ref.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=2 ** 32 - 3)
     assert ref.fb_ready and not ref.split_sampler & 1

@@ -1,6 +1,6 @@
 """The p-adic pair kernels (bn_pair.hpp, bn_pgroup.hpp: k_fbp, k_fbgp, k_crt_b_pair, k_dec_*_pair, k_dec4_*)
-against the kernels they replace, which stay in the library behind $FLEXPAI_FB_PAIR=0 / $FLEXPAI_PAIR=0
-(k_fb, k_fbg, k_crt_b, k_dec_pre/pow/fin, k_decrypt): bit-identical ciphertexts and plaintexts for the
+against the kernels they replace, which live in the test-only build (libflexpai_xcheck.so) behind
+$FLEXPAI_FB_PAIR=0 / $FLEXPAI_PAIR=0 (k_fb, k_fbg, k_crt_b, k_dec_pre/pow/fin, k_decrypt): bit-identical ciphertexts and plaintexts for the
 device-RNG sampler, the generic CRT path (explicit r) and decryption, at every key size."""
 import numpy as np
 import pytest
@@ -20,22 +20,22 @@ def _key(golden, nb):
     return O.Key(int(k["n"], 16), int(k["p"], 16), int(k["q"], 16))
 
 
-def _ctx(monkeypatch, key, pair):
+def _ctx(monkeypatch, key, pair, lib=None):
     N = _native()
     monkeypatch.setenv("FLEXPAI_FB_PAIR", "1" if pair else "0")
     monkeypatch.setenv("FLEXPAI_PAIR", "1" if pair else "0")
-    ctx = N.Context(key.n, 0, key.p, key.q)
+    ctx = N.Context(key.n, 0, key.p, key.q, lib=lib)
     ctx.set_fb_window(12)
     ctx.prepare_fixed_base()
     return ctx
 
 
 @pytest.mark.parametrize("nb", [1024, 2048, 4096])
-def test_pair_kernels_match_the_kernels_they_replace(golden, monkeypatch, nb):
+def test_pair_kernels_match_the_kernels_they_replace(golden, monkeypatch, xlib, nb):
     N = _native()
     key = _key(golden, nb)
     a = _ctx(monkeypatch, key, True)
-    b = _ctx(monkeypatch, key, False)
+    b = _ctx(monkeypatch, key, False, xlib)
     assert a.fb_pair and not b.fb_pair
     assert (a.pair_paths & 1) and not (b.pair_paths & 1)
     n = 300 if nb < 4096 else 96
@@ -105,3 +105,32 @@ def test_unbalanced_key_takes_the_generic_path():
         c, e = O.encrypt_value(x[i], key, r)
         assert got[i] == c and int(ex[i]) == e, f"element {i}"
     assert np.array_equal(ctx.decrypt(ct, ex)[0], x.astype(np.float64))
+
+
+def test_key_outside_pair_bounds_uses_the_general_kernels(xlib):
+    """p, q of 1028 and 1030 bits (n of 2058 bits): R = 2^(28 * 37) is below 2^12 p_h, so no pair kernel applies.
+    The product library then encrypts on the public-key group kernel (k_encrypt) and decrypts on the group engine
+    (k_decrypt) -- its 2S-limb lane kernels live in the test build only -- bit-exact against the oracle and against
+    the test build's 2S-limb CRT / lane path."""
+    N = _native()
+    rng = np.random.default_rng(2058)
+    p, q = _prime(1028, rng), _prime(1030, rng)
+    key = O.Key(p * q, min(p, q), max(p, q))
+    ctx = N.Context(key.n, 0, key.p, key.q)
+    assert not ctx.crt_available and not (ctx.pair_paths & 3) and not ctx.lane_decrypt
+    xc = N.Context(key.n, 0, key.p, key.q, lib=xlib)
+    assert xc.crt_available
+    x = (rng.standard_normal(150) * 1e3).astype(np.float32)
+    rs = [O.golden_r(key.n, 8, i) for i in range(x.size)]
+    ct, ex, _ = ctx.encrypt(x, obf_mode=N.PAI_OBF_GIVEN, r=rs)
+    cx, exx, _ = xc.encrypt(x, obf_mode=N.PAI_OBF_GIVEN, r=rs)
+    assert np.array_equal(ct, cx) and np.array_equal(ex, exx)
+    got = N.words_to_ints(ct)
+    for i in (0, 75, 149):
+        assert got[i] == O.encrypt_value(x[i], key, rs[i])[0], f"element {i}"
+    rk = bytes(range(7, 39))
+    a, ea, _ = ctx.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=3)
+    b, eb, _ = xc.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=3)
+    assert np.array_equal(a, b) and np.array_equal(ea, eb)
+    for d in (ctx.decrypt(a, ea), xc.decrypt(a, ea)):
+        assert np.array_equal(d[0], x.astype(np.float64))

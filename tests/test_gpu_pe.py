@@ -1,7 +1,7 @@
 """GPU parity of the public-key encryption on split pairs (kernels_pe.hpp: k_pe_pre / k_pe_pow / k_pe_fin, the
 path of every party that holds only the public key, 2048-bit n) against the reference golden vectors
 (explicit r: encryptor.py:48-69 with random_value), the CPU oracle (device ChaCha20 obfuscators) and the
-group-engine kernel it replaces (k_encrypt, $FLEXPAI_PAIR=0): bit-identical ciphertexts, exponents, statuses."""
+group-engine kernel it replaces (k_encrypt, $FLEXPAI_PAIR=0 in the test build): bit-identical ciphertexts, exponents, statuses."""
 import numpy as np
 import pytest
 
@@ -22,8 +22,9 @@ def key2048(golden):
 
 
 def _pub(monkeypatch, key, pair):
+    from flex.crypto.paillier import _native as N
     monkeypatch.setenv("FLEXPAI_PAIR", "1" if pair else "0")
-    ctx = _native().Context(key.n, 0)
+    ctx = N.Context(key.n, 0, lib=None if pair else N.load_library(N.XCHECK_LIB_PATH))
     assert bool(ctx.pair_paths & 4) == pair
     return ctx
 

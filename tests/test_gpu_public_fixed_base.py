@@ -150,9 +150,9 @@ def test_public_full_size_roundtrip(drawn):
     assert np.array_equal(half, ct[n // 2:])
 
 
-def test_split_sampler_matches_group_engine(pub, golden_pfb, monkeypatch):
-    """k_sgp (split pairs, the default) and k_pfb (pair groups, FLEXPAI_SGP=0) over the same bases and window:
-    identical ciphertexts."""
+def test_split_sampler_matches_group_engine(pub, golden_pfb, monkeypatch, xlib):
+    """k_sgp (split pairs, the default) and k_pfb (pair groups, FLEXPAI_SGP=0 in the test build) over the same bases
+    and window: identical ciphertexts."""
     N = _native()
     ctx, dec, key, bases = pub
     rk = b"\x5a" * 32
@@ -160,7 +160,7 @@ def test_split_sampler_matches_group_engine(pub, golden_pfb, monkeypatch):
     outs = []
     for sgp in ("1", "0"):
         monkeypatch.setenv("FLEXPAI_SGP", sgp)
-        c = N.Context(key.n, 0)
+        c = N.Context(key.n, 0, lib=None if sgp == "1" else xlib)
         c.set_public_bases(bases)
         c.set_pfb_window(12)
         c.prepare_public_fixed_base()

@@ -332,10 +332,32 @@ def test_c_abi_exports_every_declared_symbol():
     header = open(os.path.join(ROOT, "include", "flexpai.h")).read()
     declared = set(re.findall(r"^\s*(?:int|void|const char\*)\s+(pai_\w+)\s*\(", header, re.M))
     assert declared == set(_native.EXPORTED)        # every entry point is bound, none is undeclared
-    lib = ctypes.CDLL(_native.LIB_PATH)
-    for name in declared:
-        assert hasattr(lib, name), name
+    for path in (_native.LIB_PATH, _native.XCHECK_LIB_PATH):
+        lib = ctypes.CDLL(path)
+        for name in declared:
+            assert hasattr(lib, name), (path, name)
     _native.load_library()
+
+
+# mangled names of the kernel generations the pair kernels replaced, and of k_debug
+LEGACY_KERNELS = (b"_ZN4fpai4k_fbILi", b"_ZN4fpai8k_fb_finILi", b"_ZN4fpai5k_fbgILi", b"_ZN4fpai6k_fbgpILi",
+                  b"_ZN4fpai5k_pfbILi", b"_ZN4fpai9k_dec_preILi", b"_ZN4fpai9k_dec_powILi", b"_ZN4fpai9k_dec_finILi",
+                  b"_ZN4fpai7k_crt_bILi", b"_ZN4fpai7k_debugILi")
+
+
+def test_product_library_carries_no_superseded_kernels():
+    """the superseded kernels (and k_debug) are in the test build only; the product library
+    holds the shipping kernels (k_fbp, k_fbs, k_sgp, ...) and none of them."""
+    from flex.crypto.paillier import _native
+    if not os.path.exists(_native.LIB_PATH) or not os.path.exists(_native.XCHECK_LIB_PATH):
+        pytest.skip("libraries not built (run __graft_entry__.build())")
+    prod = open(_native.LIB_PATH, "rb").read()
+    xck = open(_native.XCHECK_LIB_PATH, "rb").read()
+    for k in LEGACY_KERNELS:
+        assert k not in prod, k
+        assert k in xck, k
+    for k in (b"_ZN4fpai5k_fbpILi", b"_ZN4fpai5k_fbsILi", b"_ZN4fpai5k_sgp", b"_ZN4fpai14k_dec_pow_pairILi"):
+        assert k in prod, k
 
 
 def test_product_path_has_no_oracle_or_cpu_fallback():

@@ -1,6 +1,12 @@
 #!/bin/bash
-# GPU check: the -m gpu suite (or TESTS="tests/test_x.py ..."; one process, per-test time limit), then one bench
-# line (BENCH_ARGS; NO_BENCH=1 skips it). Logs under gpurun_out/ (TAG prefixes their names).
+# The one GPU-iteration script (run through gpurun from the repo root). Steps, each under its own time limit and
+# chained so that the first failure ends the call; logs under gpurun_out/, names prefixed with TAG:
+#   1. the -m gpu parity tests (TESTS="tests/test_x.py ..." for a subset; NO_TESTS=1 skips), one process;
+#   2. one bench line (BENCH_ARGS; NO_BENCH=1 skips);
+#   3. PROF=1: a rocprofv3 --kernel-trace --stats profile of bench.py $PROF_ARGS (summary: ${TAG}_prof/run_kernel_stats.csv);
+#   4. PMC="FETCH_SIZE WRITE_SIZE ...": one rocprofv3 --pmc pass per counter set (sets separated by ';'), each with
+#      --kernel-trace only (MI355X_MICROARCH.md's HBM section: separate passes), over bench.py $PMC_ARGS.
+# Any other environment (FLEXPAI_FBS=1, FLEXPAI_FB_WINDOW=...) is exported by the caller and reaches every step.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out
@@ -13,7 +19,24 @@ if [ -z "$NO_TESTS" ]; then
   tail -5 $O/${T}_pytest_gpu.log
   [ $rc -ne 0 ] && { echo "pytest failed rc=$rc"; grep -E "FAILED|Error|error" $O/${T}_pytest_gpu.log | head -20; exit 1; }
 fi
-[ -n "$NO_BENCH" ] && { echo ALLDONE; exit 0; }
-timeout -k 10 ${BENCH_TIMEOUT:-600} python -u bench.py ${BENCH_ARGS:-} > $O/${T}_bench.log 2>&1 || { echo "bench failed rc=$?"; tail -30 $O/${T}_bench.log; exit 1; }
-tail -1 $O/${T}_bench.log | cut -c1-800
+if [ -z "$NO_BENCH" ]; then
+  timeout -k 10 ${BENCH_TIMEOUT:-600} python -u bench.py ${BENCH_ARGS:-} > $O/${T}_bench.log 2>&1 || { echo "bench failed rc=$?"; tail -30 $O/${T}_bench.log; exit 1; }
+  tail -1 $O/${T}_bench.log | cut -c1-800
+fi
+PA=${PROF_ARGS:---steps 5 --warmup 2 --no-cpu-baseline --no-host --no-public --no-add8 --no-strong --no-contention}
+if [ -n "$PROF" ]; then
+  timeout -k 10 ${PROF_TIMEOUT:-400} rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_prof -o run -- python3 bench.py $PA > $O/${T}_prof.log 2>&1 || { echo "prof failed rc=$?"; tail -20 $O/${T}_prof.log; exit 1; }
+  tail -1 $O/${T}_prof.log | cut -c1-400
+  head -12 $O/${T}_prof/run_kernel_stats.csv | cut -c1-160
+fi
+if [ -n "$PMC" ]; then
+  MA=${PMC_ARGS:---steps 1 --warmup 0 --no-cpu-baseline --no-decrypt --no-host --no-public --no-add8 --no-strong --no-contention}
+  i=0
+  IFS=';' read -ra SETS <<< "$PMC"
+  for set in "${SETS[@]}"; do
+    i=$((i+1))
+    timeout -s KILL ${PMC_TIMEOUT:-180} rocprofv3 --pmc $set --kernel-trace --output-format csv -d $O/${T}_pmc$i -o run -- python3 bench.py $MA > $O/${T}_pmc$i.log 2>&1 || { echo "pmc pass $i ($set) failed rc=$?"; tail -20 $O/${T}_pmc$i.log; exit 1; }
+    echo "pmc pass $i: $set"
+  done
+fi
 echo ALLDONE

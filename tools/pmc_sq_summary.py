@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 SQ counter CSVs (tools/gpu/r02_pmc_sq.sh) per kernel: issued VALU instructions,
+"""Summarise rocprofv3 SQ counter CSVs (tools/gpu/pmc_sq.sh) per kernel: issued VALU instructions,
 wave cycles, the fraction of wave cycles with an instruction issued / waiting, and VALU instructions per
 canonical MAC of the kernel when its work is known (bench.py's counts).
 

@@ -118,6 +118,15 @@ def work_fbp(nb: int, digits: int) -> dict:
     return {"k_fb_digits": 0.0, "k_fbp": float(2 * (digits * _Mf(s) + s * s + _M(s))), "k_fbp_fin": float(15 * s * s)}
 
 
+def work_fbs(nb: int, digits: int) -> dict:
+    """The pair fixed-base path on Shoup rows (kernels_fbs.hpp): k_fbs = K Shoup products per half (s = nb/64 limbs of
+    p_h; per component a quotient from the top s (s + 1) / 2 columns of X a' and the low s (s + 1) / 2 columns of X a
+    and of Q p: 3 s^2 + 3 s per pair) + the c0 chunk sum (s^2) + the b-sum correction (M(s)); k_fbp_fin as work_fbp."""
+    s = nb // 64
+    return {"k_fb_digits": 0.0, "k_fbs": float(2 * (digits * (3 * s * s + 3 * s) + s * s + _M(s))),
+            "k_fbp_fin": float(15 * s * s)}
+
+
 def work_fbg(nb: int, digits: int) -> dict:
     """Per-element MACs of the 4096-bit key holder's fixed-base path (kernels_grp.hpp), counted like work_fb:
     k_fbg = K table products mod p_h^2 per half (c0 folded into the first); Garner = one product mod p^2
@@ -421,6 +430,7 @@ def main():
     fb_info = None
     fb_pair = 0
     fb_split = False
+    fb_shoup = False
     if use_fb:
         ctx.set_fb_window(args.fb_window)     # a dedicated encrypt GPU: the largest tables that fit its HBM
         t0 = time.perf_counter()
@@ -432,6 +442,7 @@ def main():
         use_fb = ctx.fb_ready
         fb_pair = ctx.fb_pair if use_fb else 0
         fb_split = bool(ctx.split_sampler & 1) if use_fb else False   # k_sgp (kernels_sgp.hpp) for k_fbgp
+        fb_shoup = bool(ctx.split_sampler & 4) if use_fb else False   # k_fbs (kernels_fbs.hpp) for k_fbp
         if use_fb:
             fb_info = ctx.fixed_base_info()
             h_ms, d_ms, tbytes = ctx.fixed_base_setup()
@@ -1078,6 +1089,8 @@ def main():
                 works["k_sgp"] = works.pop("k_fbgp")
         elif grp_fb:
             names, works = ["k_fb_digits", "k_fbg", "k_fbg_fin"], work_fbg(nb, fb_info[2])
+        elif use_crt and use_fb and fb_pair and fb_shoup:
+            names, works = ["k_fb_digits", "k_fbs", "k_fbp_fin"], work_fbs(nb, fb_info[2])
         elif use_crt and use_fb and fb_pair:
             names, works = ["k_fb_digits", "k_fbp", "k_fbp_fin"], work_fbp(nb, fb_info[2])
         elif use_crt and use_fb:
@@ -1094,7 +1107,8 @@ def main():
         extra["stages"] = stages
         achieved = N * dom_work / (dom_ms * 1e-3)
         enc_ms = float(sum(stage_avg))
-        extra["path"] = ("crt-fixedbase-pair" if fb_pair else "crt-fixedbase") if use_fb else "crt" if use_crt else "public"
+        extra["path"] = (("crt-fixedbase-shoup" if fb_shoup else "crt-fixedbase-pair") if fb_pair else "crt-fixedbase") \
+            if use_fb else "crt" if use_crt else "public"
         if use_fb:
             extra["fixed_base"] = {"g_p": fb_info[0], "g_q": fb_info[1], "digits": fb_info[2], "window_bits": fb_info[3]}
         extra["encrypt_call_ms"] = enc_ms
@@ -1215,7 +1229,11 @@ def main():
                      "unit": "TMAC/s", "frac": achieved / INT_MAC_PEAK,
                      "traffic": load_traffic(dom, N, nb, fb_info[3] if (use_fb and dom in ("k_fb", "k_fbp", "k_fbg", "k_fbgp", "k_sgp")) else None),
                      "kernel": dom, "kernel_ms": dom_ms,
-                     "work_per_unit": (f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} products by "
+                     "work_per_unit": (f"{dom_work:.4g} MAC per element: the Shoup-row count (K = {fb_info[2]} Shoup products "
+                                       f"mod p_h^2 per half, 3 s^2 + 3 s each over s = nb/64 32-bit limbs of p_h, + the c0 sum "
+                                       f"and the b-sum correction, kernels_fbs.hpp), not SURVEY.md §8d's W_enc"
+                                       if dom == "k_fbs" else
+                                       f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} products by "
                                        f"factored rows (a, 0) mod p_h^2 per half, 4 s^2 + 2 s each over s = nb/64 32-bit limbs "
                                        f"of p_h, + the c0 sum and the b-sum correction, "
                                        f"{'kernels_fbp.hpp' if dom == 'k_fbp' else 'kernels_sgp.hpp' if dom == 'k_sgp' else 'kernels_grp_pair.hpp'}), not SURVEY.md §8d's W_enc"

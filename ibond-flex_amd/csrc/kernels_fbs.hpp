@@ -3,17 +3,19 @@
 // canonical pairs out, so k_fbp_fin recombines them unchanged and the ciphertexts are bit-identical to k_fbp's.
 //
 // Rows. A table entry T = T_k[d] mod p_h^2 (PLAIN, not Montgomery form) is stored factored as T = a (1 + p_h b),
-// a = T mod p_h, together with Shoup's quotient a' = floor(a R / p_h), R = 2^(28 S) (PWA words): the words of a
-// (PW), of a' (PWA, padded to quads), then of b R mod p_h (PW) -- 400 B per row at nb = 2048 (25 quads). The a
-// and a' quads stream into LDS by DMA one digit ahead, the b R quads into registers (summed into bs at once).
+// a = T mod p_h, together with Shoup's quotient a' = floor(a R / p_h) < R, R = 2^(28 S): the S 28-bit limbs of a
+// (one per 32-bit word, QA quads), the S limbs of a' (QAP quads), then the PW 32-bit words of b R mod p_h (QB quads)
+// -- 448 B per row at nb = 2048 (28 quads). Limbs, not packed words, so that a digit is a register of the quad that
+// holds it (no shift or align per digit). The a and a' quads stream into LDS by DMA one product ahead, the b R quads
+// into registers (summed into bs at once).
 //
 // Product of the running pair (A, B), V = A + p B (mod p^2), by a (tools/shoup_model.py checks every bound):
 //   V a = A a + p B a = r_A + p (Q_A + B a),   A a = r_A + Q_A p
 // and for each component X in {A, B} two steps:
 //   step 1: Q = floor(X a' / R) from the columns >= S - 1 of X a' only: S (S + 1) / 2 MACs, Q at most S + 1
 //           below the exact floor (the dropped columns are worth < S R);
-//   step 2: X' = init + X a - Q p from the columns 0 .. S - 1 (signed 64-bit accumulators: + X_i a_j and
-//           + (-Q_i) p_j), exact because the true value lies in [0, R): S (S + 1) MACs.
+//   step 2: X' = init + X a - Q p from the columns 0 .. S - 1, as init + X a + Q (R - p) mod R (unsigned 64-bit
+//           accumulators): S (S + 1) MACs, exact because the true value lies in [0, R).
 // Shoup's bound A a / p - A a' / R in [0, A / R) keeps A < (S + 3) p and B < 2 (S + 3) p, far below R.
 // 3 S^2 + 3 S MACs per product against 4 S^2 for the Montgomery pass pair (and no q_j multiplications).
 // After the K products the b sum is applied once (fbp_apply_bsum), then the pair is reduced to canonical.
@@ -26,73 +28,16 @@ template <int S>
 struct FbsGeom;
 template <>
 struct FbsGeom<19> {   // 1024-bit keys: p_h < 2^512, R = 2^532
-  static constexpr int PW = 16, PWA = 17, QA = 4, QAP = 5, QB = 4;
+  static constexpr int PW = 16, QA = 5, QAP = 5, QB = 4;
 };
 template <>
 struct FbsGeom<37> {   // 2048-bit keys: p_h < 2^1024, R = 2^1036
-  static constexpr int PW = 32, PWA = 33, QA = 8, QAP = 9, QB = 8;
+  static constexpr int PW = 32, QA = 10, QAP = 10, QB = 8;
 };
-// row quads: a [0, QA), a' [QA, QA + QAP), b R [QA + QAP, QA + QAP + QB)
 template <int S>
 constexpr int fbs_row_quads() { return FbsGeom<S>::QA + FbsGeom<S>::QAP + FbsGeom<S>::QB; }
 template <int S>
 constexpr int fbs_lds_quads() { return FbsGeom<S>::QA + FbsGeom<S>::QAP; }
-
-template <int C>
-__device__ __forceinline__ uint32_t fb_quad_word(const uint4& v) {
-  if constexpr (C == 0) return v.x;
-  else if constexpr (C == 1) return v.y;
-  else if constexpr (C == 2) return v.z;
-  else return v.w;
-}
-template <int OFF>
-__device__ __forceinline__ void lds_quad_wr(uint32_t addr, const fbp_u32x4& v) {
-  if constexpr (OFF < 65536) asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "v"(v), "i"(OFF) : "memory");
-  else asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr + 65536u), "v"(v), "i"(OFF - 65536) : "memory");
-}
-
-// Digits J of a number held as NQ quads at quad Q0 of this lane's LDS row ([quad][lane] layout), consumed in
-// the order J = S-1 .. 0 (DESC) or 0 .. S-1. Quads are read DQ quads ahead of the first digit that needs them,
-// in consumption order, and every wait names the exact count of reads issued after the ones it needs (the only
-// LDS operations in flight in a step are these reads).
-template <int S, int NQ, int Q0, bool DESC, int DQ>
-struct FbsReader {
-  uint32_t addr;
-  fbp_u32x4 q[NQ];
-  static constexpr int dig(int t) { return DESC ? S - 1 - t : t; }
-  static constexpr int wlo(int J) { return (28 * J) >> 5; }
-  static constexpr int whi(int J) { return (28 * J + 27) >> 5 < 4 * NQ - 1 ? (28 * J + 27) >> 5 : 4 * NQ - 1; }
-  static constexpr int rank(int qd) { return DESC ? NQ - 1 - qd : qd; }   // issue position of quad qd
-  static constexpr int quad_at(int r) { return DESC ? NQ - 1 - r : r; }
-  static constexpr int cmax(int a, int b) { return a > b ? a : b; }
-  static constexpr int need(int t) {   // highest issue position needed by the digits of steps 0 .. t
-    int m = -1;
-    for (int u = 0; u <= t; ++u) m = cmax(m, cmax(rank(wlo(dig(u)) / 4), rank(whi(dig(u)) / 4)));
-    return m;
-  }
-  static constexpr int issued(int t) { return t < 0 ? -1 : (need(t) + DQ < NQ - 1 ? need(t) + DQ : NQ - 1); }
-  template <int R0, int... Rs>
-  __device__ __forceinline__ void issue(std::integer_sequence<int, Rs...>) {
-    ((q[quad_at(R0 + Rs)] = lds_quad_rd<(Q0 + quad_at(R0 + Rs)) * LANE_BLOCK * 16>(addr)), ...);
-  }
-  template <int T>
-  __device__ __forceinline__ uint32_t operator()(std::integral_constant<int, T>) {
-    constexpr int from = issued(T - 1) + 1, to = issued(T);
-    issue<from>(std::make_integer_sequence<int, (to >= from ? to - from + 1 : 0)>{});
-    constexpr int J = dig(T), l = wlo(J), h = whi(J), gl = l / 4, gh = h / 4;
-    if constexpr (T == 0 || need(T) > need(T - 1)) {
-      constexpr int pending = to - need(T);
-      static_assert(pending >= 0 && pending <= 15, "lgkmcnt range");
-      if constexpr (gl == gh) asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(q[gl]) : "i"(pending));
-      else asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(q[gl]), "+v"(q[gh]) : "i"(pending));
-    }
-    constexpr int sh = (28 * J) & 31;
-    const uint32_t wl = quad_word<l % 4>(q[gl]);
-    if constexpr (sh + 28 <= 32) return (wl >> sh) & lane::LMASK;
-    else if constexpr (l + 1 < 4 * NQ) return __builtin_amdgcn_alignbit(quad_word<(l + 1) % 4>(q[(l + 1) / 4]), wl, sh) & lane::LMASK;
-    else return wl >> sh;   // past the stored words: zero bits
-  }
-};
 
 // step 1, digit J of a' (columns >= S - 1): P[k - (S - 1)] for k = i + J >= S - 1
 template <int S, int T, class Rd>
@@ -109,9 +54,9 @@ template <int S, class Rd, int... Ts>
 __device__ __forceinline__ void fbs_q_all(uint64_t (&P)[S + 1], const uint32_t (&X)[S], Rd& rd, std::integer_sequence<int, Ts...>) {
   (fbs_q_digit<S, Ts>(P, X, rd), ...);
 }
-// -Q: the negated limbs of floor(X a' / R) (truncated, above); rd yields the digits of a', J = S-1 .. 0
+// Q: the limbs of floor(X a' / R) (truncated, above); rd yields the digits of a', J = S-1 .. 0
 template <int S, class Rd>
-__device__ __forceinline__ void fbs_quotient(const uint32_t (&X)[S], Rd& rd, int32_t (&nq)[S]) {
+__device__ __forceinline__ void fbs_quotient(const uint32_t (&X)[S], Rd& rd, uint32_t (&q)[S]) {
   uint64_t P[S + 1];
 #pragma unroll
   for (int i = 0; i <= S; ++i) P[i] = 0;
@@ -120,181 +65,100 @@ __device__ __forceinline__ void fbs_quotient(const uint32_t (&X)[S], Rd& rd, int
 #pragma unroll
   for (int i = 1; i <= S; ++i) {
     const uint64_t v = P[i] + c;
-    nq[i - 1] = -(int32_t)lane::limb32(v);
+    q[i - 1] = lane::limb32(v);
     c = v >> lane::LB;
   }
 }
 
-// Digits J = 0 .. S-1 of a, read from the row in global memory (a is not in LDS), NQ quads, two quads ahead of the
-// digit that first needs them. The loads are inline asm, so that they stay where they are issued (left to the
-// compiler, all NQ quads were hoisted to the start and kept live, 32 VGPRs), with exact vmcnt waits: in a step 2
-// the only vector-memory operations in flight are these loads and, from digit XD on, the XN operations the caller's
-// hook issues there (the next row's). Quads 0 and 1 are loaded by the caller (EXT: already waited for) or by
-// start() (issue order = quad order either way).
-template <int OFF>
-__device__ __forceinline__ fbp_u32x4 fbs_gload(const uint4* base) {
-  fbp_u32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(v) : "v"(base), "i"(OFF) : "memory");
-  return v;
-}
-struct FbsNoHook {
-  template <int J>
-  __device__ __forceinline__ void operator()(std::integral_constant<int, J>) {}
-};
-template <int S, int NQ, int Q0, bool DESC, bool EXT, int XN, class Hook>
-struct FbsGlobalReader {
-  const uint4* row;
-  Hook hook;
-  fbp_u32x4 q[NQ];
-  static constexpr int dig(int t) { return DESC ? S - 1 - t : t; }
-  static constexpr int wlo(int J) { return (28 * J) >> 5; }
-  static constexpr int whi(int J) { return (28 * J + 27) >> 5 < 4 * NQ - 1 ? (28 * J + 27) >> 5 : 4 * NQ - 1; }
-  static constexpr int rank(int qd) { return DESC ? NQ - 1 - qd : qd; }   // issue position of quad qd
-  static constexpr int quad_at(int r) { return DESC ? NQ - 1 - r : r; }
-  static constexpr int cmax(int a, int b) { return a > b ? a : b; }
-  static constexpr int need(int t) {   // highest issue position needed by steps 0 .. t
-    int m = -1;
-    for (int u = 0; u <= t; ++u) m = cmax(m, cmax(rank(wlo(dig(u)) / 4), rank(whi(dig(u)) / 4)));
-    return m;
-  }
-  static constexpr int top(int t) { return need(t) + 2 < NQ - 1 ? need(t) + 2 : NQ - 1; }   // positions issued by step t
-  static constexpr int xd() {   // the step that issues the last quad: the hook runs there
-    int t = 0;
-    while (top(t) < NQ - 1) ++t;
-    return t;
-  }
-  // positions 0 and 1 (EXT: loaded and waited for by the caller)
-  __device__ __forceinline__ void start() {
-    q[quad_at(0)] = fbs_gload<(Q0 + quad_at(0)) * 16>(row);
-    q[quad_at(1)] = fbs_gload<(Q0 + quad_at(1)) * 16>(row);
-  }
-  template <int R0, int... Rs>
-  __device__ __forceinline__ void issue(std::integer_sequence<int, Rs...>) {
-    ((q[quad_at(R0 + Rs)] = fbs_gload<(Q0 + quad_at(R0 + Rs)) * 16>(row)), ...);
-  }
-  template <int T>
-  __device__ __forceinline__ uint32_t operator()(std::integral_constant<int, T>) {
-    constexpr int from = T == 0 ? 2 : top(T - 1) + 1, to = top(T);
-    issue<from>(std::make_integer_sequence<int, (to >= from ? to - from + 1 : 0)>{});
-    if constexpr (T == xd()) hook(std::integral_constant<int, T>{});
-    constexpr int J = dig(T), l = wlo(J), gl = l / 4, gh = whi(J) / 4;
-    constexpr bool fresh = T == 0 || need(T) > need(T - 1);
-    if constexpr (fresh && (!EXT || need(T) >= 2)) {
-      constexpr int pending = to - need(T) + (T >= xd() ? XN : 0);
-      static_assert(pending >= 0 && pending <= 63, "vmcnt range");
-      if constexpr (gl == gh) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(q[gh]) : "i"(pending));
-      else asm volatile("s_waitcnt vmcnt(%2)" : "+v"(q[gl]), "+v"(q[gh]) : "i"(pending));
-    }
-    constexpr int sh = (28 * J) & 31;
-    const uint32_t wl = quad_word<l % 4>(q[gl]);
-    if constexpr (sh + 28 <= 32) return (wl >> sh) & lane::LMASK;
-    else if constexpr (l + 1 < 4 * NQ) return __builtin_amdgcn_alignbit(quad_word<(l + 1) % 4>(q[(l + 1) / 4]), wl, sh) & lane::LMASK;
-    else return wl >> sh;
-  }
-};
-template <int S>
-using FbsAReader = FbsGlobalReader<S, FbsGeom<S>::QAP, FbsGeom<S>::QA, true, true, 0, FbsNoHook>;     // A1: a' (8, 7 given)
-template <int S>
-using FbsBReader = FbsGlobalReader<S, FbsGeom<S>::QAP, FbsGeom<S>::QA, true, false, 0, FbsNoHook>;    // B1: a'
-template <int S>
-using FbsA2Reader = FbsGlobalReader<S, FbsGeom<S>::QA, 0, false, true, 0, FbsNoHook>;                  // A2: a (0, 1 given)
-
-// step 2, digit J of a: P[i + J] += X_i a_J - Q_i p_J for i + J < S
+// step 2, digit J of a: P[i + J] += X_i a_J + Q_i pbar_J for i + J < S, pbar = R - p (limbs 2^28 - p_0, then
+// 2^28 - 1 - p_j): X a + Q (R - p) = X a - Q p mod R, all unsigned (v_mad_u64_u32 only; columns < 2 S 2^56 < 2^64)
 template <int S, int J, class Rd>
-__device__ __forceinline__ void fbs_r_digit(int64_t (&P)[S], const uint32_t (&X)[S], const int32_t (&nq)[S],
+__device__ __forceinline__ void fbs_r_digit(uint64_t (&P)[S], const uint32_t (&X)[S], const uint32_t (&q)[S],
                                             const uint32_t (&m)[S], Rd& rd) {
   const uint32_t d = rd(std::integral_constant<int, J>{});
-  const int32_t mj = (int32_t)m[J];
+  const uint32_t pb = J == 0 ? (lane::LMASK + 1u) - m[0] : lane::LMASK - m[J];
 #pragma unroll
   for (int i = 0; i + J < S; ++i) {
-    P[i + J] = (int64_t)((uint64_t)P[i + J] + (uint64_t)X[i] * d);
-    P[i + J] += (int64_t)nq[i] * mj;
+    P[i + J] += (uint64_t)X[i] * d;
+    P[i + J] += (uint64_t)q[i] * pb;
   }
 #pragma unroll
   for (int i = J; i < S; ++i) asm volatile("" : "+v"(P[i]));
   __builtin_amdgcn_sched_barrier(0);
 }
 template <int S, class Rd, int... Js>
-__device__ __forceinline__ void fbs_r_all(int64_t (&P)[S], const uint32_t (&X)[S], const int32_t (&nq)[S], const uint32_t (&m)[S],
+__device__ __forceinline__ void fbs_r_all(uint64_t (&P)[S], const uint32_t (&X)[S], const uint32_t (&q)[S], const uint32_t (&m)[S],
                                           Rd& rd, std::integer_sequence<int, Js...>) {
-  (fbs_r_digit<S, Js>(P, X, nq, m, rd), ...);
-}
-// X <- init + X a - Q p (exact, in [0, R)); INIT: the magnitudes of the negated limbs in ni are added first (a
-// compile-time choice: a pointer here made the array a stack object in scratch memory)
-template <int S, bool INIT, class Rd>
-__device__ __forceinline__ void fbs_remainder(uint32_t (&X)[S], const int32_t (&nq)[S], const uint32_t (&m)[S], Rd& rd,
-                                              const int32_t (&ni)[S]) {
-  int64_t P[S];
-#pragma unroll
-  for (int i = 0; i < S; ++i) P[i] = INIT ? (int64_t)(-ni[i]) : 0;
-  fbs_r_all<S>(P, X, nq, m, rd, std::make_integer_sequence<int, S>{});
-  int64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < S; ++i) {
-    const int64_t v = P[i] + c;
-    X[i] = lane::limb32((uint64_t)v);
-    c = v >> lane::LB;   // arithmetic: the low part of a signed sum
-  }
+  (fbs_r_digit<S, Js>(P, X, q, m, rd), ...);
 }
 
-// x <- x - 2^e m while x >= 2^e m, e = E .. 0 (x < 2^(E+1) m on entry -> x < m), counting the multiples into t;
-// 2^e m is formed from m in the loop (one shift per limb), not held
-template <int S, int E>
-__device__ __forceinline__ void fbs_reduce(uint32_t (&x)[S], const uint32_t (&m)[S], uint32_t& t) {
-#pragma unroll 1
-  for (int e = E; e >= 0; --e) {
-    int32_t c = 0;
-    uint32_t d[S];
-    uint32_t sc = 0;
+// x <- x mod m for x < 2^7 m, counting the multiples into t: the quotient estimated from the top two limbs
+// (fb_shoup_possible: m > 2^(28 (S - 1)), so the estimate's error is far below one), subtracted in one signed pass,
+// then at most two conditional subtractions (in place of 6-7 shift-and-subtract passes).
+template <int S>
+__device__ __forceinline__ void fbs_reduce_est(uint32_t (&x)[S], const uint32_t (&m)[S], uint32_t& t) {
+  const double xt = (double)x[S - 1] * 268435456.0 + (double)x[S - 2];
+  const double mt = (double)m[S - 1] * 268435456.0 + (double)m[S - 2] + 1.0;
+  const double qe = xt / mt - 1.0 / 1048576.0;
+  const int32_t q = qe > 0.0 ? (int32_t)qe : 0;   // floor(x / m) - 1 <= q <= floor(x / m)
+  {
+    int64_t c = 0;
+    const int32_t nq = -q;
 #pragma unroll
     for (int i = 0; i < S; ++i) {
-      const uint64_t me = ((uint64_t)m[i] << e) + sc;
-      sc = (uint32_t)(me >> lane::LB);
-      const int32_t v = (int32_t)x[i] - (int32_t)((uint32_t)me & lane::LMASK) + c;
+      const int64_t v = (int64_t)x[i] + (int64_t)nq * (int32_t)m[i] + c;
+      x[i] = (uint32_t)v & lane::LMASK;
+      c = v >> lane::LB;
+    }
+  }
+  t += (uint32_t)q;
+#pragma unroll 1
+  for (int r = 0; r < 2; ++r) {
+    int32_t c = 0;
+    uint32_t d[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      const int32_t v = (int32_t)x[i] - (int32_t)m[i] + c;
       d[i] = (uint32_t)v & lane::LMASK;
       c = v >> lane::LB;
     }
     const bool lt = c != 0;
 #pragma unroll
     for (int i = 0; i < S; ++i) x[i] = lt ? x[i] : d[i];
-    t += lt ? 0u : (1u << e);
+    t += lt ? 0u : 1u;
   }
 }
 
 // ---------------------------------------------------------------- the sampler on split pairs
 // Element-half e on lanes 2e, 2e+1 (kernels_sgp.hpp's layout): the even lane keeps A, the odd lane B, and both run
 // the same Shoup pass on their own component at once -- step 1 (their quotient), then step 2, the odd lane's
-// accumulator starting at the even lane's Q_A (one DPP per limb). Per lane: the component, -Q and one accumulator
+// accumulator starting at the even lane's Q_A (one DPP per limb). Per lane: the component, Q and one accumulator
 // row (148 VGPRs in step 2) and half of the b sum (16 words + a carry).
 //
 // Rows in LDS, double-buffered (product k reads buffer k & 1 while row k+1 streams into the other): DMA instruction
 // g of a wave fetches quad 2g + t of pair p's row on lane 2p + t, landing at [g][lane] (1 KB per instruction), so
 // quad Q of the pair's row sits at (Q / 2) KB + (Q & 1) 16 B from the pair's base: both lanes of a pair read the same
-// addresses (a broadcast), consecutive pairs consecutive 32 B. The b R quads go to registers (4 per lane).
+// addresses (a broadcast), consecutive pairs consecutive 32 B. The b R quads go to registers (QB / 2 per lane).
+// At S = 37: 10 DMA instructions, 2 x 10 KB per wave, 80 KB per block -- two blocks fill the CU's 160 KB.
 template <int S>
-constexpr int fbs_dma_insts() { return (FbsGeom<S>::QA + FbsGeom<S>::QAP + 1) / 2; }   // 9 at S = 37
+constexpr int fbs_dma_insts() { return (FbsGeom<S>::QA + FbsGeom<S>::QAP + 1) / 2; }
 template <int S>
 constexpr int fbs_wave_buf_bytes() { return fbs_dma_insts<S>() * 1024; }
 template <int Q>
 constexpr int fbs_pair_off() { return (Q >> 1) * 1024 + (Q & 1) * 16; }
 
-// digits of a' (quads QA .. QA+QAP-1 of the row, consumed J = S-1 .. 0) or of a (quads 0 .. QA-1, J = 0 .. S-1) from
-// the pair's row in LDS; reads DQ quads ahead in consumption order, exact lgkmcnt waits (only these reads in flight)
+// limbs of a' (quads QA .. QA+QAP-1 of the row, consumed J = S-1 .. 0) or of a (quads 0 .. QA-1, J = 0 .. S-1) from
+// the pair's row in LDS: limb J is word J % 4 of quad J / 4. Quads are read DQ ahead in consumption order, with exact
+// lgkmcnt waits (only these reads are in flight: the row DMA and the digit loads count in vmcnt).
 template <int S, int NQ, int Q0, bool DESC, int DQ>
 struct FbsPairReader {
+  static_assert(4 * NQ >= S, "limbs per number");
   uint32_t addr;
   fbp_u32x4 q[NQ];
   static constexpr int dig(int t) { return DESC ? S - 1 - t : t; }
-  static constexpr int wlo(int J) { return (28 * J) >> 5; }
-  static constexpr int whi(int J) { return (28 * J + 27) >> 5 < 4 * NQ - 1 ? (28 * J + 27) >> 5 : 4 * NQ - 1; }
   static constexpr int rank(int qd) { return DESC ? NQ - 1 - qd : qd; }
   static constexpr int quad_at(int r) { return DESC ? NQ - 1 - r : r; }
-  static constexpr int cmax(int a, int b) { return a > b ? a : b; }
-  static constexpr int need(int t) {
-    int m = -1;
-    for (int u = 0; u <= t; ++u) m = cmax(m, cmax(rank(wlo(dig(u)) / 4), rank(whi(dig(u)) / 4)));
-    return m;
-  }
+  static constexpr int need(int t) { return rank(dig(t) / 4); }   // monotone in t
   static constexpr int issued(int t) { return t < 0 ? -1 : (need(t) + DQ < NQ - 1 ? need(t) + DQ : NQ - 1); }
   template <int R0, int... Rs>
   __device__ __forceinline__ void issue(std::integer_sequence<int, Rs...>) {
@@ -304,18 +168,13 @@ struct FbsPairReader {
   __device__ __forceinline__ uint32_t operator()(std::integral_constant<int, T>) {
     constexpr int from = issued(T - 1) + 1, to = issued(T);
     issue<from>(std::make_integer_sequence<int, (to >= from ? to - from + 1 : 0)>{});
-    constexpr int J = dig(T), l = wlo(J), h = whi(J), gl = l / 4, gh = h / 4;
+    constexpr int J = dig(T), g = J / 4;
     if constexpr (T == 0 || need(T) > need(T - 1)) {
       constexpr int pending = to - need(T);
       static_assert(pending >= 0 && pending <= 15, "lgkmcnt range");
-      if constexpr (gl == gh) asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(q[gl]) : "i"(pending));
-      else asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(q[gl]), "+v"(q[gh]) : "i"(pending));
+      asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(q[g]) : "i"(pending));
     }
-    constexpr int sh = (28 * J) & 31;
-    const uint32_t wl = quad_word<l % 4>(q[gl]);
-    if constexpr (sh + 28 <= 32) return (wl >> sh) & lane::LMASK;
-    else if constexpr (l + 1 < 4 * NQ) return __builtin_amdgcn_alignbit(quad_word<(l + 1) % 4>(q[(l + 1) / 4]), wl, sh) & lane::LMASK;
-    else return wl >> sh;
+    return quad_word<J % 4>(q[g]);
   }
 };
 
@@ -412,25 +271,25 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbs(FbpParams p) {
         for (int q = 0; q < G::QB / 2; ++q) bv[q] = fbp_u32x4{0u, 0u, 0u, 0u};
       }
       __builtin_amdgcn_sched_barrier(0);
-      int32_t nq[S];
+      uint32_t q[S];
       {
         FbsPairReader<S, G::QAP, G::QA, true, 1> r1{cur};
-        fbs_quotient<S>(X, r1, nq);
+        fbs_quotient<S>(X, r1, q);
       }
       {   // step 2; the odd lane's accumulator starts at the even lane's Q_A
-        int64_t P[S];
+        uint64_t P[S];
 #pragma unroll
         for (int i = 0; i < S; ++i) {
-          const int32_t qa = __builtin_amdgcn_update_dpp(0, nq[i], 0xA0, 0xF, 0xF, false);   // quad_perm [0,0,2,2]
-          P[i] = odd ? (int64_t)(-qa) : 0;
+          const uint32_t qa = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q[i], 0xA0, 0xF, 0xF, false);   // quad_perm [0,0,2,2]
+          P[i] = odd ? (uint64_t)qa : 0ull;
         }
         FbsPairReader<S, G::QA, 0, false, 1> r2{cur};
-        fbs_r_all<S>(P, X, nq, m, r2, std::make_integer_sequence<int, S>{});
-        int64_t c = 0;
+        fbs_r_all<S>(P, X, q, m, r2, std::make_integer_sequence<int, S>{});
+        uint64_t c = 0;   // (mod R: the carry out of limb S - 1 is dropped)
 #pragma unroll
         for (int i = 0; i < S; ++i) {
-          const int64_t v = P[i] + c;
-          X[i] = lane::limb32((uint64_t)v);
+          const uint64_t v = P[i] + c;
+          X[i] = lane::limb32(v);
           c = v >> lane::LB;
         }
       }
@@ -454,7 +313,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbs(FbpParams p) {
     }
     if (!odd && valid) {
       uint32_t t = 0;
-      fbs_reduce<S, 5>(X, m, t);                          // (S + 3) p < 64 p
+      fbs_reduce_est<S>(X, m, t);                         // (S + 3) p < 2^7 p
       {
         uint32_t c = t;
 #pragma unroll
@@ -466,7 +325,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbs(FbpParams p) {
       }
       fbp_apply_bsum<S, PW>(X, B, bs, bc, m, mprime);     // B + REDC(A bs R) < 2 (S + 3) p + 64 + 2 p < 128 p
       uint32_t tb = 0;
-      fbs_reduce<S, 6>(B, m, tb);
+      fbs_reduce_est<S>(B, m, tb);
       uint32_t* o = p.out + fbp_pair_index<S>(e, half, p.n);
 #pragma unroll
       for (int j = 0; j < 2 * S; ++j) o[j * 64] = j < S ? X[j] : B[j - S];
@@ -487,6 +346,17 @@ struct FbsConst {
 template <int S, int... Gs>
 __device__ __forceinline__ void fbs_store_words(uint4* __restrict__ dst, const uint32_t (&x)[S], std::integer_sequence<int, Gs...>) {
   ((dst[Gs] = make_uint4(fb_word<S, 4 * Gs>(x), fb_word<S, 4 * Gs + 1>(x), fb_word<S, 4 * Gs + 2>(x), fb_word<S, 4 * Gs + 3>(x))),
+   ...);
+}
+template <int N, int I>
+__device__ __forceinline__ uint32_t fbs_limb_or0(const uint32_t (&x)[N]) {
+  if constexpr (I < N) return x[I];
+  else return 0u;
+}
+template <int S, int N, int... Gs>   // limbs 0 .. S-1 of x, one per word, zero-padded to whole quads
+__device__ __forceinline__ void fbs_store_limbs(uint4* __restrict__ dst, const uint32_t (&x)[N], std::integer_sequence<int, Gs...>) {
+  ((dst[Gs] = make_uint4(4 * Gs < S ? fbs_limb_or0<N, 4 * Gs>(x) : 0u, 4 * Gs + 1 < S ? fbs_limb_or0<N, 4 * Gs + 1>(x) : 0u,
+                         4 * Gs + 2 < S ? fbs_limb_or0<N, 4 * Gs + 2>(x) : 0u, 4 * Gs + 3 < S ? fbs_limb_or0<N, 4 * Gs + 3>(x) : 0u)),
    ...);
 }
 
@@ -594,8 +464,8 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_fbs_fill(const FbpHalf* halves, 
     }
   }
   uint4* dst = table + ((size_t)k * ent + d) * TQ;
-  fbs_store_words<S>(dst, A, std::make_integer_sequence<int, G::QA>{});
-  fbs_store_words<S + 1>(dst + G::QA, ap, std::make_integer_sequence<int, G::QAP>{});
+  fbs_store_limbs<S>(dst, A, std::make_integer_sequence<int, G::QA>{});
+  fbs_store_limbs<S>(dst + G::QA, ap, std::make_integer_sequence<int, G::QAP>{});   // a' < R: limb S is zero
   fbs_store_words<S>(dst + G::QA + G::QAP, bR, std::make_integer_sequence<int, G::QB>{});
 }
 

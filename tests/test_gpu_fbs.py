@@ -9,7 +9,7 @@ from oracle import paillier_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-ROW_BYTES = {1024: 208, 2048: 400}   # a (QA quads), a' (QAP), b R (QB): 4 + 5 + 4 and 8 + 9 + 8 quads
+ROW_BYTES = {1024: 224, 2048: 448}   # a limbs (QA quads), a' limbs (QAP), b R words (QB): 5 + 5 + 4 and 10 + 10 + 8
 
 
 def _key(golden, nb):
@@ -67,7 +67,7 @@ def test_shoup_rows_match_montgomery_rows_and_oracle(golden, monkeypatch, nb):
 @pytest.mark.parametrize("nb,window", [(1024, 20), (2048, 16), (2048, 20), (2048, 22)])
 def test_shoup_rows_match_reference_goldens(golden, golden_fb, monkeypatch, nb, window):
     """The reference's own ciphertexts (window-independent: a_h is reduced mod p_h - 1 before it is cut into
-    digits); W = 22 is the largest nb = 2048 window whose Shoup tables (2 x 79 GB) fit one MI355X."""
+    digits); W = 22 is the largest nb = 2048 window whose Shoup tables (2 x 88.3 GB) fit one MI355X."""
     from flex.crypto.paillier import _native as N
     key = _key(golden, nb)
     g = golden_fb["keys"][str(nb)]

@@ -51,6 +51,20 @@ __global__ void k_mad_u64(uint64_t* out, uint32_t s) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = r;
 }
 
+__global__ void k_mad_i64(uint64_t* out, uint32_t s) {
+  uint64_t a[CHAINS];
+#pragma unroll
+  for (int i = 0; i < CHAINS; ++i) a[i] = threadIdx.x + i;
+  uint32_t x = s + threadIdx.x;
+  for (int it = 0; it < ITERS; ++it) {
+#define OP(i) asm volatile("v_mad_i64_i32 %0, vcc, %1, %2, %0" : "+v"(a[i]) : "v"(x), "v"(s) : "vcc");
+    REP16(OP)
+#undef OP
+  }
+  uint64_t r = 0; for (int i = 0; i < CHAINS; ++i) r += a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+
 __global__ void k_mul_hi_u32(uint32_t* out, uint32_t s) {
   uint32_t a[CHAINS];
 #pragma unroll
@@ -169,7 +183,7 @@ int main() {
   struct T { const char* name; int which; } tests[] = {
     {"v_fma_f32", 0}, {"v_fma_f64", 1}, {"v_mad_u64_u32", 2}, {"v_mul_hi_u32", 3},
     {"v_mul_lo_u32", 4}, {"v_mad_u32_u24", 5}, {"v_lshl_add_u64", 6}, {"v_addc_co_u32", 7},
-    {"v_add3_u32", 8}, {"v_add_u32_dpp row_shr", 9}, {"v_cvt_f64_u32", 10}};
+    {"v_add3_u32", 8}, {"v_add_u32_dpp row_shr", 9}, {"v_cvt_f64_u32", 10}, {"v_mad_i64_i32", 11}};
   double fma32_rate = 0;
   for (auto& t : tests) {
     float best = 1e30f;
@@ -187,6 +201,7 @@ int main() {
         case 8: k_add3_u32<<<blocks, threads>>>((uint32_t*)buf, 12345u); break;
         case 9: k_dpp_shr<<<blocks, threads>>>((uint32_t*)buf, 12345u); break;
         case 10: k_cvt_f64_u32<<<blocks, threads>>>((double*)buf, 12345u); break;
+        case 11: k_mad_i64<<<blocks, threads>>>((uint64_t*)buf, 12345u); break;
       }
       hipEventRecord(e1); hipEventSynchronize(e1);
       float ms; hipEventElapsedTime(&ms, e0, e1);

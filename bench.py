@@ -347,9 +347,8 @@ def main():
                     help="device-RNG sampler of r^n on the CRT path (kernels_fb.hpp vs r from ChaCha20)")
     ap.add_argument("--fb-window", type=int, default=23, choices=(8, 12, 16, 20, 21, 22, 23, 24),
                     help="largest digit window of the fixed-base tables; the library takes the largest one <= this "
-                         "whose tables fit the free HBM (nb = 2048: W = 23, 45 pair products per half, 2 x 96.6 GB; "
-                         "nb = 4096: W = 21, 98 products per half, 2 x 121.7 GB). With the pair sampler W = 23 "
-                         "measured 1.8 %% faster than 22 (profiles/r02_window_sweep_pair.txt)")
+                         "whose tables fit the free HBM (nb = 2048: W = 22 with Shoup rows, 47 products per half, "
+                         "2 x 88.3 GB; nb = 4096: W = 21, 98 products per half, 2 x 121.7 GB)")
     ap.add_argument("--pfb-window", type=int, default=20, choices=(12, 16, 20),
                     help="digit window of the public-key fixed-base leg (W = 20: 266 row products per element, "
                          "139 GB of tables; the library default is 16)")
@@ -945,7 +944,7 @@ def main():
                                      "PaillierEncryptedNumber (encryptor.py:99-114 API), incl. materialisation")
         del objs
         # the drop-in path's own device rate: the runtime's context at the library's default window (callers
-        # of PaillierEncryptor reach this, not the bench's W = 23 context), device-resident input
+        # of PaillierEncryptor reach this, not the bench's W = 22 context), device-resident input
         rctx = _runtime.context(pk)
         ct_r = torch.empty((N, W), dtype=torch.int32, device=dev)
         ex_r = torch.empty(N, dtype=torch.int32, device=dev)
@@ -1020,7 +1019,7 @@ def main():
 
     # ---- a party holding ONLY the public key (HE_OTP_LR / HE_LR_FP hosts): public fixed bases (kernels_pfb.hpp)
     if not args.no_public and solo and nb == 2048:
-        # the key holder's tables (2 x 96.6 GB at W = 23) make room for the public ones (W = 20: 139 GB); nothing
+        # the key holder's tables (2 x 88.3 GB at W = 22) make room for the public ones (W = 20: 139 GB); nothing
         # after this leg encrypts with the key holder's context
         ctx.set_fb_window(16)
         torch.cuda.synchronize()
@@ -1227,7 +1226,7 @@ def main():
                    "world_size_seen": dist.get_world_size() if world > 1 else 1},
         "roofline": {"bound": "valu-int-mac", "achieved": achieved / 1e12, "peak": INT_MAC_PEAK / 1e12,
                      "unit": "TMAC/s", "frac": achieved / INT_MAC_PEAK,
-                     "traffic": load_traffic(dom, N, nb, fb_info[3] if (use_fb and dom in ("k_fb", "k_fbp", "k_fbg", "k_fbgp", "k_sgp")) else None),
+                     "traffic": load_traffic(dom, N, nb, fb_info[3] if (use_fb and dom in ("k_fb", "k_fbp", "k_fbs", "k_fbg", "k_fbgp", "k_sgp")) else None),
                      "kernel": dom, "kernel_ms": dom_ms,
                      "work_per_unit": (f"{dom_work:.4g} MAC per element: the Shoup-row count (K = {fb_info[2]} Shoup products "
                                        f"mod p_h^2 per half, 3 s^2 + 3 s each over s = nb/64 32-bit limbs of p_h, + the c0 sum "

@@ -1,8 +1,12 @@
 // Pair fixed-base kernels (kernels_fbp.hpp): instantiations and launches.
 #include "engine_fbp.hpp"
+#ifndef FLEXPAI_XCHECK
+#define FLEXPAI_XCHECK 0   // 1: the test-only library (flexpai.hip: xcheck_env)
+#endif
 
 namespace fpai {
 
+#if FLEXPAI_XCHECK
 int fbp_occupancy(int s, int* occ) {
   hipError_t e;
   if (s == 19) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, k_fbp<19>, LANE_BLOCK, 0);
@@ -11,13 +15,16 @@ int fbp_occupancy(int s, int* occ) {
   if (e != hipSuccess || *occ < 1) *occ = 1;
   return 0;
 }
+#endif
 
+#if FLEXPAI_XCHECK
 hipError_t fbp_launch(int s, const FbpParams& p, int gx, hipStream_t st) {
   if (s == 19) hipLaunchKernelGGL(k_fbp<19>, dim3(gx, 2), dim3(LANE_BLOCK), 0, st, p);
   else if (s == 37) hipLaunchKernelGGL(k_fbp<37>, dim3(gx, 2), dim3(LANE_BLOCK), 0, st, p);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
+#endif
 
 int fbp_fin_occupancy(int s, int* occ) {
   hipError_t e;
@@ -52,6 +59,7 @@ hipError_t fbp_build_phase1(int s, const FbpHalf* d_halves, int K, int W, hipStr
 }
 
 // phase 2 (after the host wrote the chain inverses): the inverse tables, then the factored rows
+#if FLEXPAI_XCHECK
 hipError_t fbp_build_phase2(int s, const FbpHalf* d_halves, uint4* t0, uint4* t1, int K, int W, hipStream_t st) {
   const int per = ((1 << W) + LANE_BLOCK - 1) / LANE_BLOCK;
   const dim3 ig((2 * K + 63) / 64, 2);
@@ -66,5 +74,6 @@ hipError_t fbp_build_phase2(int s, const FbpHalf* d_halves, uint4* t0, uint4* t1
   }
   return hipGetLastError();
 }
+#endif
 
 }  // namespace fpai

@@ -24,8 +24,8 @@
 #include "engine_fbs.hpp"
 
 // FLEXPAI_XCHECK (the test-only library libflexpai_xcheck.so, __graft_entry__.build): the kernel generations the
-// pair kernels replaced -- k_fb/k_fb_fin, k_fbg, k_fbgp, k_pfb, the 2S-limb k_dec_* and k_crt_b -- and k_debug,
-// selected by $FLEXPAI_FB_PAIR=0 / $FLEXPAI_SGP=0 / $FLEXPAI_PAIR=0, so that the tests can cross-check the shipping
+// pair kernels replaced -- k_fb/k_fb_fin, k_fbg, k_fbgp, k_pfb, k_fbp, the 2S-limb k_dec_* and k_crt_b -- and k_debug,
+// selected by $FLEXPAI_FB_PAIR=0 / $FLEXPAI_SGP=0 / $FLEXPAI_FBS=0 / $FLEXPAI_PAIR=0, so that the tests can cross-check the shipping
 // kernels against them. The product library (FLEXPAI_XCHECK 0) does not contain them and ignores those variables.
 #ifndef FLEXPAI_XCHECK
 #define FLEXPAI_XCHECK 0
@@ -735,13 +735,14 @@ static int fb_pair_possible(const pai_ctx* c) {
   return ps;
 }
 
-// Shoup rows (kernels_fbs.hpp) on the pair path: $FLEXPAI_FBS=1 (default 0: k_fbp's Montgomery rows).
-// Their a' = floor(a R / p_h) < R and k_fbs_fill's mu = floor(R^2 / p_h) must fit S + 1 limbs: p_h > 2^(28 (S - 1)).
+// Shoup rows (kernels_fbs.hpp, k_fbs) on the pair path: the product's sampler for 1024/2048-bit keys. The test build
+// keeps k_fbp's Montgomery rows behind $FLEXPAI_FBS=0 for the cross-checks. Shoup's a' = floor(a R / p_h) < R and
+// k_fbs_fill's mu = floor(R^2 / p_h) must fit S + 1 limbs: p_h > 2^(28 (S - 1)).
 static bool fb_shoup_possible(const pai_ctx* c) {
   const int ps = fb_pair_possible(c);
   if (!ps) return false;
-  const char* e = getenv("FLEXPAI_FBS");
-  if (!e || atoi(e) == 0) return false;
+  const char* e = xcheck_env("FLEXPAI_FBS");
+  if (e && atoi(e) == 0) return false;
   for (const HBig* h : {&c->fb_p, &c->fb_q})
     if (h->bits() <= (size_t)LB * (ps - 1)) return false;
   return true;
@@ -913,7 +914,7 @@ static int ensure_fb(pai_ctx* c) {
   const bool pair_ok = ps != 0;
   const bool shoup = pair_ok && fb_shoup_possible(c);
 #if !FLEXPAI_XCHECK
-  if (!grp && !pair_ok) return fb_unavailable(c, "key outside the pair sampler's bounds");
+  if (!grp && !shoup) return fb_unavailable(c, "key outside the pair sampler's bounds");
 #endif
   // 4096-bit keys: pair products on lane groups of 4 x 19 limbs (kernels_grp_pair.hpp), R = 2^(28 76) >= 2^24 p_h
   const bool gpair_ok = grp && fb_gpair_possible(c);
@@ -1162,8 +1163,7 @@ static int ensure_fb(pai_ctx* c) {
                                   : fb_build_tables(sb, c->d_fb_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
 #else
   const hipError_t be = gpair_ok ? fbgp_build_phase2(c->d_fbgp_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
-                        : shoup  ? fbs_build_phase2(ps, c->d_fbp_halves, c->d_fbs_cst, (uint4*)t[0], (uint4*)t[1], K, W, nullptr)
-                                 : fbp_build_phase2(ps, c->d_fbp_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
+                                 : fbs_build_phase2(ps, c->d_fbp_halves, c->d_fbs_cst, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
 #endif
   if (be != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return fb_unavailable(c, "table construction failed");
@@ -1698,10 +1698,12 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
   }
 #else
   if (grp && !(c->fb_gpair && c->d_sgp_fb)) return fail(PAI_ERR_KEY, "fixed-base encrypt: no split-pair tables");
-  if (!grp && !c->fb_pair_s) return fail(PAI_ERR_KEY, "fixed-base encrypt: no pair tables");
+  if (!grp && !c->fb_shoup) return fail(PAI_ERR_KEY, "fixed-base encrypt: no Shoup tables");
 #endif
-  if (c->fb_pair_s && (c->fb_shoup ? fbs_occupancy(c->fb_pair_s, &occF) : fbp_occupancy(c->fb_pair_s, &occF)))
-    return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
+#if FLEXPAI_XCHECK
+  if (c->fb_pair_s && !c->fb_shoup && fbp_occupancy(c->fb_pair_s, &occF)) return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
+#endif
+  if (c->fb_shoup && fbs_occupancy(c->fb_pair_s, &occF)) return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
   // elements per block: one per lane, one per lane pair (k_fbs), or one per lane group (grp)
   const int EPB = grp ? BLOCK / GRP_TPI : c->fb_shoup ? LANE_BLOCK / 2 : LANE_BLOCK;
   const long long lane_blocks = (chunk + EPB - 1) / EPB;
@@ -1744,7 +1746,10 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     const int gF = (int)std::min<long long>(gxF, (n + EPB - 1) / EPB);
     if (c->fb_pair_s) {
       const FbpParams pp{c->d_fbp_halves, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
-      HIPCHK(c->fb_shoup ? fbs_launch(c->fb_pair_s, pp, gF, st) : fbp_launch(c->fb_pair_s, pp, gF, st));
+#if FLEXPAI_XCHECK
+      if (!c->fb_shoup) HIPCHK(fbp_launch(c->fb_pair_s, pp, gF, st));
+#endif
+      if (c->fb_shoup) HIPCHK(fbs_launch(c->fb_pair_s, pp, gF, st));
     } else if (grp && c->fb_gpair) {
       const FbgpParams pg{c->d_fbgp_halves, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
       if (c->d_sgp_fb) {   // split pairs (kernels_sgp.hpp): SGP_PAIRS elements per block, grid (gx, 2)

@@ -302,7 +302,8 @@ class Context:
 
     @property
     def fb_pair(self) -> int:
-        """Limbs of p_h of the resident pair tables (kernels_fbp.hpp: k_fbp), 0 for k_fb tables or none."""
+        """Limbs of p_h of the resident pair tables (kernels_fbs.hpp: k_fbs; kernels_fbp.hpp: k_fbp in the test build),
+        0 for k_fb tables or none."""
         return int(self._get_option(PAI_OPT_FB_PAIR))
 
     @property

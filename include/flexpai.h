@@ -112,7 +112,7 @@ typedef struct pai_comm pai_comm;
                                     free device memory less max(4 GiB, 1/12 of the device)).
                                     $FLEXPAI_FB_WINDOW=auto: a process holding ONE private key asks for 24 and
                                     gets the largest window whose tables fit $FLEXPAI_FB_AUTO_FRAC (default
-                                    0.75) of the free memory (W = 23 at nb = 2048, 21 at nb = 4096 on an idle
+                                    0.75) of the free memory (W = 22 at nb = 2048, 21 at nb = 4096 on an idle
                                     MI355X); a process holding several keys gets 16                          */
 #define PAI_OPT_FB_READY 7       /* read-only: 1 when the fixed-base tables are resident                    */
 #define PAI_OPT_FB_PAIR 8        /* read-only: limbs of p_h (19, 37; 76 for the 4096-bit pair-group tables)
@@ -135,7 +135,8 @@ typedef struct pai_comm pai_comm;
                                   * public tables are sampled on split pairs (kernels_sgp.hpp: k_sgp, the default;
                                   * $FLEXPAI_SGP=0 at table build selects k_fbgp / k_pfb); bit 2 = the resident
                                   * 1024/2048-bit key-holder tables hold Shoup rows sampled on split pairs
-                                  * (kernels_fbs.hpp: k_fbs; $FLEXPAI_FBS at table build)                      */
+                                  * (kernels_fbs.hpp: k_fbs, the default; $FLEXPAI_FBS=0 in the test build keeps
+                                  * k_fbp's Montgomery rows)                                                   */
 
 /* Number of visible GPUs (0 when there is none or the runtime cannot start). */
 int pai_device_count(int* count);

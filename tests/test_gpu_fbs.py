@@ -1,7 +1,8 @@
 """GPU parity of the Shoup-row sampler (kernels_fbs.hpp: k_fbs_fill builds the rows, k_fbs samples on split lane
-pairs), selected with $FLEXPAI_FBS=1 at table build: the same distribution and the same canonical pairs out as k_fbp
-(Montgomery rows), so the ciphertexts must be bit-identical to k_fbp's and to the reference's own ciphertexts under
-the sampler's obfuscator (tests/golden/paillier_golden_fb.json, made by tests/golden/make_golden_fb.py)."""
+pairs), the product's key-holder sampler at 1024/2048 bits: the same distribution and the same canonical pairs out as
+k_fbp (Montgomery rows; the test build with $FLEXPAI_FBS=0), so the ciphertexts must be bit-identical to k_fbp's and
+to the reference's own ciphertexts under the sampler's obfuscator (tests/golden/paillier_golden_fb.json, made by
+tests/golden/make_golden_fb.py)."""
 import numpy as np
 import pytest
 
@@ -18,11 +19,12 @@ def _key(golden, nb):
 
 
 def _ctx(N, key, shoup, monkeypatch, window):
+    """shoup: the product library; else the test build with $FLEXPAI_FBS=0 (k_fbp)."""
     if shoup:
-        monkeypatch.setenv("FLEXPAI_FBS", "1")
+        ctx = N.Context(key.n, 0, key.p, key.q)
     else:
-        monkeypatch.delenv("FLEXPAI_FBS", raising=False)
-    ctx = N.Context(key.n, 0, key.p, key.q)
+        monkeypatch.setenv("FLEXPAI_FBS", "0")
+        ctx = N.Context(key.n, 0, key.p, key.q, lib=N.load_library(N.XCHECK_LIB_PATH))
     ctx.set_fb_window(window)
     ctx.prepare_fixed_base()
     monkeypatch.delenv("FLEXPAI_FBS", raising=False)   # the choice is made at table build

@@ -52,7 +52,7 @@ def _child(mode, **env):
 
 def _fb_bytes(W, nb=2048):
     K = -(-(nb // 2) // W)                      # digits of p_h - 1 (1024 bits for the golden key)
-    return 2 * K * (1 << W) * 256
+    return 2 * K * (1 << W) * 448               # Shoup rows (kernels_fbs.hpp): 10 + 10 + 8 quads
 
 
 def test_auto_window_one_key_takes_the_largest_that_fits():
@@ -63,7 +63,7 @@ def test_auto_window_one_key_takes_the_largest_that_fits():
     assert out["window"] == want, out
     assert out["table_bytes"] == _fb_bytes(want)
     if free > 280e9:                            # an otherwise idle MI355X: the bench's window
-        assert out["window"] == 23
+        assert out["window"] == 22
 
 
 def test_auto_window_fraction_caps_the_tables():

@@ -342,12 +342,12 @@ def test_c_abi_exports_every_declared_symbol():
 # mangled names of the kernel generations the pair kernels replaced, and of k_debug
 LEGACY_KERNELS = (b"_ZN4fpai4k_fbILi", b"_ZN4fpai8k_fb_finILi", b"_ZN4fpai5k_fbgILi", b"_ZN4fpai6k_fbgpILi",
                   b"_ZN4fpai5k_pfbILi", b"_ZN4fpai9k_dec_preILi", b"_ZN4fpai9k_dec_powILi", b"_ZN4fpai9k_dec_finILi",
-                  b"_ZN4fpai7k_crt_bILi", b"_ZN4fpai7k_debugILi")
+                  b"_ZN4fpai7k_crt_bILi", b"_ZN4fpai7k_debugILi", b"_ZN4fpai5k_fbpILi", b"_ZN4fpai10k_fbp_fillILi")
 
 
 def test_product_library_carries_no_superseded_kernels():
     """the superseded kernels (and k_debug) are in the test build only; the product library
-    holds the shipping kernels (k_fbp, k_fbs, k_sgp, ...) and none of them."""
+    holds the shipping kernels (k_fbs, k_fbp_fin, k_sgp, ...) and none of them."""
     from flex.crypto.paillier import _native
     if not os.path.exists(_native.LIB_PATH) or not os.path.exists(_native.XCHECK_LIB_PATH):
         pytest.skip("libraries not built (run __graft_entry__.build())")
@@ -356,7 +356,7 @@ def test_product_library_carries_no_superseded_kernels():
     for k in LEGACY_KERNELS:
         assert k not in prod, k
         assert k in xck, k
-    for k in (b"_ZN4fpai5k_fbpILi", b"_ZN4fpai5k_fbsILi", b"_ZN4fpai5k_sgp", b"_ZN4fpai14k_dec_pow_pairILi"):
+    for k in (b"_ZN4fpai5k_fbsILi", b"_ZN4fpai9k_fbp_finILi", b"_ZN4fpai5k_sgp", b"_ZN4fpai14k_dec_pow_pairILi"):
         assert k in prod, k
 
 

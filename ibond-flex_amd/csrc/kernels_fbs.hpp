@@ -279,16 +279,17 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbs(FbpParams p) {
       {   // step 2; the odd lane's accumulator starts at the even lane's Q_A
         uint64_t P[S];
 #pragma unroll
-        for (int i = 0; i < S; ++i) {
-          const uint32_t qa = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q[i], 0xA0, 0xF, 0xF, false);   // quad_perm [0,0,2,2]
-          P[i] = odd ? (uint64_t)qa : 0ull;
-        }
+        for (int i = 0; i < S; ++i) P[i] = 0;   // (the first MACs take a zero addend)
         FbsPairReader<S, G::QA, 0, false, 1> r2{cur};
         fbs_r_all<S>(P, X, q, m, r2, std::make_integer_sequence<int, S>{});
+        // normalise, the odd lane adding the even lane's Q_A on the way: one DPP and one MAC by 0 / 1 per limb
+        uint32_t ob = odd ? 1u : 0u;
+        asm volatile("" : "+v"(ob));   // (a multiplier, not a select)
         uint64_t c = 0;   // (mod R: the carry out of limb S - 1 is dropped)
 #pragma unroll
         for (int i = 0; i < S; ++i) {
-          const uint64_t v = P[i] + c;
+          const uint32_t qa = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q[i], 0xA0, 0xF, 0xF, false);   // quad_perm [0,0,2,2]
+          const uint64_t v = P[i] + c + (uint64_t)qa * ob;
           X[i] = lane::limb32(v);
           c = v >> lane::LB;
         }

@@ -114,3 +114,37 @@ def test_shoup_rows_full_size_1m(golden, monkeypatch):
         assert np.array_equal(val, x.astype(np.float64))
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("pbits", [(1020, 1021), (1016, 1017), (508, 509)])
+def test_shoup_rows_short_primes(monkeypatch, pbits):
+    """Primes below the full half size (n of 2041, 2033 and 1017 bits; 2033 is the shortest 2048-class n whose n^2
+    still fills the 128-word rows the fixed-base path requires): Shoup's mu = floor(R^2 / p_h) takes more limbs and a'
+    stays below R. Sampler bit-exact against the oracle and against k_fbp of the test build; decrypts."""
+    from flex.crypto.paillier import _native as N
+    from tests.test_gpu_pair_paths import _prime
+    rng = np.random.default_rng(sum(pbits))
+    while True:
+        p, q = _prime(pbits[0], rng), _prime(pbits[1], rng)
+        if p < q < 2 * p:
+            break
+    key = O.Key(p * q, p, q)
+    x = (rng.standard_normal(300) * 100).astype(np.float32)
+    rk = bytes(range(3, 35))
+    outs = []
+    for shoup in (True, False):
+        ctx = _ctx(N, key, shoup, monkeypatch, 12)
+        try:
+            assert bool(ctx.split_sampler & 4) == shoup and ctx.fb_ready
+            params = ctx.fixed_base_info()
+            ct, ex, st = ctx.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=17)
+            assert np.all(st == 0)
+            outs.append((ct, ex))
+            if shoup:
+                got = N.words_to_ints(ct)
+                for i in (0, 150, 299):
+                    assert (got[i], int(ex[i])) == O.fb_encrypt_value(x[i], key, rk, 17 + i, params), i
+                assert np.array_equal(ctx.decrypt(ct, ex)[0], x.astype(np.float64))
+        finally:
+            ctx.close()
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])

@@ -517,10 +517,49 @@ __device__ __forceinline__ uint64_t fbpf_col(const uint32_t (&a1)[S], const uint
   }
   return s;
 }
+// The ciphertext words leave through the wave's LDS tile (dead once w_q is in registers), HW words of each ciphertext
+// at a time (64 at nb = 2048, 32 at 1024: what a lane's share of the tile holds): each lane writes its words to its
+// own row (stride HW + 4 words, padded against bank conflicts), then the wave stores the 64 rows as instructions of
+// 1 KB, each whole HW-word pieces of 1024 / (4 HW) ciphertexts -- full lines, where per-lane 16-B stores 512 B apart
+// left L2 to write back partial lines (1.8x the output bytes, profiles/pmc_k_fbp_fin_latest.json of round 3).
+template <int CW>
+struct FbpfHW {   // words per piece: 64 of a 2048-bit key's 128, 32 of a 1024-bit key's 64
+  static constexpr int value = CW >= 128 ? 64 : 32;
+};
+template <int HW>
+struct FbpfOut {
+  static constexpr int OST = HW + 4, LPE = HW / 4, EPI = 64 / LPE;   // row stride; lanes per piece; pieces per store
+  uint32_t lrow;       // this lane's row in the tile (LDS byte address)
+  uint32_t tile;       // the tile (wave-uniform LDS byte address)
+  uint32_t* ct;        // the wave's first ciphertext
+  int ct_words, nvalid;   // words per ciphertext; valid elements of the wave (<= 64)
+  int lane;
+  __device__ __forceinline__ void put(int w, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {   // words w .. w+3
+    const fbp_u32x4 v = {a, b, c, d};
+    asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(lrow), "v"(v), "i"(0) : "memory");
+    lrow += 16;
+    (void)w;
+  }
+  __device__ __forceinline__ void flush(int half) {   // rows -> words [64 half, 64 half + 64) of each ciphertext
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int sub = lane % LPE, el = lane / LPE;
+#pragma unroll
+    for (int g = 0; g < 64 / EPI; ++g) {
+      const int e = EPI * g + el;
+      fbp_u32x4 v;
+      const uint32_t a = tile + (uint32_t)((e * OST + 4 * sub) * 4);
+      asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v) :: "memory");
+      if (e < nvalid) *reinterpret_cast<fbp_u32x4*>(ct + (size_t)e * ct_words + HW * half + 4 * sub) = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // (the rows are rewritten by the next piece)
+    lrow -= HW * 4;
+  }
+};
 template <int S, int CW, int K>
 __device__ __forceinline__ void fbpf_out_step(uint64_t& acc, uint64_t& buf, uint32_t (&o4)[4], const uint32_t (&a1)[S],
                                               const uint32_t (&b1)[S], const uint32_t (&ha)[S], const uint32_t (&hb)[S],
-                                              const uint32_t* __restrict__ cq, uint4* dst, bool valid) {
+                                              const uint32_t* __restrict__ cq, FbpfOut<FbpfHW<CW>::value>& out) {
   acc += fbpf_col<S, K>(a1, b1, ha, hb, cq);
   const uint32_t limb = (uint32_t)acc & lane::LMASK;
   acc >>= lane::LB;
@@ -531,17 +570,38 @@ __device__ __forceinline__ void fbpf_out_step(uint64_t& acc, uint64_t& buf, uint
     o4[w % 4] = (uint32_t)buf;
     buf >>= 32;
     if constexpr (w % 4 == 3 && w < CW) {
-      if (valid) dst[w / 4] = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+      constexpr int HW = FbpfHW<CW>::value;
+      out.put(w - 3, o4[0], o4[1], o4[2], o4[3]);
+      if constexpr (w % HW == HW - 1) out.flush(w / HW);
     }
   }
 }
 template <int S, int CW, int... Ks>
 __device__ __forceinline__ void fbpf_out_all(const uint32_t (&a1)[S], const uint32_t (&b1)[S], const uint32_t (&ha)[S],
-                                             const uint32_t (&hb)[S], const uint32_t* __restrict__ cq, uint4* dst, bool valid,
+                                             const uint32_t (&hb)[S], const uint32_t* __restrict__ cq, FbpfOut<FbpfHW<CW>::value>& out,
                                              std::integer_sequence<int, Ks...>) {
+  static_assert(CW % FbpfHW<CW>::value == 0, "whole pieces");
   uint64_t acc = 0, buf = 0;
   uint32_t o4[4] = {0u, 0u, 0u, 0u};
-  (fbpf_out_step<S, CW, Ks>(acc, buf, o4, a1, b1, ha, hb, cq, dst, valid), ...);
+  (fbpf_out_step<S, CW, Ks>(acc, buf, o4, a1, b1, ha, hb, cq, out), ...);
+}
+
+// the wave's 64-element tile of half h's pairs (2S limbs x 64 elements, contiguous, 256-B aligned; tiles are padded
+// to 64 elements) -> the wave's LDS tile at lb, 1 KB per DMA
+template <int S>
+__device__ __forceinline__ void fbpf_tile_dma(const uint32_t* pr, long long e0, int h, long long n, uint32_t lb, int lane) {
+  uint64_t src = (uint64_t)(reinterpret_cast<const uint4*>(pr + fbp_pair_index<S>(e0, h, n)) + lane);
+  constexpr int NI = (32 * S + 63) / 64, REM = (32 * S) % 64;
+#pragma unroll
+  for (int g = 0; g < NI; ++g) {
+    uint32_t dst = lb + (uint32_t)(g * 1024);
+    asm volatile("" : "+s"(dst));
+    if (REM == 0 || g + 1 < NI || lane < REM)
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(size_t)dst, 16, 0, 0);
+    src += 1024;
+    asm volatile("" : "+v"(src));   // one address register, advanced per DMA (not 19 precomputed)
+  }
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 template <int S>
@@ -550,7 +610,8 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
   constexpr int NL = (32 * CW + 27) / 28;             // limbs that cover them
   static_assert(NL <= 4 * S, "c < n^2 fits 4 S limbs");
   __shared__ uint32_t cs[12 * S];
-  // the waves' 64-element tiles of w_p pairs (2S limbs x 64 elements each), streamed in by DMA during X's product
+  // the waves' 64-element tiles of w_p pairs (2S limbs x 64 elements each), streamed in by DMA during X's product; then
+  // w_q's tile for the final sum, then the ciphertext rows on the way out
   __shared__ __attribute__((aligned(16))) uint32_t wpl[(LANE_BLOCK / 64) * 2 * S * 64];
   for (int j = threadIdx.x; j < 12 * S; j += blockDim.x) cs[j] = p.cs[j];
   __syncthreads();
@@ -567,24 +628,15 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
     const bool valid = i < p.n;
     const long long ii = valid ? i : p.n - 1;
     const uint32_t* pq = p.pr + fbp_pair_index<S>(ii, 1, p.n);
-    {   // the wave's w_p tile (contiguous, 256-B aligned; tiles are padded to 64 elements) -> LDS, 1 KB per DMA
-      long long e0 = base + (threadIdx.x & ~63);
-      if (e0 >= p.n) e0 = (p.n - 1) & ~63ll;
-      uint64_t src = (uint64_t)(reinterpret_cast<const uint4*>(p.pr + fbp_pair_index<S>(e0, 0, p.n)) + lane);
-      typedef __attribute__((address_space(3))) uint32_t lds_u32;
+    // the wave's first element (wave-uniform: in SGPRs, so it costs no VGPRs across the products)
+    long long e0 = base + (long long)(uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+    const bool wave_live = e0 < p.n;   // (a wave past the end computes the last element; it must not store)
+    if (!wave_live) e0 = (p.n - 1) & ~63ll;
+    typedef __attribute__((address_space(3))) uint32_t lds_u32;
+    {   // the wave's w_p tile -> LDS
       const uint32_t lb = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds_u32*)wpp);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous element's reads of the tile are done
-      constexpr int NI = (32 * S + 63) / 64, REM = (32 * S) % 64;
-#pragma unroll
-      for (int g = 0; g < NI; ++g) {
-        uint32_t dst = lb + (uint32_t)(g * 1024);
-        asm volatile("" : "+s"(dst));
-        if (REM == 0 || g + 1 < NI || lane < REM)
-          __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(size_t)dst, 16, 0, 0);
-        src += 1024;
-        asm volatile("" : "+v"(src));   // one address register, advanced per DMA (not 19 precomputed)
-      }
-      __builtin_amdgcn_sched_barrier(0);
+      fbpf_tile_dma<S>(p.pr, e0, 0, p.n, lb, lane);
     }
     // X = q B_q mod p^2
     uint32_t xa[S], xb[S];
@@ -614,15 +666,45 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
     // h = D q^-2 mod p^2, canonical
     pair::mont_mul<S>(xa, xb, FbpFinDigits<S>{cs + 2 * S}, m, mprime);
     pair::canon<S>(xa, xb, m);
+    {   // w_p is consumed: the wave's w_q tile -> the same LDS tile, read by the final sum (instead of w_q from HBM a
+        // second time); issued after h's product, which holds every register
+      const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      const uint32_t lb = (uint32_t)(size_t)(lds_u32*)(wpl + wv * 2 * S * 64);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every lane's reads of w_p are done
+      int ln = threadIdx.x & 63;
+      asm volatile("" : "+v"(ln));
+      fbpf_tile_dma<S>(p.pr, e0, 1, p.n, lb, ln);
+    }
     // c = w_q + q^2 h
     uint32_t a1[S], b1[S];
+    {
+      lds_dma_wait();   // the w_q tile landed
+      int tx = threadIdx.x;
+      asm volatile("" : "+v"(tx));
+      const uint32_t* wq = wpl + (tx >> 6) * 2 * S * 64 + (tx & 63);
 #pragma unroll
-    for (int j = 0; j < S; ++j) {
-      a1[j] = pq[j * 64];
-      b1[j] = pq[(S + j) * 64];
+      for (int j = 0; j < S; ++j) {
+        a1[j] = wq[j * 64];
+        b1[j] = wq[(S + j) * 64];
+      }
     }
-    fbpf_out_all<S, CW>(a1, b1, xa, xb, cs + 4 * S, reinterpret_cast<uint4*>(p.ct + ii * p.ct_words), valid,
-                        std::make_integer_sequence<int, NL>{});
+    {
+      using Out = FbpfOut<FbpfHW<CW>::value>;
+      static_assert(64 * Out::OST <= 2 * S * 64, "the output rows fit the tile");
+      const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      const uint32_t tile = (uint32_t)(size_t)(lds_u32*)(wpl + wv * 2 * S * 64);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every lane's reads of w_q are done (a1, b1 in registers)
+      const long long left = p.n - e0;
+      const uint64_t cta = (uint64_t)(p.ct + (size_t)e0 * p.ct_words);   // wave-uniform: SGPRs
+      // (readfirstlane returns int: through uint32_t, or an address half >= 2^31 sign-extends)
+      uint32_t* ctw = (uint32_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cta >> 32)) << 32) |
+                                  (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cta));
+      int ln = threadIdx.x & 63;
+      asm volatile("" : "+v"(ln));
+      Out out{tile + (uint32_t)(ln * Out::OST * 4), tile, ctw, p.ct_words,
+              wave_live ? (int)__builtin_amdgcn_readfirstlane((uint32_t)(left < 64 ? left : 64)) : 0, ln};
+      fbpf_out_all<S, CW>(a1, b1, xa, xb, cs + 4 * S, out, std::make_integer_sequence<int, NL>{});
+    }
   }
 }
 

@@ -586,6 +586,68 @@ __device__ __forceinline__ void fbpf_out_all(const uint32_t (&a1)[S], const uint
   (fbpf_out_step<S, CW, Ks>(acc, buf, o4, a1, b1, ha, hb, cq, out), ...);
 }
 
+// The final sum as c = A_q + q (B_q + q h), h = H_A + p H_B < p^2 (2S limbs): three product-scanning passes whose
+// multiplier limbs are p (SGPRs) and q (VGPRs, the same value in every lane), S^2 + 2 S^2 + 3 S^2 MACs -- the count of
+// the direct sum over the constants q, q^2 and p q^2, but without an LDS read per MAC for the constant's limb.
+template <int S, int K>
+__device__ __forceinline__ uint64_t fbpf_hcol(const uint32_t (&ha)[S], const uint32_t (&hb)[S], const uint32_t (&m)[S]) {
+  uint64_t s = K < S ? (uint64_t)ha[K] : 0ull;
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+    if (K - i >= 0 && K - i < S) s += (uint64_t)hb[i] * m[K - i];
+  return s;
+}
+template <int S, int... Ks>
+__device__ __forceinline__ void fbpf_h(const uint32_t (&ha)[S], const uint32_t (&hb)[S], const uint32_t (&m)[S],
+                                       uint32_t (&h)[2 * S], std::integer_sequence<int, Ks...>) {
+  uint64_t acc = 0;
+  ((acc += fbpf_hcol<S, Ks>(ha, hb, m), h[Ks] = lane::limb32(acc), acc >>= lane::LB), ...);
+}
+template <int S, int K>
+__device__ __forceinline__ uint64_t fbpf_tcol(const uint32_t (&h)[2 * S], const uint32_t (&qv)[S], const uint32_t* wq) {
+  uint64_t s = K < S ? (uint64_t)wq[(S + K) * 64] : 0ull;   // B_q from the w_q tile
+#pragma unroll
+  for (int i = 0; i < 2 * S; ++i)
+    if (K - i >= 0 && K - i < S) s += (uint64_t)h[i] * qv[K - i];
+  return s;
+}
+template <int S, int... Ks>
+__device__ __forceinline__ void fbpf_t(const uint32_t (&h)[2 * S], const uint32_t (&qv)[S], const uint32_t* wq,
+                                       uint32_t (&t)[3 * S], std::integer_sequence<int, Ks...>) {
+  uint64_t acc = 0;
+  ((acc += fbpf_tcol<S, Ks>(h, qv, wq), t[Ks] = lane::limb32(acc), acc >>= lane::LB), ...);
+}
+template <int S, int CW, int K>
+__device__ __forceinline__ void fbpf_cstep(uint64_t& acc, uint64_t& buf, uint32_t (&o4)[4], const uint32_t (&t)[3 * S],
+                                           const uint32_t (&qv)[S], const uint32_t (&a1)[S], FbpfOut<FbpfHW<CW>::value>& out) {
+  uint64_t s = K < S ? (uint64_t)a1[K] : 0ull;
+#pragma unroll
+  for (int i = 0; i < 3 * S; ++i)
+    if (K - i >= 0 && K - i < S) s += (uint64_t)t[i] * qv[K - i];
+  acc += s;
+  const uint32_t limb = (uint32_t)acc & lane::LMASK;
+  acc >>= lane::LB;
+  constexpr int NB = (28 * K) % 32;
+  buf |= (uint64_t)limb << NB;
+  if constexpr (NB + 28 >= 32) {
+    constexpr int w = (28 * K) / 32;
+    o4[w % 4] = (uint32_t)buf;
+    buf >>= 32;
+    if constexpr (w % 4 == 3 && w < CW) {
+      constexpr int HW = FbpfHW<CW>::value;
+      out.put(w - 3, o4[0], o4[1], o4[2], o4[3]);
+      if constexpr (w % HW == HW - 1) out.flush(w / HW);
+    }
+  }
+}
+template <int S, int CW, int... Ks>
+__device__ __forceinline__ void fbpf_c(const uint32_t (&t)[3 * S], const uint32_t (&qv)[S], const uint32_t (&a1)[S],
+                                       FbpfOut<FbpfHW<CW>::value>& out, std::integer_sequence<int, Ks...>) {
+  uint64_t acc = 0, buf = 0;
+  uint32_t o4[4] = {0u, 0u, 0u, 0u};
+  (fbpf_cstep<S, CW, Ks>(acc, buf, o4, t, qv, a1, out), ...);
+}
+
 // the wave's 64-element tile of half h's pairs (2S limbs x 64 elements, contiguous, 256-B aligned; tiles are padded
 // to 64 elements) -> the wave's LDS tile at lb, 1 KB per DMA
 template <int S>
@@ -675,25 +737,35 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
       asm volatile("" : "+v"(ln));
       fbpf_tile_dma<S>(p.pr, e0, 1, p.n, lb, ln);
     }
-    // c = w_q + q^2 h
-    uint32_t a1[S], b1[S];
+    // c = w_q + q^2 h = A_q + q (B_q + q h), h = H_A + p H_B (fbpf_h / fbpf_t / fbpf_c)
+    uint32_t t[3 * S];
     {
+      uint32_t h[2 * S];
+      fbpf_h<S>(xa, xb, m, h, std::make_integer_sequence<int, 2 * S>{});
+      uint32_t qv[S];
+#pragma unroll
+      for (int j = 0; j < S; ++j) qv[j] = cs[4 * S + j];
       lds_dma_wait();   // the w_q tile landed
+      int tx = threadIdx.x;
+      asm volatile("" : "+v"(tx));
+      const uint32_t* wq = wpl + (tx >> 6) * 2 * S * 64 + (tx & 63);
+      fbpf_t<S>(h, qv, wq, t, std::make_integer_sequence<int, 3 * S>{});
+    }
+    {
+      uint32_t a1[S], qv[S];
       int tx = threadIdx.x;
       asm volatile("" : "+v"(tx));
       const uint32_t* wq = wpl + (tx >> 6) * 2 * S * 64 + (tx & 63);
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         a1[j] = wq[j * 64];
-        b1[j] = wq[(S + j) * 64];
+        qv[j] = cs[4 * S + j];
       }
-    }
-    {
       using Out = FbpfOut<FbpfHW<CW>::value>;
       static_assert(64 * Out::OST <= 2 * S * 64, "the output rows fit the tile");
       const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
       const uint32_t tile = (uint32_t)(size_t)(lds_u32*)(wpl + wv * 2 * S * 64);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every lane's reads of w_q are done (a1, b1 in registers)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every lane's reads of w_q are done (a1 in registers)
       const long long left = p.n - e0;
       const uint64_t cta = (uint64_t)(p.ct + (size_t)e0 * p.ct_words);   // wave-uniform: SGPRs
       // (readfirstlane returns int: through uint32_t, or an address half >= 2^31 sign-extends)
@@ -703,7 +775,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
       asm volatile("" : "+v"(ln));
       Out out{tile + (uint32_t)(ln * Out::OST * 4), tile, ctw, p.ct_words,
               wave_live ? (int)__builtin_amdgcn_readfirstlane((uint32_t)(left < 64 ? left : 64)) : 0, ln};
-      fbpf_out_all<S, CW>(a1, b1, xa, xb, cs + 4 * S, out, std::make_integer_sequence<int, NL>{});
+      fbpf_c<S, CW>(t, qv, a1, out, std::make_integer_sequence<int, NL>{});
     }
   }
 }

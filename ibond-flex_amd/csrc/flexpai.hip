@@ -382,6 +382,61 @@ static bool build_lane_program(const HBig& e, std::vector<uint32_t>& prog) {
   return loaded;
 }
 
+// Op list of the factored 4096-bit decryption (d4f_run, kernels_dec4.hpp): the table's 30 one-pass products by the
+// kept (A~, 0) (odd powers stored in tiles 0..15), the sliding-window chain over e = p_h - 2 with B-free multipliers,
+// then Y' (A~, 0) (iota taken before it) and the product with (1, 0) into tile D4F_G. kf gets the closing sum's
+// constants: K'_t = R sum over the chain's multiplies by entry t of 2^(squares after it) mod p_h, slot 0 = -R mod
+// p_h (entry 1 is B-free, its slot carries the ciphertext's B_c term). tools/dec4f_model.py restates the algebra.
+static bool build_dec4f_program(const HBig& ph, size_t RS, std::vector<uint32_t>& prog, std::vector<uint32_t>& kf) {
+  const HBig e = sub(ph, HBig(2));
+  if (e.bits() < 8) return false;
+  std::vector<uint16_t> sched;
+  int first = 0;
+  sliding_schedule(e, sched, first);
+  auto op = [](uint32_t flags, int bidx, int aidx, int sidx) {
+    return flags | ((uint32_t)bidx << 8) | ((uint32_t)aidx << 16) | ((uint32_t)sidx << 24);
+  };
+  prog.clear();
+  for (int t = 2; t < 2 * LANE_NTILE; ++t) prog.push_back(op(LOP_B_READY | ((t & 1) ? LOP_STORE : 0u), 0, 0, (t - 1) / 2));
+  bool loaded = false;
+  size_t first_sq = SIZE_MAX;
+  for (size_t i = 0; i + 1 < sched.size(); i += 2) {
+    const int nsq = sched[i], idx = sched[i + 1];
+    for (int t = 0; t < nsq; ++t) {
+      if (first_sq == SIZE_MAX) first_sq = prog.size();
+      prog.push_back(loaded ? op(LOP_SQR, 0, 0, 0) : op(LOP_SQR | LOP_A_FROM_T, 0, first, 0));
+      loaded = true;
+    }
+    if (idx != 0xFFFF) {
+      if (first_sq != SIZE_MAX) {
+        prog[first_sq] |= LOP_PREFETCH | ((uint32_t)idx << 8);
+        prog.push_back(op(LOP_B_READY, idx, 0, 0));
+      } else {
+        prog.push_back(loaded ? op(0, idx, 0, 0) : op(LOP_A_FROM_T, idx, first, 0));
+      }
+      loaded = true;
+      first_sq = SIZE_MAX;
+    }
+  }
+  if (!loaded) return false;
+  prog.push_back(op(LOP_IOTA, 0, 0, 0));                      // Z = Y' (A~, 0), A~ = tile 0's even component
+  prog.push_back(op(LOP_B_CONST | LOP_STORE, 0, 0, D4F_G));   // (1 + p G) = Z (1, 0)
+  std::vector<HBig> K(LANE_NTILE, HBig(0));
+  size_t after = 0;
+  for (size_t i = sched.size(); i >= 2; i -= 2) {
+    const int nsq = sched[i - 2], idx = sched[i - 1];
+    if (idx != 0xFFFF) K[idx] = mod(add(K[idx], mul_pow2_mod(HBig(1), after, ph)), ph);
+    after += (size_t)nsq;
+  }
+  kf.clear();
+  for (int t = 0; t < LANE_NTILE; ++t) {
+    const HBig v = t == 0 ? sub(ph, mul_pow2_mod(HBig(1), RS, ph)) : mul_pow2_mod(K[t], RS, ph);
+    const std::vector<uint32_t> l = v.limbs(D4_S, LB);
+    kf.insert(kf.end(), l.begin(), l.end());
+  }
+  return true;
+}
+
 template <typename K>
 static int grid_for(pai_ctx* c, K kernel, size_t lds, long long units, int per_block) {
   int occ = 0;
@@ -1224,19 +1279,20 @@ static int setup_fbg(pai_ctx* c, const HBig& p, const HBig& q) {
       auto one_minus = [&](const HBig& r) {   // (1 - r) mod p_h for 0 < r < p_h
         return mod(sub(add(ph, HBig(1)), r), ph);
       };
-      std::vector<uint32_t> pd;
-      if (!build_lane_program(sub(ph, HBig(1)), pd)) return 0;
+      std::vector<uint32_t> pd, kf;
+      if (!build_dec4f_program(ph, RS, pd, kf)) return 0;
       HBig oi = inv_mod(mod(primes[1 - h], ph), ph);
       if (oi.is_zero()) return 0;
       const HBig hh = sub(ph, oi);
-      uint32_t *dp, *dx1, *dxk, *dck, *dhr, *dprog;
+      uint32_t *dp, *dx1, *dxk, *dck, *dhr, *dprog, *dkf;
       if ((rc = upload(c, ph.limbs(D4_S, LB), &dp)) ||
           (rc = upload(c, one_minus(mul_pow2_mod(HBig(1), RS, ph)).limbs(D4_S, LB), &dx1)) ||
           (rc = upload(c, one_minus(mul_pow2_mod(HBig(1), RS * kp, ph)).limbs(D4_S, LB), &dxk)) ||
           (rc = upload(c, split(mul_pow2_mod(HBig(1), RS * (kp + 1), m2)), &dck)) ||
-          (rc = upload(c, mul_pow2_mod(hh, RS, ph).limbs(D4_S, LB), &dhr)) || (rc = upload(c, pd, &dprog)))
+          (rc = upload(c, mul_pow2_mod(hh, RS, ph).limbs(D4_S, LB), &dhr)) || (rc = upload(c, pd, &dprog)) ||
+          (rc = upload(c, kf, &dkf)))
         return rc;
-      dh[h] = Dec4Half{dp, dx1, dxk, dck, dhr, dprog, (int)pd.size(), mont_prime(ph, LB)};
+      dh[h] = Dec4Half{dp, dx1, dxk, dck, dhr, dprog, (int)pd.size(), mont_prime(ph, LB), dkf};
     }
     std::vector<Dec4Half> dv(dh, dh + 2);
     if ((rc = upload(c, dv, &c->d_dec4_halves))) return rc;

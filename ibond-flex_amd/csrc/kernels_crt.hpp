@@ -32,6 +32,7 @@ enum : uint32_t {
                         // MUL's operand), so the HBM latency of the table row hides behind the squarings
   LOP_B_READY = 32u,    // MUL op: the LDS multiplier already holds the operand (prefetched or kept)
   LOP_B_SET = 64u,      // after the op: LDS multiplier <- a
+  LOP_IOTA = 128u,      // k_dec4_pow (factored chain): before the op, the even lane's A goes to the LDS B half
 };
 constexpr int LANE_NTILE = 16;   // odd powers x^1 .. x^31
 constexpr int KMAX_CHUNKS = 5;   // stage A reduces r of up to KMAX_CHUNKS * LB * SA bits

@@ -16,8 +16,8 @@
 //
 //   k_dec4_pre  per element-half: c R as a pair (one split CIOS over the ciphertext's limbs against the
 //               constant pair of R^(K+1))
-//   k_dec4_pow  per element-half: c^(p_h - 1) by the lane machine's op list (kernels_crt.hpp) on split
-//               pairs, left in plain form by a product with (1, 0)              (decryptor.py:55-61)
+//   k_dec4_pow  per element-half: c^(p_h - 1) on split pairs with B-free window multipliers (d4f_run, below),
+//               left in plain form by a product with (1, 0)                     (decryptor.py:55-61)
 //   k_dec4_L    per element-half: L_h = B of the canonical pair (A = 1; A = 0 for c == 0 mod p_h, L = B - 1),
 //               m_h = L_h h_h mod p_h
 //   k_dec4_fin  per element (lane group of 4, the bn_group engine): CRT (gmpy_math.py:31-40) and
@@ -37,9 +37,10 @@ struct Dec4Half {
   const uint32_t* XK;      // (1 - R^K) mod p_h, K = ciphertext chunks of S limbs
   const uint32_t* cK;      // pair of R^(K+1) mod p_h^2 ([A: S][B: S])
   const uint32_t* hR;      // h_h R mod p_h
-  const uint32_t* prog;    // lane-machine op list for c^(p_h - 1) (kernels_crt.hpp)
+  const uint32_t* prog;    // op list of the factored chain (d4f_run): table, p_h - 2, the two closing products
   int nprog;
   uint32_t mprime;
+  const uint32_t* kf;      // [16][S] K'_t of the closing Horner sum (d4f_run; slot 0: -R mod p_h)
 };
 
 struct Dec4Params {
@@ -279,11 +280,176 @@ __device__ __forceinline__ void d4r_run(uint32_t (&a)[S], uint32_t* st, const La
   }
 }
 
+// ---- k_dec4_pow: B-free window multipliers (round 4)
+// A product by a pair (a, 0) is one pass on both lanes (U = REDC(A_x a) | REDC(B_x a - m)); by a general pair it is
+// two. So the window table is factored, P_t = a_t (1 + p b_t) (a_t, H_t its components, b_t = H_t / a_t mod p), the
+// chain multiplies by (a_t, 0) only, and the dropped factors are put back at the end, where they commute: squares
+// double them, so they total 1 + p s, s = sum_t K_t b_t with K_t = sum over the chain's multiplies by entry t of
+// 2^(squares after it), a constant of the key (the host's build_dec4f_program). b_t needs a_t^-1, and the chain
+// provides it: it runs the exponent p - 2, whose result Y' is A~^-1 R^2 mod p (Fermat) -- iota. With the ciphertext
+// pair c~ = A~ + p B_c = A~ (1 + p u) (the base is B-free: (A~, 0), u = B_c / A~):
+//   P_t      = mm-powers of (A~, 0): 30 one-pass products, odd t stored in tiles 0..15 (tile 0 keeps B_c in the odd
+//              lane's component)
+//   Y'       = the chain over p - 2 (first load: the full pair P_first)
+//   1 + p G  = mm(mm(Y', (A~, 0)), (1, 0))                             (Y' A~ == 1 mod p: c~^(p-1) in plain form)
+//   delta    = s - u = REDC(acc iota), acc = sum_j c_j (w R^-1)^j by Horner, w = REDC(iota iota),
+//              c_j = REDC(H_{2j+1} K'_{2j+1}) R^-1 (K'_t = K_t R), c_0 = -B_c R^-1 (K'_1 = -R: b_1 = 0)
+//   output   = (A, G + delta): c^(p-1) mod p^2 = (1 + p G)(1 + p delta)   (tools/dec4f_model.py checks the algebra)
+// Per 2048-bit p_h: 2043 squares + 341 one-pass products + 30 (table) + 2 + 34 (Horner) passes, against
+// 2043 + 2 x 341 + 33 before. The Horner passes run in the odd lane (the even lane's copy is discarded); K'_t is
+// staged per step through a block-wide LDS row, so the loop over steps is block-uniform.
+constexpr int D4F_G = LANE_NTILE;         // spare tile: the pair (1 + p G)
+constexpr int D4F_ACC = LANE_NTILE + 1;   // spare tile: the Horner accumulator
+constexpr int D4F_HORNER = 2 * LANE_NTILE + 2;   // passes after the chain: w, 16 x (c_j, acc), delta
+static_assert((LANE_NTILE + 2) * tile_quads<D4_S>() <= LANE_NTILE * tile_quads<D4_S>() + RBUF_WORDS / 4,
+              "the two spare tiles fit the lane scratch");
+
+// the even lane's component of tile k -> LDS row dst (the odd lane's copy is not needed: B-free multipliers)
+template <int S, int... Gs>
+__device__ __forceinline__ void d4f_mult_load(const LaneScratch& t, int k, uint32_t* dst, bool odd, std::integer_sequence<int, Gs...>) {
+  constexpr int TQ = tile_quads<S>();
+  d4_fence();
+  if (!odd) {
+    uint4 v[sizeof...(Gs)];
+    ((v[Gs] = t.quad(k * TQ + Gs)), ...);
+    (((4 * Gs < S ? (dst[4 * Gs] = v[Gs].x) : 0u), (4 * Gs + 1 < S ? (dst[4 * Gs + 1] = v[Gs].y) : 0u),
+      (4 * Gs + 2 < S ? (dst[4 * Gs + 2] = v[Gs].z) : 0u), (4 * Gs + 3 < S ? (dst[4 * Gs + 3] = v[Gs].w) : 0u)),
+     ...);
+  }
+  d4_fence();
+}
+
+template <int S>
+__device__ __forceinline__ void d4f_run(uint32_t (&a)[S], uint32_t* st, uint32_t* kb, const LaneScratch& tl,
+                                        const uint32_t* __restrict__ prog, int nprog, const uint32_t* __restrict__ kf,
+                                        const uint32_t* x1, const uint32_t (&m)[S], uint32_t mprime, int tig) {
+  constexpr int TQ = tile_quads<S>();
+  using Q = std::make_integer_sequence<int, TQ>;
+  const bool odd = tig != 0;
+  // the table's base (A~, 0), the multiplier A~ kept in the LDS A row by the table's products (LOP_B_READY)
+  d4r_tile_store<S>(tl, 0, a, Q{});
+  d4_fence();
+  if (!odd) {
+#pragma unroll
+    for (int j = 0; j < S; ++j) st[j] = a[j];
+  }
+#pragma unroll
+  for (int j = 0; j < S; ++j) a[j] = odd ? 0u : a[j];
+  d4_fence();
+#pragma unroll 1
+  for (int i = 0; i < nprog; ++i) {
+    const uint32_t op = lane_op(prog, i);
+    if (op & LOP_A_FROM_T) {
+      const int k = (op >> 16) & 0xFF;
+      d4r_tile_load<S>(tl, k, a, Q{});
+      if (k == 0) {   // tile 0's odd component is B_c; the entry is (A~, 0)
+#pragma unroll
+        for (int j = 0; j < S; ++j) a[j] = odd ? 0u : a[j];
+      }
+    }
+    if (op & LOP_IOTA) {   // iota = Y' mod p (any representative < 2p) -> the LDS B row
+      d4_fence();
+      if (!odd) {
+#pragma unroll
+        for (int j = 0; j < S; ++j) st[S + j] = a[j];
+      }
+      d4_fence();
+    }
+    uint64_t P[S];
+    if (op & LOP_SQR) {
+      if (op & LOP_PREFETCH) d4f_mult_load<S>(tl, (op >> 8) & 0xFF, st, odd, Q{});
+#pragma unroll
+      for (int j = 0; j < S; ++j) P[j] = odd ? (uint64_t)x1[j] : 0ull;
+      d4r_sqr_pass<S>(P, a, tig, m, mprime, odd, std::make_integer_sequence<int, S>{});
+    } else {
+      if (op & LOP_B_CONST) {
+        d4_fence();
+        if (!odd) {
+#pragma unroll
+          for (int j = 0; j < S; ++j) st[j] = j == 0 ? 1u : 0u;
+        }
+        d4_fence();
+      } else if (!(op & LOP_B_READY)) {
+        d4f_mult_load<S>(tl, (op >> 8) & 0xFF, st, odd, Q{});
+      }
+      // (A_x + p B_x)(a, 0): U = REDC(A_x a) (even), REDC(B_x a - m) (odd)
+#pragma unroll
+      for (int j = 0; j < S; ++j) P[j] = 0;
+      d4_pass<S>(P, a, st, 0, m, mprime, odd, std::make_integer_sequence<int, S>{});
+    }
+    lane::normalize<S>(P, a);
+    if (op & LOP_STORE) d4r_tile_store<S>(tl, op >> 24, a, Q{});
+  }
+  // the closing Horner sum (odd lane; LDS: st = [w][iota], kb = K'_t); a holds (1 + p G), also in tile D4F_G
+#pragma unroll 1
+  for (int s = 0; s < D4F_HORNER; ++s) {
+    const bool first = s == 0, last = s == D4F_HORNER - 1;
+    const bool cj = !first && !last && (s & 1);   // c_j = REDC(H_t K'_t)
+    const int j = LANE_NTILE - 1 - (s - 1) / 2;
+    uint64_t P[S];
+    const uint32_t* dig;
+    if (cj) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < S; i += blockDim.x) kb[i] = kf[j * S + i];
+      __syncthreads();
+      d4r_tile_load<S>(tl, j, a, Q{});
+#pragma unroll
+      for (int i = 0; i < S; ++i) P[i] = 0;
+      dig = kb;
+    } else if (first) {   // w = REDC(iota iota)
+#pragma unroll
+      for (int i = 0; i < S; ++i) a[i] = st[S + i];
+#pragma unroll
+      for (int i = 0; i < S; ++i) P[i] = 0;
+      dig = st + S;
+    } else if (!last) {   // acc = REDC(c_j + acc w)
+#pragma unroll
+      for (int i = 0; i < S; ++i) P[i] = a[i];
+      if (j == LANE_NTILE - 1) {
+#pragma unroll
+        for (int i = 0; i < S; ++i) a[i] = 0;
+      } else {
+        d4r_tile_load<S>(tl, D4F_ACC, a, Q{});
+      }
+      dig = st;
+    } else {              // delta = REDC(acc iota)
+      d4r_tile_load<S>(tl, D4F_ACC, a, Q{});
+#pragma unroll
+      for (int i = 0; i < S; ++i) P[i] = 0;
+      dig = st + S;
+    }
+    d4_pass<S>(P, a, dig, 0, m, mprime, false, std::make_integer_sequence<int, S>{});
+    lane::normalize<S>(P, a);
+    if (first) {
+      d4_fence();
+      if (!odd) {
+#pragma unroll
+        for (int i = 0; i < S; ++i) st[i] = a[i];
+      }
+      d4_fence();
+    } else if (!last && !cj) {
+      d4r_tile_store<S>(tl, D4F_ACC, a, Q{});
+    }
+  }
+  // output (A, G + delta): G < 2p, delta < 2p
+  {
+    uint32_t g[S];
+    d4r_tile_load<S>(tl, D4F_G, g, Q{});
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      const uint32_t v = g[i] + (odd ? a[i] : 0u) + c;
+      a[i] = v & lane::LMASK;
+      c = v >> lane::LB;
+    }
+  }
+}
+
 template <int S>
 __global__ __launch_bounds__(LANE_BLOCK, 2) void k_dec4_pow(Dec4Params p) {
   constexpr int TQ = tile_quads<S>();
   using Q = std::make_integer_sequence<int, TQ>;
-  __shared__ uint32_t lds[D4_PAIRS * D4R_SLOT + S];
+  __shared__ uint32_t lds[D4_PAIRS * D4R_SLOT + 2 * S];
   const int half = blockIdx.y;
   const Dec4Half* H = p.halves + half;
   uint32_t m[S];
@@ -292,7 +458,9 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_dec4_pow(Dec4Params p) {
   const uint32_t mprime = H->mprime;
   const int nprog = H->nprog;
   const uint32_t* prog = H->prog;
+  const uint32_t* kf = H->kf;
   uint32_t* x1 = lds + D4_PAIRS * D4R_SLOT;   // (1 - R) mod p_h: the odd row's start in squares (LDS: no SGPRs)
+  uint32_t* kb = x1 + S;                       // K'_t of the current Horner step (block-wide)
   for (int i = threadIdx.x; i < S; i += blockDim.x) x1[i] = H->X1[i];
   __syncthreads();
   const int tig = threadIdx.x & 1;
@@ -306,11 +474,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_dec4_pow(Dec4Params p) {
     uint32_t a[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) a[i] = p.x[((size_t)half * 2 * S + tig * S + i) * p.n + ee];
-    d4r_tile_store<S>(tl, 0, a, Q{});
-    d4r_run<S>(a, st, tl, prog, nprog, x1, m, mprime, tig, [&](uint32_t* dst) {   // (1, 0): leave Montgomery form
-#pragma unroll
-      for (int j = 0; j < S; ++j) dst[j] = (tig == 0 && j == 0) ? 1u : 0u;
-    });
+    d4f_run<S>(a, st, kb, tl, prog, nprog, kf, x1, m, mprime, tig);
     if (valid) {
 #pragma unroll
       for (int i = 0; i < S; ++i) p.x[((size_t)half * 2 * S + tig * S + i) * p.n + e] = a[i];

@@ -123,6 +123,37 @@ __device__ __forceinline__ void mont_mul(uint32_t (&A)[S], uint32_t (&B)[S], Get
   lane::normalize<S>(P2, B);
 }
 
+// ---- two B-free operands against two pair constants at once: (X1, 0) C1 + (X2, 0) C2, times R^-1 (k_fbp_fin's
+// w_q q^-2 = A_q q^-2 + B_q q^-1). Lock-step rows as in mont_mul: P1 += X1 c1a_J + X2 c2a_J, P2 += X1 c1b_J + X2 c2b_J,
+// one reduction for both products (6 S^2 MACs, against 4 S^2 + 4 S^2 for two products); per position and digit at most
+// two products and one reduction product, within mont_mul's bound. get(J) returns (c1a, c1b, c2a, c2b) of digit J.
+template <int S, int J, class Get>
+__device__ __forceinline__ void mul2_step(uint64_t (&P1)[S], uint64_t (&P2)[S], const uint32_t (&X1)[S], const uint32_t (&X2)[S],
+                                          Get& get, const uint32_t (&m)[S], uint32_t mprime) {
+  const uint4 d = get(std::integral_constant<int, J>{});
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    P1[(i + J) % S] += (uint64_t)X1[i] * d.x + (uint64_t)X2[i] * d.z;
+    P2[(i + J) % S] += (uint64_t)X1[i] * d.y + (uint64_t)X2[i] * d.w;
+  }
+  red2<S, J>(P1, P2, m, mprime);
+}
+template <int S, class Get, int... Js>
+__device__ __forceinline__ void mul2_all(uint64_t (&P1)[S], uint64_t (&P2)[S], const uint32_t (&X1)[S], const uint32_t (&X2)[S],
+                                         Get& get, const uint32_t (&m)[S], uint32_t mprime, std::integer_sequence<int, Js...>) {
+  (mul2_step<S, Js>(P1, P2, X1, X2, get, m, mprime), ...);
+}
+// (X1, X2) <- the pair (U, V) of (X1 C1 + X2 C2) R^-1 mod p^2 (X1, X2 < 2p; C1, C2 canonical pairs): U, V < 2p
+template <int S, class Get>
+__device__ __forceinline__ void mont_mul2_a0(uint32_t (&X1)[S], uint32_t (&X2)[S], Get&& get, const uint32_t (&m)[S],
+                                             uint32_t mprime) {
+  uint64_t P1[S], P2[S];
+  zero2<S>(P1, P2);
+  mul2_all<S>(P1, P2, X1, X2, get, m, mprime, std::make_integer_sequence<int, S>{});
+  lane::normalize<S>(P1, X1);
+  lane::normalize<S>(P2, X2);
+}
+
 // ---- products by a pair (a, 0): a factored table row (kernels_fbp.hpp)
 // (A + p B) a R^-1 == U + p REDC(B a - m) (mod p^2): the A1 B2 term is gone, 4 S^2 MACs. Run as two CIOS passes
 // over the digits of a -- U = REDC(A a), handing each reduction digit q1_j to put(j, q1_j), then REDC(B a - m),

@@ -1054,11 +1054,21 @@ static int ensure_fb(pai_ctx* c) {
         const std::vector<uint32_t> v = mul_pow2_mod(mod(other, P), (size_t)FBP_CB * k, P).limbs(ps, LB);
         nm_p.insert(nm_p.end(), v.begin(), v.end());
       }
-      uint32_t *pp, *pone, *pbases, *pnm, *ppbig;
+      // position 0's lo entries are multiplied by kappa R (FbpHalf::kapR): kappa = q^-2 mod p^2 for the p half, so
+      // that the sampler leaves w_p q^-2 for k_fbp_fin; 1 for the q half
+      std::vector<uint32_t> kap_p;
+      if (h == 0) {
+        const HBig kap = inv_mod(sq[1], sq[0]);
+        if (kap.is_zero()) return fb_unavailable(c, "q^2 not invertible mod p^2");
+        split(mul_pow2_mod(kap, RS, m2), kap_p);
+      }
+      uint32_t *pp, *pone, *pbases, *pnm, *ppbig, *pkap = nullptr;
       if ((rc = upload_fb(c, P.limbs(ps, LB), &pp)) || (rc = upload_fb(c, one_p, &pone)) ||
           (rc = upload_fb(c, bases_p, &pbases)) || (rc = upload_fb(c, nm_p, &pnm)) ||
-          (rc = upload_fb(c, mul(P, pow2(FBP_PB)).limbs(ps, LB), &ppbig)))
+          (rc = upload_fb(c, mul(P, pow2(FBP_PB)).limbs(ps, LB), &ppbig)) ||
+          (h == 0 && (rc = upload_fb(c, kap_p, &pkap))))
         return fb_unavailable(c, pai_last_error());
+      if (h != 0) pkap = pone;
       // factored rows (kernels_fbp.hpp): inverse tables of the lo/hi entries' A parts and the batch inversion's
       // scratch -- released with lohi
       void *vinv = nullptr, *vpre = nullptr, *vcv = nullptr;
@@ -1071,7 +1081,7 @@ static int ensure_fb(pai_ctx* c) {
       for (void* q : {vinv, vpre, vcv}) fb_scratch.push_back(q);
       pcval[h] = (uint32_t*)vcv;
       pv[h] = FbpHalf{(const uint4*)t[h], pp, pone, pbases, dlohi, pnm, ppbig, mont_prime(P, LB),
-                      (uint32_t*)vinv, (uint32_t*)vpre, (uint32_t*)vcv};
+                      (uint32_t*)vinv, (uint32_t*)vpre, (uint32_t*)vcv, pkap};
       if (shoup) {
         const HBig R2 = pow2(2 * RS);
         const HBig mu = div_big(R2, P);
@@ -1170,7 +1180,7 @@ static int ensure_fb(pai_ctx* c) {
       std::vector<FbsConst> fcv(fc, fc + 2);
       if ((rc = upload_fb(c, fcv, &c->d_fbs_cst))) return fb_unavailable(c, pai_last_error());
     }
-    // k_fbp_fin (kernels_fbp.hpp): (q R)^, (q^-2 R)^ as pairs over p, then q, q^2, p q^2, 4p, 3p
+    // k_fbp_fin (kernels_fbp.hpp): (q^-1 R)^, (q^-2 R)^ as pairs over p, then q, q^2, p q^2, 2p, 3p
     const HBig &P = primes[0], &Q = primes[1];
     const size_t RS = (size_t)LB * ps;
     std::vector<uint32_t> cs;
@@ -1183,12 +1193,14 @@ static int ensure_fb(pai_ctx* c) {
       put(sub(v, mul(qt, P)), ps);
       put(qt, ps);
     };
-    put_pair(mul_pow2_mod(mod(Q, sq[0]), RS, sq[0]));
+    const HBig qinv = inv_mod(mod(Q, sq[0]), sq[0]);
+    if (qinv.is_zero()) return fb_unavailable(c, "q not invertible mod p^2");
+    put_pair(mul_pow2_mod(qinv, RS, sq[0]));
     put_pair(mul_pow2_mod(coef, RS, sq[0]));
     put(Q, ps);
     put(sq[1], 2 * ps);
     put(mul(P, sq[1]), 3 * ps);
-    put(mul(P, HBig(4)), ps);
+    put(mul(P, HBig(2)), ps);
     put(mul(P, HBig(3)), ps);
     if ((rc = upload_fb(c, cs, &c->d_fbp_fin_cs))) return fb_unavailable(c, pai_last_error());
     c->d_fbp_fin_p = const_cast<uint32_t*>(pv[0].p);

@@ -45,6 +45,9 @@ struct FbpHalf {
   uint32_t* inv;           // [K][2][FB_LO][S]: (A of lo/hi entry)^-1 R mod p_h
   uint32_t* pre;           // [2K][2^max(LO,HI)][S] prefix products
   uint32_t* cval;          // [2K][S]: each chain's product, then its inverse R^2 (host)
+  // pair of kappa R mod p_h^2, multiplied into position 0's lo entries (k_fbp_lohi): kappa = q^-2 mod p^2 for the p
+  // half, so that every row of position 0 carries it and k_fbp_fin receives w_p q^-2; kappa = 1 (oneR) for the q half
+  const uint32_t* kapR;
 };
 
 // The canonical pairs k_fbp leaves for k_fbp_fin, in tiles of 64 elements: [half][i / 64][2S limbs][i % 64] (n
@@ -483,26 +486,43 @@ struct FbpFinParams {
   const uint32_t* pr;      // canonical pairs from k_fbp in 64-element tiles (fbp_pair_index; half 0: p, half 1: q)
   long long n;
   const uint32_t* p;       // S limbs of p
-  const uint32_t* cs;      // 12 S words: (qR)^ [2S], (q^-2 R)^ [2S], q [S], q^2 [2S], p q^2 [3S], 4p [S], 3p [S]
+  const uint32_t* cs;      // 12 S words: (q^-1 R)^ [2S], (q^-2 R)^ [2S], q [S], q^2 [2S], p q^2 [3S], 2p [S], 3p [S]
   uint32_t mprime;         // -p^-1 mod 2^28
   uint32_t* ct;
   int ct_words;
 };
 
 template <int S>
-struct FbpFinDigits {   // multiplier digit pairs of a pair constant in LDS (A limbs, then B), read one digit ahead
-  const uint32_t* d;    // (the read for digit J+1 is issued in digit J's region, past its sched_barrier)
-  uint32_t na = 0, nb = 0;
+struct FbpFin2Digits {   // digits (c1a, c1b, c2a, c2b) of C1 = (q^-2 R)^ at d + 2S and C2 = (q^-1 R)^ at d, one digit ahead
+  const uint32_t* d;
+  uint4 nx = make_uint4(0u, 0u, 0u, 0u);
   template <int J>
-  __device__ __forceinline__ uint2 operator()(std::integral_constant<int, J>) {
-    const uint2 r = J == 0 ? make_uint2(d[0], d[S]) : make_uint2(na, nb);
-    if constexpr (J + 1 < S) {
-      na = d[J + 1];
-      nb = d[S + J + 1];
-    }
+  __device__ __forceinline__ uint4 operator()(std::integral_constant<int, J>) {
+    const uint4 r = J == 0 ? make_uint4(d[2 * S], d[3 * S], d[0], d[S]) : nx;
+    if constexpr (J + 1 < S) nx = make_uint4(d[2 * S + J + 1], d[3 * S + J + 1], d[J + 1], d[S + J + 1]);
     return r;
   }
 };
+
+// the pair (A, B), A < 3p, B < 4p (B + 2 < 4p once A's multiples of p moved in) -> canonical A, B < p
+template <int S>
+__device__ __forceinline__ void fbpf_canon3(uint32_t (&A)[S], uint32_t (&B)[S], const uint32_t (&m)[S]) {
+#pragma unroll 1
+  for (int r = 0; r < 2; ++r) {
+    uint32_t d[S];
+    const bool lt = lane::sub<S>(A, m, d);
+    uint32_t c = lt ? 0u : 1u;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      A[i] = lt ? A[i] : d[i];
+      const uint32_t v = B[i] + c;
+      B[i] = v & lane::LMASK;
+      c = v >> lane::LB;
+    }
+  }
+#pragma unroll 1
+  for (int r = 0; r < 3; ++r) lane::cond_sub<S>(B, m);
+}
 
 // limb K of A_q + q B_q + q^2 H_A + p q^2 H_B (constants q, q^2, p q^2 at cq, cq + S, cq + 3S in LDS)
 template <int S, int K>
@@ -681,7 +701,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
 #pragma unroll
   for (int j = 0; j < S; ++j) m[j] = p.p[j];
   const uint32_t mprime = p.mprime;
-  const uint32_t* p4 = cs + 10 * S;
+  const uint32_t* p2 = cs + 10 * S;
   const uint32_t* p3 = cs + 11 * S;
   const int lane = threadIdx.x & 63;
   uint32_t* wpp = wpl + (threadIdx.x >> 6) * 2 * S * 64;   // limb j of this lane's w_p at wpp[64 j + lane]
@@ -700,15 +720,17 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous element's reads of the tile are done
       fbpf_tile_dma<S>(p.pr, e0, 0, p.n, lb, lane);
     }
-    // X = q B_q mod p^2
+    // Y = w_q q^-2 mod p^2 = A_q q^-2 + B_q q^-1: one lock-step pass over the two B-free operands (bn_pair.hpp
+    // mont_mul2_a0), 6 S^2 MACs
     uint32_t xa[S], xb[S];
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      xa[j] = pq[(S + j) * 64];
-      xb[j] = 0u;
+      xa[j] = pq[j * 64];
+      xb[j] = pq[(S + j) * 64];
     }
-    pair::mont_mul<S>(xa, xb, FbpFinDigits<S>{cs}, m, mprime);
-    // D = w_p - w_q as a pair with non-negative parts
+    pair::mont_mul2_a0<S>(xa, xb, FbpFin2Digits<S>{cs}, m, mprime);
+    // h = w_p q^-2 - Y (the p half's position-0 rows carry q^-2, FbpHalf::kapR), as the pair
+    // D = (W_A + 2p - Y_A, W_B + 3p - Y_B - 2): parts in (0, 3p) and (p - 2, 4p), then canonical
     {
       lds_dma_wait();   // the w_p tile landed
       int tx = threadIdx.x;
@@ -717,17 +739,15 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
       int64_t ca = 0, cb = 0;
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        const int64_t va = (int64_t)wq[j * 64] + (int64_t)p4[j] - (int64_t)pq[j * 64] - (int64_t)xa[j] + ca;
-        const int64_t vb = (int64_t)wq[(S + j) * 64] + (int64_t)p3[j] - (int64_t)xb[j] - (j == 0 ? 4 : 0) + cb;
+        const int64_t va = (int64_t)wq[j * 64] + (int64_t)p2[j] - (int64_t)xa[j] + ca;
+        const int64_t vb = (int64_t)wq[(S + j) * 64] + (int64_t)p3[j] - (int64_t)xb[j] - (j == 0 ? 2 : 0) + cb;
         xa[j] = (uint32_t)va & lane::LMASK;
         xb[j] = (uint32_t)vb & lane::LMASK;
         ca = va >> lane::LB;
         cb = vb >> lane::LB;
       }
     }
-    // h = D q^-2 mod p^2, canonical
-    pair::mont_mul<S>(xa, xb, FbpFinDigits<S>{cs + 2 * S}, m, mprime);
-    pair::canon<S>(xa, xb, m);
+    fbpf_canon3<S>(xa, xb, m);
     {   // w_p is consumed: the wave's w_q tile -> the same LDS tile, read by the final sum (instead of w_q from HBM a
         // second time); issued after h's product, which holds every register
       const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -782,7 +802,8 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
 
 // ---------------------------------------------------------------- per-key table in pair form
 // k_fbp_lohi: per position k, lo[j] = B_k^j R (j < 2^LO) and hi[j] = B_k^(2^LO j) R (j < 2^(W-LO)) by
-// square-and-multiply from R (the pair of one); k_fbp_inv_*: the inverses of their A parts mod p_h; k_fbp_fill:
+// square-and-multiply from R (the pair of one; position 0's lo entries times kappa R, FbpHalf::kapR, so that
+// T_0[d] = kappa B_0^d); k_fbp_inv_*: the inverses of their A parts mod p_h; k_fbp_fill:
 // T_k[d] R = lo[d & (2^LO - 1)] hi[d >> LO] R^-1, one pair product per entry, factored (header) and stored as words.
 template <int S>
 __global__ __launch_bounds__(LANE_BLOCK) void k_fbp_lohi(const FbpHalf* halves, int K, int W) {
@@ -806,6 +827,11 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_fbp_lohi(const FbpHalf* halves, 
         if ((j >> b) & 1u)
           pair::mont_mul<S>(A, B, [&](auto J) { return make_uint2(x[decltype(J)::value], x[S + decltype(J)::value]); }, m,
                             H->mprime);
+      }
+      if (k == 0 && s == 0) {   // position 0's lo entries carry kappa
+        const uint32_t* kr = H->kapR;
+        pair::mont_mul<S>(A, B, [&](auto J) { return make_uint2(kr[decltype(J)::value], kr[S + decltype(J)::value]); }, m,
+                          H->mprime);
       }
       uint32_t* o = H->lohi + (((size_t)k * 2 + s) * FB_LO + j) * 2 * S;
 #pragma unroll

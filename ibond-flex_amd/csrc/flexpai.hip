@@ -1050,9 +1050,12 @@ static int ensure_fb(pai_ctx* c) {
         for (int q = 0; q < W; ++q) y = M2.mul(y, y);
       }
       const HBig other = primes[1 - h];
+      std::vector<uint32_t> nmr_p;   // the same times R (k_fbs: gamma R joins the b sum)
       for (int k = 0; k < FBP_NC; ++k) {
         const std::vector<uint32_t> v = mul_pow2_mod(mod(other, P), (size_t)FBP_CB * k, P).limbs(ps, LB);
         nm_p.insert(nm_p.end(), v.begin(), v.end());
+        const std::vector<uint32_t> r = mul_pow2_mod(mod(other, P), (size_t)FBP_CB * k + RS, P).limbs(ps, LB);
+        nmr_p.insert(nmr_p.end(), r.begin(), r.end());
       }
       // position 0's lo entries are multiplied by kappa R (FbpHalf::kapR): kappa = q^-2 mod p^2 for the p half, so
       // that the sampler leaves w_p q^-2 for k_fbp_fin; 1 for the q half
@@ -1062,9 +1065,9 @@ static int ensure_fb(pai_ctx* c) {
         if (kap.is_zero()) return fb_unavailable(c, "q^2 not invertible mod p^2");
         split(mul_pow2_mod(kap, RS, m2), kap_p);
       }
-      uint32_t *pp, *pone, *pbases, *pnm, *ppbig, *pkap = nullptr;
+      uint32_t *pp, *pone, *pbases, *pnm, *pnmr, *ppbig, *pkap = nullptr;
       if ((rc = upload_fb(c, P.limbs(ps, LB), &pp)) || (rc = upload_fb(c, one_p, &pone)) ||
-          (rc = upload_fb(c, bases_p, &pbases)) || (rc = upload_fb(c, nm_p, &pnm)) ||
+          (rc = upload_fb(c, bases_p, &pbases)) || (rc = upload_fb(c, nm_p, &pnm)) || (rc = upload_fb(c, nmr_p, &pnmr)) ||
           (rc = upload_fb(c, mul(P, pow2(FBP_PB)).limbs(ps, LB), &ppbig)) ||
           (h == 0 && (rc = upload_fb(c, kap_p, &pkap))))
         return fb_unavailable(c, pai_last_error());
@@ -1081,7 +1084,7 @@ static int ensure_fb(pai_ctx* c) {
       for (void* q : {vinv, vpre, vcv}) fb_scratch.push_back(q);
       pcval[h] = (uint32_t*)vcv;
       pv[h] = FbpHalf{(const uint4*)t[h], pp, pone, pbases, dlohi, pnm, ppbig, mont_prime(P, LB),
-                      (uint32_t*)vinv, (uint32_t*)vpre, (uint32_t*)vcv, pkap};
+                      (uint32_t*)vinv, (uint32_t*)vpre, (uint32_t*)vcv, pkap, pnmr};
       if (shoup) {
         const HBig R2 = pow2(2 * RS);
         const HBig mu = div_big(R2, P);

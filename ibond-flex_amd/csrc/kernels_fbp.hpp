@@ -48,6 +48,7 @@ struct FbpHalf {
   // pair of kappa R mod p_h^2, multiplied into position 0's lo entries (k_fbp_lohi): kappa = q^-2 mod p^2 for the p
   // half, so that every row of position 0 carries it and k_fbp_fin receives w_p q^-2; kappa = 1 (oneR) for the q half
   const uint32_t* kapR;
+  const uint32_t* nmR;     // [NC][S] (n / p_h) 2^(CB c) R mod p_h: k_fbs's start gamma R in the b sum (kernels_fbs.hpp)
 };
 
 // The canonical pairs k_fbp leaves for k_fbp_fin, in tiles of 64 elements: [half][i / 64][2S limbs][i % 64] (n

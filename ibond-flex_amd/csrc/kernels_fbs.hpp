@@ -129,6 +129,47 @@ __device__ __forceinline__ void fbs_reduce_est(uint32_t (&x)[S], const uint32_t 
   }
 }
 
+// the S limbs of a from the pair's row (a reader over quads 0 .. QA-1)
+template <int S, class Rd, int... Ts>
+__device__ __forceinline__ void fbs_read_limbs(uint32_t (&x)[S], Rd& rd, std::integer_sequence<int, Ts...>) {
+  ((x[Ts] = rd(std::integral_constant<int, Ts>{})), ...);
+}
+
+template <int S, int HW, int... Js>
+__device__ __forceinline__ void fbs_gamma_pick(const uint32_t (&g)[S], bool odd, uint32_t (&w)[HW], uint32_t& wc,
+                                               std::integer_sequence<int, Js...>) {
+  ((w[Js] = odd ? fb_word<S, HW + Js>(g) : fb_word<S, Js>(g)), ...);
+  wc = odd ? fb_word<S, 2 * HW>(g) : 0u;
+}
+
+// The start of the b sum: c0 = 1 + n M = 1 + p_h gamma, gamma = (n / p_h) M mod p_h, is the factored value
+// 1 (1 + p_h gamma), so the product starts from the first row's (a_0, 0) and gamma R joins the b R words: this lane's
+// words tig HW .. tig HW + HW - 1 of gamma R (unreduced: a sum of 8-bit chunks of |M| times (n / p_h) 2^(8 c) R mod p_h,
+// < 2040 p_h, or 2^11 p_h minus that for M < 0) and, in the odd lane, word PW as the carry word. With the K rows'
+// b R words (< p_h each) the sum stays below 2^12 p_h <= R = 2^(28 S): fbp_apply_bsum's S-limb operand.
+template <int S, int HW>
+__device__ __forceinline__ void fbs_gamma_words(int64_t M, const FbpHalf* __restrict__ H, bool odd, uint32_t (&w)[HW],
+                                                uint32_t& wc) {
+  const bool neg = M < 0;
+  const uint64_t mag = neg ? (uint64_t)0 - (uint64_t)M : (uint64_t)M;
+  uint32_t mc[FBP_NC];
+#pragma unroll
+  for (int c = 0; c < FBP_NC; ++c) mc[c] = (uint32_t)((mag >> (FBP_CB * c)) & ((1ull << FBP_CB) - 1ull));
+  const uint32_t* nm = opaque_uniform(H->nmR);
+  const uint32_t* pb = opaque_uniform(H->pbig);
+  uint32_t g[S];
+  int64_t carry = 0;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    uint64_t s = 0;
+#pragma unroll
+    for (int c = 0; c < FBP_NC; ++c) s += (uint64_t)nm[c * S + j] * mc[c];
+    const int64_t v = carry + (neg ? (int64_t)pb[j] - (int64_t)s : (int64_t)s);
+    g[j] = (uint32_t)v & lane::LMASK;
+    carry = v >> lane::LB;
+  }
+  fbs_gamma_pick<S, HW>(g, odd, w, wc, std::make_integer_sequence<int, HW>{});
+}
 // ---------------------------------------------------------------- the sampler on split pairs
 // Element-half e on lanes 2e, 2e+1 (kernels_sgp.hpp's layout): the even lane keeps A, the odd lane B, and both run
 // the same Shoup pass on their own component at once -- step 1 (their quotient), then step 2, the odd lane's
@@ -233,17 +274,10 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbs(FbpParams p) {
       p.exp[e] = ex;
       if (p.status) p.status[e] = stt;
     }
-    uint32_t X[S];   // even lane: A; odd lane: B (the start c0 = (1, gamma))
-    {
-      uint32_t A0[S], B0[S];
-      fbp_c0<S>(M, H, A0, B0);
-#pragma unroll
-      for (int j = 0; j < S; ++j) X[j] = odd ? B0[j] : A0[j];
-    }
+    uint32_t X[S];   // even lane: A; odd lane: B -- (a_0, 0) from the first row (below)
     const uint32_t* dg = p.digits + (size_t)half * K * p.n + ee;
-    uint32_t bsw[HW], bcc = 0;
-#pragma unroll
-    for (int j = 0; j < HW; ++j) bsw[j] = 0;
+    uint32_t bsw[HW], bcc;   // this lane's half of the b sum, started at gamma R (c0 = 1 (1 + p gamma), factored)
+    fbs_gamma_words<S, HW>(M, H, odd, bsw, bcc);
     static_assert(G::QB / 2 == HW / 4, "b R quads per lane");
     fbp_u32x4 bv[G::QB / 2];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous element's reads of both buffers are done
@@ -271,6 +305,13 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbs(FbpParams p) {
         for (int q = 0; q < G::QB / 2; ++q) bv[q] = fbp_u32x4{0u, 0u, 0u, 0u};
       }
       __builtin_amdgcn_sched_barrier(0);
+      if (k == 0) {   // c0 T_0 = (1 + p gamma) a_0 (1 + p b_0): the pair (a_0, 0), the factors in the b sum -- no product
+        FbsPairReader<S, G::QA, 0, false, 1> ra{cur};
+        fbs_read_limbs<S>(X, ra, std::make_integer_sequence<int, S>{});
+#pragma unroll
+        for (int i = 0; i < S; ++i) X[i] = odd ? 0u : X[i];
+        continue;
+      }
       uint32_t q[S];
       {
         FbsPairReader<S, G::QAP, G::QA, true, 1> r1{cur};

@@ -119,12 +119,14 @@ def work_fbp(nb: int, digits: int) -> dict:
 
 
 def work_fbs(nb: int, digits: int) -> dict:
-    """The pair fixed-base path on Shoup rows (kernels_fbs.hpp): k_fbs = K Shoup products per half (s = nb/64 limbs of
-    p_h; per component a quotient from the top s (s + 1) / 2 columns of X a' and the low s (s + 1) / 2 columns of X a
-    and of Q p: 3 s^2 + 3 s per pair) + the c0 chunk sum (s^2) + the b-sum correction (M(s)); k_fbp_fin as work_fbp."""
+    """The pair fixed-base path on Shoup rows (kernels_fbs.hpp): k_fbs = K - 1 Shoup products per half (the first row
+    is the start (a_0, 0), c0's gamma R joins the b sum; s = nb/64 limbs of p_h; per component a quotient from the top
+    s (s + 1) / 2 columns of X a' and the low s (s + 1) / 2 columns of X a and of Q p: 3 s^2 + 3 s per pair) + the c0
+    chunk sum (s^2) + the b-sum correction (M(s)); k_fbp_fin: Y = w_q q^-2 in one two-operand pass (6 s^2) and the
+    final sum (6 s^2)."""
     s = nb // 64
-    return {"k_fb_digits": 0.0, "k_fbs": float(2 * (digits * (3 * s * s + 3 * s) + s * s + _M(s))),
-            "k_fbp_fin": float(15 * s * s)}
+    return {"k_fb_digits": 0.0, "k_fbs": float(2 * ((digits - 1) * (3 * s * s + 3 * s) + s * s + _M(s))),
+            "k_fbp_fin": float(12 * s * s)}
 
 
 def work_fbg(nb: int, digits: int) -> dict:
@@ -1228,8 +1230,8 @@ def main():
                      "unit": "TMAC/s", "frac": achieved / INT_MAC_PEAK,
                      "traffic": load_traffic(dom, N, nb, fb_info[3] if (use_fb and dom in ("k_fb", "k_fbp", "k_fbs", "k_fbg", "k_fbgp", "k_sgp")) else None),
                      "kernel": dom, "kernel_ms": dom_ms,
-                     "work_per_unit": (f"{dom_work:.4g} MAC per element: the Shoup-row count (K = {fb_info[2]} Shoup products "
-                                       f"mod p_h^2 per half, 3 s^2 + 3 s each over s = nb/64 32-bit limbs of p_h, + the c0 sum "
+                     "work_per_unit": (f"{dom_work:.4g} MAC per element: the Shoup-row count (K - 1 = {fb_info[2] - 1} Shoup products "
+                                       f"mod p_h^2 per half (the first of K rows is the start), 3 s^2 + 3 s each over s = nb/64 32-bit limbs of p_h, + the c0 sum "
                                        f"and the b-sum correction, kernels_fbs.hpp), not SURVEY.md §8d's W_enc"
                                        if dom == "k_fbs" else
                                        f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} products by "

@@ -3342,8 +3342,8 @@ int pai_decrypt(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, do
 }
 
 // ------------------------------------------------------------------ debugging hook (tests / tools only)
-// Copies the per-half sampler outputs (c0 G_h^a_h mod h^2) of the last fixed-base chunk: limbs [2][SB][n]
-// (k_fb, k_fbg), or canonical pairs [2][2S][n] with *sb = 2S when the pair tables are resident (k_fbp).
+// Copies the per-half sampler outputs (c0 G_h^a_h mod h^2) of the last fixed-base chunk: limbs [2][SB][n] (k_fb,
+// k_fbg), or canonical pairs [2][2S][n] with *sb = 2S for the pair tables (k_fbs/k_fbp; the p half times q^-2).
 extern "C" int pai_debug_fb_w(pai_ctx* c, uint32_t* out, size_t max_words, long long* n, int* sb) {
   if (!c || !c->fb_last_w) return fail(PAI_ERR_ARG, "no fixed-base output");
   CtxLock lk(c);

@@ -18,7 +18,9 @@
 //           accumulators): S (S + 1) MACs, exact because the true value lies in [0, R).
 // Shoup's bound A a / p - A a' / R in [0, A / R) keeps A < (S + 3) p and B < 2 (S + 3) p, far below R.
 // 3 S^2 + 3 S MACs per product against 4 S^2 for the Montgomery pass pair (and no q_j multiplications).
-// After the K products the b sum is applied once (fbp_apply_bsum), then the pair is reduced to canonical.
+// The first row is the start: c0 T_0 = (1 + p gamma) a_0 (1 + p b_0) is the pair (a_0, 0) with gamma R and b_0 R in the
+// b sum (fbs_gamma_words), so K - 1 products follow. After them the b sum is applied once (fbp_apply_bsum), then the
+// pair is reduced to canonical.
 #pragma once
 #include "kernels_fbp.hpp"
 

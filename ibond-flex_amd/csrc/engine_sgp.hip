@@ -1,4 +1,7 @@
 // Split-pair fixed-base sampler (kernels_sgp.hpp): instantiation and launch. LDS is static (rows + b sums).
+#ifndef FLEXPAI_XCHECK
+#define FLEXPAI_XCHECK 0   // 1: the test-only library (address guards, guard.hpp)
+#endif
 #include "engine_sgp.hpp"
 
 namespace fpai {

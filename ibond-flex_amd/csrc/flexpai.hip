@@ -145,6 +145,7 @@ struct pai_ctx {
   uint32_t* fb_last_w = nullptr;  // debugging: k_fb output of the last chunk ([2][SB][fb_last_n])
   long long fb_last_n = 0;
   uint64_t fb_table_bytes = 0;
+  GuardRec* d_guard = nullptr;  // test build: the address guards' record (guard.hpp); null in the product
   // public-key fixed-base obfuscators (kernels_pfb.hpp): device-RNG encryption without the private key.
   // Built lazily past the break-even count (or pai_ctx_public_fb_prepare); never needed for correctness.
   int pfb_state = FB_UNTRIED;
@@ -224,6 +225,7 @@ pai_ctx::~pai_ctx() {
   if (s_comp) (void)hipStreamDestroy(s_comp);
   if (s_copy) (void)hipStreamDestroy(s_copy);
   if (d_hostio) (void)hipFree(d_hostio);
+  if (d_guard) (void)hipFree(d_guard);
   for (void* p : allocs) (void)hipFree(p);
   for (void* p : priv_allocs) (void)hipFree(p);
   for (void* p : fb_mem) (void)hipFree(p);
@@ -612,8 +614,36 @@ int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** ou
     delete c;
     return rc;
   }
+#if FLEXPAI_XCHECK
+  if (hipMalloc(&c->d_guard, sizeof(GuardRec)) != hipSuccess || hipMemset(c->d_guard, 0, sizeof(GuardRec)) != hipSuccess) {
+    delete c;
+    return fail(PAI_ERR_HIP, "pai_ctx_create: guard record");
+  }
+#endif
   *out = c;
   return 0;
+}
+
+// The test build's address guards (guard.hpp): the sizes the samplers' indices must stay below, as allocated here.
+// $FLEXPAI_GUARD_INJECT=rows (test build only) passes a table of one row, so that every row index trips the guard:
+// the self-test of the mechanism (tests/test_gpu_guard.py).
+static GuardArgs guard_args(const pai_ctx* c, unsigned long long rows, unsigned long long digits, unsigned long long out,
+                            unsigned long long in) {
+  const char* inj = xcheck_env("FLEXPAI_GUARD_INJECT");
+  if (inj && std::strcmp(inj, "rows") == 0) rows = 1;
+  return GuardArgs{c->d_guard, rows, digits, out, in};
+}
+// after the guarded launches of a call: a violation fails the call with the first one's site, value and limit
+static int guard_collect(pai_ctx* c, hipStream_t st) {
+  if (!c->d_guard) return 0;
+  HIPCHK(hipStreamSynchronize(st));
+  GuardRec g{};
+  HIPCHK(hipMemcpy(&g, c->d_guard, sizeof(g), hipMemcpyDeviceToHost));
+  if (!g.hits) return 0;
+  HIPCHK(hipMemset(c->d_guard, 0, sizeof(GuardRec)));
+  return fail(PAI_ERR_HIP, std::string("address guard: ") + std::to_string(g.hits) + " violation(s), first at " +
+                               guard_site_name(g.site) + ": index " + std::to_string(g.val) + " >= limit " +
+                               std::to_string(g.lim) + " (element " + std::to_string(g.elem) + ")");
 }
 
 // Fixed-base obfuscation setup (kernels_fb.hpp): the smallest g >= 2 that generates Z_P* as far as
@@ -1228,15 +1258,18 @@ static int ensure_fb(pai_ctx* c) {
 #if FLEXPAI_XCHECK
   const hipError_t be = gpair_ok  ? fbgp_build_phase2(c->d_fbgp_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
                         : grp     ? grp_build_tables(c->d_fb_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
-                        : shoup   ? fbs_build_phase2(ps, c->d_fbp_halves, c->d_fbs_cst, (uint4*)t[0], (uint4*)t[1], K, W, nullptr)
+                        : shoup   ? fbs_build_phase2(ps, c->d_fbp_halves, c->d_fbs_cst, (uint4*)t[0], (uint4*)t[1], K, W, nullptr,
+                                                     guard_args(c, (unsigned long long)K << W, 0, 0, 0))
                         : pair_ok ? fbp_build_phase2(ps, c->d_fbp_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr)
                                   : fb_build_tables(sb, c->d_fb_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
 #else
   const hipError_t be = gpair_ok ? fbgp_build_phase2(c->d_fbgp_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
-                                 : fbs_build_phase2(ps, c->d_fbp_halves, c->d_fbs_cst, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
+                                 : fbs_build_phase2(ps, c->d_fbp_halves, c->d_fbs_cst, (uint4*)t[0], (uint4*)t[1], K, W, nullptr,
+                                                    guard_args(c, (unsigned long long)K << W, 0, 0, 0));
 #endif
   if (be != hipSuccess || hipDeviceSynchronize() != hipSuccess)
     return fb_unavailable(c, "table construction failed");
+  if (guard_collect(c, nullptr)) return fb_unavailable(c, pai_last_error());
   for (void* p : lohi) fb_scratch.push_back(p);
   for (void* p : fb_scratch) {
     c->fb_mem.erase(std::find(c->fb_mem.begin(), c->fb_mem.end(), p));
@@ -1797,6 +1830,8 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     pd.raw_bits = c->fb_raw_bits;
     pd.red = c->d_fb_red;
     pd.digits = digits;
+    const unsigned long long dig_words = (unsigned long long)2 * c->fb_K * chunk, w_words = wbytes * (size_t)fbp_npad(chunk) / 4;
+    pd.g = guard_args(c, 0, dig_words, 0, 0);
     const int gD = (int)std::min<long long>((long long)8 * c->cus, (n + FB_DIG_BLOCK - 1) / FB_DIG_BLOCK);
     stage_mark(c, 0, st);
     HIPCHK(fb_launch_digits(pd, gD, st));
@@ -1816,7 +1851,8 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     pf.status = e.status ? e.status + off : nullptr;
     const int gF = (int)std::min<long long>(gxF, (n + EPB - 1) / EPB);
     if (c->fb_pair_s) {
-      const FbpParams pp{c->d_fbp_halves, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
+      FbpParams pp{c->d_fbp_halves, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
+      pp.g = guard_args(c, (unsigned long long)pf.K << pf.W, dig_words, w_words, 0);
 #if FLEXPAI_XCHECK
       if (!c->fb_shoup) HIPCHK(fbp_launch(c->fb_pair_s, pp, gF, st));
 #endif
@@ -1826,7 +1862,8 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
       if (c->d_sgp_fb) {   // split pairs (kernels_sgp.hpp): SGP_PAIRS elements per block, grid (gx, 2)
         int occS = 1;
         sgp_occupancy(&occS);
-        const SgpParams sp{c->d_sgp_fb, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
+        SgpParams sp{c->d_sgp_fb, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
+        sp.g = guard_args(c, (unsigned long long)pf.K << pf.W, dig_words, w_words, 0);
         const long long nb = (n + SGP_PAIRS - 1) / SGP_PAIRS;
         HIPCHK(sgp_launch(sp, (int)std::max<long long>(1, std::min<long long>(nb, (long long)occS * c->cus / 2)), 2, st));
       } else {
@@ -1861,8 +1898,9 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     if (c->fb_pair_s) {   // Garner on pairs (kernels_fbp.hpp)
       int occP = 1;
       fbp_fin_occupancy(c->fb_pair_s, &occP);
-      const FbpFinParams pp{w, n, c->d_fbp_fin_p, c->d_fbp_fin_cs, c->fbp_fin_mprime, e.ct + (size_t)off * c->ct_words,
-                            c->ct_words};
+      FbpFinParams pp{w, n, c->d_fbp_fin_p, c->d_fbp_fin_cs, c->fbp_fin_mprime, e.ct + (size_t)off * c->ct_words,
+                      c->ct_words};
+      pp.g = guard_args(c, 0, 0, (unsigned long long)n * c->ct_words, w_words);
       const long long nb = (n + LANE_BLOCK - 1) / LANE_BLOCK;
       HIPCHK(fbp_launch_fin(c->fb_pair_s, pp, (int)std::max<long long>(1, std::min<long long>(nb, (long long)occP * c->cus)), st));
       stage_mark(c, 3, st);
@@ -2152,8 +2190,10 @@ static int launch_pfb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     if (c->d_sgp_pfb) {   // split pairs (kernels_sgp.hpp)
       int occS = 1;
       sgp_occupancy(&occS);
-      const SgpParams sp{c->d_sgp_pfb, n, c->pfb_K, c->pfb_W_used, digits, xw, pp.x, pp.dtype, pp.exp_mode, pp.fexp, pp.exp,
-                         pp.status};
+      SgpParams sp{c->d_sgp_pfb, n, c->pfb_K, c->pfb_W_used, digits, xw, pp.x, pp.dtype, pp.exp_mode, pp.fexp, pp.exp,
+                   pp.status};
+      sp.g = guard_args(c, (unsigned long long)c->pfb_K << c->pfb_W_used, (unsigned long long)c->pfb_K * chunk,
+                        (unsigned long long)2 * PFB_SP * chunk, 0);
       const long long nb = (n + SGP_PAIRS - 1) / SGP_PAIRS;
       HIPCHK(sgp_launch(sp, (int)std::max<long long>(1, std::min<long long>(nb, (long long)occS * c->cus)), 1, st));
     } else {
@@ -2277,7 +2317,10 @@ static int launch_pe(pai_ctx* c, const EncParams& e, hipStream_t st) {
 template <int SA, int SB>
 static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
   static_assert(SB == 2 * SA || SB == 2 * SA - 1, "stage sizes");
-  if (e.obf == PAI_OBF_RNG && c->fb_enabled && fb_wanted(c, e.n) && ensure_fb(c)) return launch_fb(c, e, st);
+  if (e.obf == PAI_OBF_RNG && c->fb_enabled && fb_wanted(c, e.n) && ensure_fb(c)) {
+    const int rc = launch_fb(c, e, st);
+    return rc ? rc : guard_collect(c, st);
+  }
   const long long N = e.n;
   const int r_words = e.obf == PAI_OBF_GIVEN ? e.r_words : e.rng_words;
   const int kchunks = (32 * r_words + LB * SA - 1) / (LB * SA);
@@ -2401,14 +2444,18 @@ int pai_encrypt_dev(pai_ctx* c, int dtype, const void* d_x, size_t N, int exp_mo
   p.nprog = c->nprog;
   p.ct_words = c->ct_words;
   hipStream_t st = (hipStream_t)stream;
-  if (obf_mode == PAI_OBF_RNG && c->fbg_ok && c->crt_enabled && c->fb_enabled && fb_wanted(c, p.n) && ensure_fb(c))
-    return launch_fb(c, p, st);
+  if (obf_mode == PAI_OBF_RNG && c->fbg_ok && c->crt_enabled && c->fb_enabled && fb_wanted(c, p.n) && ensure_fb(c)) {
+    const int rc = launch_fb(c, p, st);
+    return rc ? rc : guard_collect(c, st);
+  }
   if (obf_mode != PAI_OBF_NONE && c->crt_ok && c->crt_enabled) {
     if (c->crt_sa == 19) return launch_crt<19, 37>(c, p, st);
     if (c->crt_sa == 37) return launch_crt<37, 74>(c, p, st);
   }
-  if (obf_mode == PAI_OBF_RNG && c->pfb_enabled && pfb_supported(c) && pfb_wanted(c, p.n) && ensure_pfb(c))
-    return launch_pfb(c, p, st);
+  if (obf_mode == PAI_OBF_RNG && c->pfb_enabled && pfb_supported(c) && pfb_wanted(c, p.n) && ensure_pfb(c)) {
+    const int rc = launch_pfb(c, p, st);
+    return rc ? rc : guard_collect(c, st);
+  }
   if (obf_mode != PAI_OBF_NONE && c->pe_ok && c->ct_words == 2 * 64) return launch_pe(c, p, st);
   switch (c->tpi_e) {
     case 2: return launch_encrypt<2>(c, p, st);

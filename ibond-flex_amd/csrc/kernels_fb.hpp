@@ -33,6 +33,7 @@
 // flight (it cannot tell the LDS buffer's two uses apart).
 #pragma once
 #include "kernels_crt.hpp"
+#include "guard.hpp"
 
 namespace fpai {
 
@@ -96,6 +97,7 @@ struct FbDigitParams {
   int K, W, raw_bits;
   const FbRed* red;        // [2]
   uint32_t* digits;        // [2][K][n]
+  GuardArgs g;             // test build: digits = 2 K n
 };
 
 struct FbFinParams {
@@ -212,7 +214,7 @@ __global__ __launch_bounds__(FB_DIG_BLOCK) void k_fb_digits(FbDigitParams p) {
     for (int k = 0; k < p.K; ++k) {
       const int bit = k * p.W, wi = bit >> 5, sh = bit & 31;
       const uint64_t v = (((uint64_t)a[wi + 1] << 32) | a[wi]) >> sh;
-      p.digits[((size_t)half * p.K + k) * p.n + i] = (uint32_t)(v & mask);
+      p.digits[FPAI_GUARD_IDX(p.g, GS_DIG_OUT, ((size_t)half * p.K + k) * p.n + i, p.g.digits, i)] = (uint32_t)(v & mask);
     }
   }
 }

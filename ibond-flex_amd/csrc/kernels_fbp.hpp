@@ -70,6 +70,7 @@ struct FbpParams {
   int dtype, exp_mode, fexp;
   int32_t* exp;
   int32_t* status;
+  GuardArgs g;             // test build (guard.hpp): rows = K 2^W, digits = 2 K n, out = the pair tiles' words
 };
 
 // LDS words at a byte offset from this lane's row base (offsets past the 16-bit immediate take a second base)
@@ -491,6 +492,7 @@ struct FbpFinParams {
   uint32_t mprime;         // -p^-1 mod 2^28
   uint32_t* ct;
   int ct_words;
+  GuardArgs g;             // test build (guard.hpp): in = the pair tiles' words, out = n ct_words
 };
 
 template <int S>
@@ -672,8 +674,10 @@ __device__ __forceinline__ void fbpf_c(const uint32_t (&t)[3 * S], const uint32_
 // the wave's 64-element tile of half h's pairs (2S limbs x 64 elements, contiguous, 256-B aligned; tiles are padded
 // to 64 elements) -> the wave's LDS tile at lb, 1 KB per DMA
 template <int S>
-__device__ __forceinline__ void fbpf_tile_dma(const uint32_t* pr, long long e0, int h, long long n, uint32_t lb, int lane) {
-  uint64_t src = (uint64_t)(reinterpret_cast<const uint4*>(pr + fbp_pair_index<S>(e0, h, n)) + lane);
+__device__ __forceinline__ void fbpf_tile_dma(const uint32_t* pr, long long e0, int h, long long n, uint32_t lb, int lane,
+                                              GuardArgs gd) {
+  const size_t t0 = fbp_pair_index<S>(e0, h, n);
+  uint64_t src = (uint64_t)(reinterpret_cast<const uint4*>(pr + (FPAI_GUARD_OK(gd, GS_FIN_TILE, t0 + 2 * S * 64 - 1, gd.in, e0) ? t0 : 0)) + lane);
   constexpr int NI = (32 * S + 63) / 64, REM = (32 * S) % 64;
 #pragma unroll
   for (int g = 0; g < NI; ++g) {
@@ -710,7 +714,8 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
     const long long i = base + threadIdx.x;
     const bool valid = i < p.n;
     const long long ii = valid ? i : p.n - 1;
-    const uint32_t* pq = p.pr + fbp_pair_index<S>(ii, 1, p.n);
+    const size_t iq = fbp_pair_index<S>(ii, 1, p.n);
+    const uint32_t* pq = p.pr + (FPAI_GUARD_OK(p.g, GS_FIN_TILE, iq + (2 * S - 1) * 64, p.g.in, ii) ? iq : 0);
     // the wave's first element (wave-uniform: in SGPRs, so it costs no VGPRs across the products)
     long long e0 = base + (long long)(uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
     const bool wave_live = e0 < p.n;   // (a wave past the end computes the last element; it must not store)
@@ -719,7 +724,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
     {   // the wave's w_p tile -> LDS
       const uint32_t lb = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds_u32*)wpp);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous element's reads of the tile are done
-      fbpf_tile_dma<S>(p.pr, e0, 0, p.n, lb, lane);
+      fbpf_tile_dma<S>(p.pr, e0, 0, p.n, lb, lane, p.g);
     }
     // Y = w_q q^-2 mod p^2 = A_q q^-2 + B_q q^-1: one lock-step pass over the two B-free operands (bn_pair.hpp
     // mont_mul2_a0), 6 S^2 MACs
@@ -756,7 +761,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every lane's reads of w_p are done
       int ln = threadIdx.x & 63;
       asm volatile("" : "+v"(ln));
-      fbpf_tile_dma<S>(p.pr, e0, 1, p.n, lb, ln);
+      fbpf_tile_dma<S>(p.pr, e0, 1, p.n, lb, ln, p.g);
     }
     // c = w_q + q^2 h = A_q + q (B_q + q h), h = H_A + p H_B (fbpf_h / fbpf_t / fbpf_c)
     uint32_t t[3 * S];
@@ -794,8 +799,9 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbp_fin(FbpFinParams p) {
                                   (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cta));
       int ln = threadIdx.x & 63;
       asm volatile("" : "+v"(ln));
-      Out out{tile + (uint32_t)(ln * Out::OST * 4), tile, ctw, p.ct_words,
-              wave_live ? (int)__builtin_amdgcn_readfirstlane((uint32_t)(left < 64 ? left : 64)) : 0, ln};
+      int nv = wave_live ? (int)__builtin_amdgcn_readfirstlane((uint32_t)(left < 64 ? left : 64)) : 0;
+      if (nv > 0 && !FPAI_GUARD_OK(p.g, GS_FIN_CT, (size_t)(e0 + nv) * p.ct_words - 1, p.g.out, e0)) nv = 0;
+      Out out{tile + (uint32_t)(ln * Out::OST * 4), tile, ctw, p.ct_words, nv, ln};
       fbpf_c<S, CW>(t, qv, a1, out, std::make_integer_sequence<int, NL>{});
     }
   }

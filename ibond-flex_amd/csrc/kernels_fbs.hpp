@@ -239,6 +239,20 @@ __device__ __forceinline__ void fbs_row_fetch(const uint4* row, uint32_t lb, int
   for (int q = 0; q < QH; ++q) bv[q] = b[q];
 }
 
+#if FLEXPAI_XCHECK
+// test build (guard.hpp): digit k of element ee in half h, its offset and value checked; the row index checked
+__device__ __forceinline__ uint32_t fbs_guard_digit(const FbpParams& p, int h, int k, long long ee, unsigned int s_off,
+                                                    unsigned int s_val) {
+  const uint32_t d = p.digits[FPAI_GUARD_IDX(p.g, s_off, ((size_t)h * p.K + k) * p.n + ee, p.g.digits, ee)];
+  return (uint32_t)FPAI_GUARD_IDX(p.g, s_val, d, 1ull << p.W, ee);
+}
+#define FBS_DIGIT(k) fbs_guard_digit(p, half, (k), ee, GS_FBS_DIGIT, GS_FBS_DVAL)
+#define FBS_ROW(k, d) FPAI_GUARD_IDX(p.g, GS_FBS_ROW, ((size_t)(k) << W) + (d), p.g.rows, ee)
+#else
+#define FBS_DIGIT(k) dg[(size_t)(k) * p.n]
+#define FBS_ROW(k, d) (((size_t)(k) << W) + (d))
+#endif
+
 template <int S>
 __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbs(FbpParams p) {
   using G = FbsGeom<S>;
@@ -278,13 +292,14 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbs(FbpParams p) {
     }
     uint32_t X[S];   // even lane: A; odd lane: B -- (a_0, 0) from the first row (below)
     const uint32_t* dg = p.digits + (size_t)half * K * p.n + ee;
+    (void)dg;
     uint32_t bsw[HW], bcc;   // this lane's half of the b sum, started at gamma R (c0 = 1 (1 + p gamma), factored)
     fbs_gamma_words<S, HW>(M, H, odd, bsw, bcc);
     static_assert(G::QB / 2 == HW / 4, "b R quads per lane");
     fbp_u32x4 bv[G::QB / 2];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous element's reads of both buffers are done
-    fbs_row_fetch<S>(table + (size_t)dg[0] * TQ, wbase, tig, bv);
-    uint32_t dn = K > 1 ? dg[(size_t)p.n] : 0u;
+    fbs_row_fetch<S>(table + (size_t)FBS_ROW(0, FBS_DIGIT(0)) * TQ, wbase, tig, bv);
+    uint32_t dn = K > 1 ? FBS_DIGIT(1) : 0u;
     for (int k = 0; k < K; ++k) {
       lds_dma_wait();                                     // row k in buffer k & 1, its b R in bv, digit k+1 in dn
       {                                                   // this lane's half of the b sum
@@ -300,8 +315,8 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbs(FbpParams p) {
       }
       const uint32_t cur = pbase + (uint32_t)((k & 1) * WB);
       if (k + 1 < K) {                                    // row k+1 -> the other buffer (read two products ago: done)
-        fbs_row_fetch<S>(table + (((size_t)(k + 1) << W) + dn) * TQ, wbase + (uint32_t)(((k + 1) & 1) * WB), tig, bv);
-        dn = k + 2 < K ? dg[(size_t)(k + 2) * p.n] : 0u;
+        fbs_row_fetch<S>(table + FBS_ROW(k + 1, dn) * TQ, wbase + (uint32_t)(((k + 1) & 1) * WB), tig, bv);
+        dn = k + 2 < K ? FBS_DIGIT(k + 2) : 0u;
       } else {
 #pragma unroll
         for (int q = 0; q < G::QB / 2; ++q) bv[q] = fbp_u32x4{0u, 0u, 0u, 0u};
@@ -371,8 +386,10 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbs(FbpParams p) {
       uint32_t tb = 0;
       fbs_reduce_est<S>(B, m, tb);
       uint32_t* o = p.out + fbp_pair_index<S>(e, half, p.n);
+      if (FPAI_GUARD_OK(p.g, GS_FBS_OUT, fbp_pair_index<S>(e, half, p.n) + (2 * S - 1) * 64, p.g.out, e)) {
 #pragma unroll
-      for (int j = 0; j < 2 * S; ++j) o[j * 64] = j < S ? X[j] : B[j - S];
+        for (int j = 0; j < 2 * S; ++j) o[j * 64] = j < S ? X[j] : B[j - S];
+      }
     }
   }
 }
@@ -406,7 +423,7 @@ __device__ __forceinline__ void fbs_store_limbs(uint4* __restrict__ dst, const u
 
 template <int S>
 __global__ __launch_bounds__(LANE_BLOCK) void k_fbs_fill(const FbpHalf* halves, const FbsConst* cst, int K, int W, uint4* table0,
-                                                         uint4* table1) {
+                                                         uint4* table1, GuardArgs g) {
   using G = FbsGeom<S>;
   constexpr int TQ = fbs_row_quads<S>();
   const int ent = 1 << W;
@@ -419,7 +436,8 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_fbs_fill(const FbpHalf* halves, 
   const FbsConst* C = cst + half;
   uint4* table = half ? table1 : table0;
   const int LO = W / 2;
-  const int dl = d & ((1 << LO) - 1), dh = d >> LO;
+  const int dl = (int)FPAI_GUARD_IDX(g, GS_FILL_LOHI, (unsigned)(d & ((1 << LO) - 1)), FB_LO, d),
+            dh = (int)FPAI_GUARD_IDX(g, GS_FILL_LOHI, (unsigned)(d >> LO), FB_LO, d);
   const uint32_t* lo = H->lohi + (((size_t)k * 2 + 0) * FB_LO + dl) * 2 * S;
   const uint32_t* hi = H->lohi + (((size_t)k * 2 + 1) * FB_LO + dh) * 2 * S;
   uint32_t m[S], A[S], B[S];
@@ -507,7 +525,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_fbs_fill(const FbpHalf* halves, 
       inc = v >> lane::LB;
     }
   }
-  uint4* dst = table + ((size_t)k * ent + d) * TQ;
+  uint4* dst = table + FPAI_GUARD_IDX(g, GS_FILL_ROW, (size_t)k * ent + d, g.rows, d) * TQ;
   fbs_store_limbs<S>(dst, A, std::make_integer_sequence<int, G::QA>{});
   fbs_store_limbs<S>(dst + G::QA, ap, std::make_integer_sequence<int, G::QAP>{});   // a' < R: limb S is zero
   fbs_store_words<S>(dst + G::QA + G::QAP, bR, std::make_integer_sequence<int, G::QB>{});

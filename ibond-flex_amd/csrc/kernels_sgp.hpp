@@ -52,6 +52,7 @@ struct SgpParams {
   int dtype, exp_mode, fexp;
   int32_t* exp;            // written by half 0
   int32_t* status;
+  GuardArgs g;             // test build (guard.hpp): rows = K 2^W, digits = halves K n, out = halves 2 S n
 };
 
 // LDS word of a row's a half: DMA group g = pair >> 2 at g SGP_GROUP; within it word w of pair j = pair & 3 at
@@ -101,7 +102,7 @@ __device__ __forceinline__ void sgp_pass(uint64_t (&P)[S], const uint32_t (&a)[S
 // the a halves of the wave's 32 rows of product k -> LDS (8 DMA instructions of 1 KB, 4 pairs each); lane L of
 // instruction g fetches column L >> 2 of pair 4 g + (L & 3), whose row index it takes from that pair's even lane
 __device__ __forceinline__ void sgp_rows_dma(const uint4* __restrict__ table, size_t k, int W, uint32_t d,
-                                             const uint32_t* wave_rows, int lane) {
+                                             const uint32_t* wave_rows, int lane, GuardArgs gd) {
   typedef __attribute__((address_space(3))) uint32_t lds_u32;
   const uint32_t lb = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds_u32*)wave_rows);
   const size_t kb = k << W;
@@ -111,7 +112,7 @@ __device__ __forceinline__ void sgp_rows_dma(const uint4* __restrict__ table, si
 #pragma unroll
   for (int g = 0; g < 8; ++g) {
     const uint32_t dg = (uint32_t)__builtin_amdgcn_ds_bpermute((8 * g + 2 * jj) * 4, (int)d);
-    const uint4* src = table + (kb + dg) * FBGP_ROW4 + col;
+    const uint4* src = table + FPAI_GUARD_IDX(gd, GS_SGP_ROW, kb + dg, gd.rows, (long long)k) * FBGP_ROW4 + col;
     uint32_t dst = lb + (uint32_t)(g * SGP_GROUP * 4);
     asm volatile("" : "+s"(dst));
     __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(size_t)dst, 16, 0, 0);
@@ -119,8 +120,9 @@ __device__ __forceinline__ void sgp_rows_dma(const uint4* __restrict__ table, si
 }
 
 // this lane's 32 words of the row's b half (b R words [32 tig, 32 tig + 32))
-__device__ __forceinline__ void sgp_b_load(const uint4* __restrict__ table, size_t k, int W, uint32_t d, int tig, uint4 (&bv)[8]) {
-  const uint4* src = table + ((k << W) + d) * FBGP_ROW4 + (FBGP_PW / 4) + 8 * tig;
+__device__ __forceinline__ void sgp_b_load(const uint4* __restrict__ table, size_t k, int W, uint32_t d, int tig, uint4 (&bv)[8],
+                                           GuardArgs gd) {
+  const uint4* src = table + FPAI_GUARD_IDX(gd, GS_SGP_ROW, (k << W) + d, gd.rows, (long long)k) * FBGP_ROW4 + (FBGP_PW / 4) + 8 * tig;
 #pragma unroll
   for (int q = 0; q < 8; ++q) bv[q] = src[q];
 }
@@ -166,6 +168,17 @@ __device__ __forceinline__ void sgp_div56(uint32_t (&z)[S], const uint32_t (&m)[
   for (int i = 0; i < S; ++i) R[i] = Q[(i + 2) % S];   // limb i of the quotient
   lane::normalize<S>(R, z);
 }
+
+#if FLEXPAI_XCHECK
+// test build (guard.hpp): digit k of element ee in half h, its offset and value checked
+__device__ __forceinline__ uint32_t sgp_guard_digit(const SgpParams& p, int h, int k, long long ee) {
+  const uint32_t d = p.digits[FPAI_GUARD_IDX(p.g, GS_SGP_DIGIT, ((size_t)h * p.K + k) * p.n + ee, p.g.digits, ee)];
+  return (uint32_t)FPAI_GUARD_IDX(p.g, GS_SGP_DVAL, d, 1ull << p.W, ee);
+}
+#define SGP_DIGIT(k) sgp_guard_digit(p, half, (k), ee)
+#else
+#define SGP_DIGIT(k) dg[(size_t)(k) * p.n]
+#endif
 
 template <int S>
 __global__ __launch_bounds__(LANE_BLOCK, 2) void k_sgp(SgpParams p) {
@@ -232,16 +245,17 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_sgp(SgpParams p) {
       for (int i = 0; i < S; ++i) x[i] = odd ? Xs[i] : cag[i];
     }
     const uint32_t* dg = p.digits + (size_t)half * K * p.n + ee;
+    (void)dg;
     wave_lds_fence();   // the previous element's reads of rows / bs are done
     for (int i = tig; i < SGP_BW; i += 2) bs[i] = 0u;
     uint32_t cc = 0;
     uint4 bv[8];
     {
-      const uint32_t d0 = dg[0];
-      sgp_rows_dma(table, 0, W, d0, wave_rows, lane);
-      sgp_b_load(table, 0, W, d0, tig, bv);
+      const uint32_t d0 = SGP_DIGIT(0);
+      sgp_rows_dma(table, 0, W, d0, wave_rows, lane, p.g);
+      sgp_b_load(table, 0, W, d0, tig, bv, p.g);
     }
-    uint32_t dn = K > 1 ? dg[(size_t)p.n] : 0u;
+    uint32_t dn = K > 1 ? SGP_DIGIT(1) : 0u;
     for (int k = 0; k < K; ++k) {
       lds_dma_wait();   // row k's a half in LDS, its b words in bv, digit k+1 in dn
       sgp_bsum_add(bs, bv, tig, cc);
@@ -251,14 +265,14 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_sgp(SgpParams p) {
       sgp_pass<S, SGP_AW, true>(P, x, my_row, m, mprime, odd, std::make_integer_sequence<int, S>{});
       if (k + 1 < K) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the rows are consumed before they are overwritten
-        sgp_rows_dma(table, (size_t)(k + 1), W, dn, wave_rows, lane);
+        sgp_rows_dma(table, (size_t)(k + 1), W, dn, wave_rows, lane, p.g);
       }
       __builtin_amdgcn_sched_barrier(0);
       lane::normalize<S>(P, x);
       __builtin_amdgcn_sched_barrier(0);
       if (k + 1 < K) {   // (after the normalization: the b words do not share registers with P)
-        sgp_b_load(table, (size_t)(k + 1), W, dn, tig, bv);
-        dn = k + 2 < K ? dg[(size_t)(k + 2) * p.n] : 0u;
+        sgp_b_load(table, (size_t)(k + 1), W, dn, tig, bv, p.g);
+        dn = k + 2 < K ? SGP_DIGIT(k + 2) : 0u;
       } else {           // (defined on every path, or bv stays live -- and spilled -- across the product)
 #pragma unroll
         for (int q = 0; q < 8; ++q) bv[q] = make_uint4(0u, 0u, 0u, 0u);
@@ -295,7 +309,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_sgp(SgpParams p) {
         c = v >> LB;
       }   // A < 2p (even), B < 4p (odd): what k_fbgp_w and k_pe_fin take
     }
-    if (valid) {
+    if (valid && FPAI_GUARD_OK(p.g, GS_SGP_OUT, ((size_t)half * 2 * S + tig * S + S - 1) * p.n + e, p.g.out, e)) {
 #pragma unroll
       for (int i = 0; i < S; ++i) p.out[((size_t)half * 2 * S + tig * S + i) * p.n + e] = x[i];
     }

@@ -1,6 +1,7 @@
 #!/bin/bash
 # The one GPU-iteration script (run through gpurun from the repo root). Steps, each under its own time limit and
 # chained so that the first failure ends the call; logs under gpurun_out/, names prefixed with TAG:
+#   0. the address-guarded sampler suite (tests/test_gpu_guard.py on libflexpai_xcheck.so; NO_GUARD=1 skips);
 #   1. the -m gpu parity tests (TESTS="tests/test_x.py ..." for a subset; NO_TESTS=1 skips), one process;
 #   2. one bench line (BENCH_ARGS; NO_BENCH=1 skips);
 #   3. PROF=1: a rocprofv3 --kernel-trace --stats profile of bench.py $PROF_ARGS (summary: ${TAG}_prof/run_kernel_stats.csv);
@@ -14,6 +15,12 @@ T=${TAG:-run}
 mkdir -p $O
 export TMPDIR=/tmp
 cd $R
+if [ -z "$NO_TESTS" ] && [ -z "$NO_GUARD" ]; then
+  # the guarded samplers first (csrc/guard.hpp, the test build): a kernel draft whose indices leave their buffers fails
+  # here with the site named, before any unguarded kernel of the draft runs
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_guard.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/${T}_guard.log 2>&1 || { echo "guarded suite failed"; grep -E "FAILED|Error|error" $O/${T}_guard.log | head -20; exit 1; }
+  tail -1 $O/${T}_guard.log
+fi
 if [ -z "$NO_TESTS" ]; then
   timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > $O/${T}_pytest_gpu.log 2>&1; rc=$?
   tail -5 $O/${T}_pytest_gpu.log

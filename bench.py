@@ -177,6 +177,66 @@ def work_add(exps: "torch.Tensor", nb: int) -> float:
     return float((n * (k - 1) + sq) * _M(nb // 16))
 
 
+# ------------------------------------------------------------- per-rank HBM plan
+FB_ROW_BYTES = {1024: 224, 2048: 448, 4096: 512}   # Shoup rows (k_fbs) at 1024/2048, factored word rows (k_sgp) at 4096
+FB_WINDOWS = (24, 23, 22, 21, 20, 16, 12, 8)        # the library's ladder (flexpai.hip ensure_fb)
+GiB = 1 << 30
+
+
+def fb_table_bytes(nb: int, w: int) -> int:
+    """Both halves' fixed-base tables at window w: 2 x K x 2^w rows, K = ceil(bits(p_h - 1) / w) (fb_digit_count)."""
+    return 2 * (-(-(nb // 2) // w)) * (1 << w) * FB_ROW_BYTES[nb]
+
+
+def fb_reserve(device_bytes: int) -> int:
+    """What the library keeps free beside its tables (flexpai.hip fb_budget): max(4 GiB, 1/12 of the device)."""
+    return max(4 * GiB, device_bytes // 12)
+
+
+def rank_memory_plan(cfg_id: int, world: int, nb: int, strong_leg: bool = True) -> dict:
+    """Bytes one rank allocates beside the fixed-base tables for the timed legs of bench.py: the shard outputs
+    (double-buffered at N > 1) and the all-gather receive buffers, the library's per-chunk work (digits + pairs of at
+    most CRT_CHUNK = 4M elements), the decrypt check, and an allowance for RCCL and the torch context."""
+    W = 2 * nb // 32                         # ciphertext words
+    ctb = W * 4 + 4                          # ciphertext + exponent bytes per element
+    K = -(-(nb // 2) // 16)                  # digits per half at the smallest window the legs might see (upper bound)
+    S2 = 2 * (nb // 64 + 5)                  # words of a pair (2 S limbs) per half, rounded up
+    work = 2 * K * 4 + 2 * S2 * 4            # library work per element of a chunk: digits + pairs
+    dec = 8 + 4 + 2 * 2 * S2 * 4             # decrypt check: value + status + the library's pair outputs
+
+    def leg(total, shard):
+        n = -(-total // world) if shard == "strong" else total
+        nb_ = 2 if world > 1 else 1
+        return {"shard_outputs": nb_ * n * ctb + 8 * n,                     # + input and status
+                "gathered_outputs": nb_ * world * n * ctb if world > 1 else 0,
+                "library_work": min(n, 4 << 20) * work,
+                "decrypt_check": min(n, 2 << 20) * dec}
+
+    plan = {f"config{cfg_id}": leg(CONFIGS[cfg_id]["total"], CONFIGS[cfg_id]["shard"])}
+    if cfg_id == 1 and strong_leg and nb == 2048:
+        plan["config3_leg"] = leg(CONFIGS[3]["total"], "strong")
+    plan["rccl_and_runtime_allowance"] = 3 * GiB
+    return plan
+
+
+def plan_total(plan: dict) -> int:
+    return sum(v if isinstance(v, int) else sum(v.values()) for v in plan.values())
+
+
+def preflight_window(cfg_id: int, world: int, nb: int, fb_window: int, device_bytes: int, strong_leg: bool = True) -> dict:
+    """The window the tables can have on this device beside every leg: the largest w <= fb_window of the library's
+    ladder with tables + the legs' plan + the library's reserve <= device memory; and the window the tables alone
+    would get. bench.py refuses to run (SystemExit) when the legs would force a smaller window than the tables alone,
+    or when the library then builds a smaller one than planned: a silently smaller W is a different measurement."""
+    legs = plan_total(rank_memory_plan(cfg_id, world, nb, strong_leg))
+    res = fb_reserve(device_bytes)
+    alone = next((w for w in FB_WINDOWS if w <= fb_window and fb_table_bytes(nb, w) + res <= device_bytes), None)
+    both = next((w for w in FB_WINDOWS if w <= fb_window and fb_table_bytes(nb, w) + max(res, legs) <= device_bytes), None)
+    return {"window": both, "window_tables_alone": alone, "legs_bytes": legs, "reserve_bytes": res,
+            "tables_bytes": fb_table_bytes(nb, both) if both else None, "device_bytes": device_bytes,
+            "ok": both is not None and both == alone}
+
+
 def lib_sha16() -> str:
     """sha256 (16 hex digits) of the libflexpai.so this process runs."""
     from flex.crypto.paillier import _native
@@ -341,7 +401,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, choices=sorted(CONFIGS), default=None,
-                    help="BASELINE.json config (default: 1 on one GPU, 3 on several)")
+                    help="BASELINE.json config (default: 1 at every N; the configs[3] leg runs inside it unless "
+                         "--no-strong)")
     ap.add_argument("--n", type=int, default=None, help="override: total elements (per GPU for weak configs)")
     ap.add_argument("--nb", type=int, default=None, help="override: Paillier key bits")
     ap.add_argument("--path", choices=("crt", "public"), default="crt")
@@ -350,7 +411,7 @@ def main():
     ap.add_argument("--fb-window", type=int, default=23, choices=(8, 12, 16, 20, 21, 22, 23, 24),
                     help="largest digit window of the fixed-base tables; the library takes the largest one <= this "
                          "whose tables fit the free HBM (nb = 2048: W = 22 with Shoup rows, 47 products per half, "
-                         "2 x 88.3 GB; nb = 4096: W = 21, 98 products per half, 2 x 121.7 GB)")
+                         "2 x 88.3 GB; nb = 4096: W = 21, 98 products per half, 2 x 105.2 GB)")
     ap.add_argument("--pfb-window", type=int, default=20, choices=(12, 16, 20),
                     help="digit window of the public-key fixed-base leg (W = 20: 266 row products per element, "
                          "139 GB of tables; the library default is 16)")
@@ -434,6 +495,13 @@ def main():
     fb_shoup = False
     if use_fb:
         ctx.set_fb_window(args.fb_window)     # a dedicated encrypt GPU: the largest tables that fit its HBM
+        free0, total0 = torch.cuda.mem_get_info(dev)
+        pf = preflight_window(cfg_id, world, nb, args.fb_window, free0, strong_leg=not args.no_strong)
+        setup["memory_preflight"] = pf
+        if not pf["ok"]:
+            raise SystemExit(f"memory preflight: the legs of this run ({pf['legs_bytes'] / 1e9:.1f} GB per rank) would "
+                             f"force the fixed-base window from W = {pf['window_tables_alone']} to {pf['window']} on "
+                             f"{free0 / 1e9:.1f} GB free: {pf}")
         t0 = time.perf_counter()
         try:
             ctx.prepare_fixed_base()
@@ -441,6 +509,9 @@ def main():
             setup["fixed_base_unavailable"] = str(exc)
         setup["fixed_base_build_wall_ms"] = (time.perf_counter() - t0) * 1e3
         use_fb = ctx.fb_ready
+        if use_fb and pf["window"] and ctx.fb_window < pf["window"]:
+            raise SystemExit(f"memory preflight: the library built W = {ctx.fb_window} tables, below the planned "
+                             f"W = {pf['window']} ({pf})")
         fb_pair = ctx.fb_pair if use_fb else 0
         fb_split = bool(ctx.split_sampler & 1) if use_fb else False   # k_sgp (kernels_sgp.hpp) for k_fbgp
         fb_shoup = bool(ctx.split_sampler & 4) if use_fb else False   # k_fbs (kernels_fbs.hpp) for k_fbp

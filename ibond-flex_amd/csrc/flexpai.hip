@@ -11,6 +11,7 @@
 #include <string>
 #include <sys/random.h>
 #include <thread>
+#include <array>
 #include <vector>
 
 #include "flexpai.h"
@@ -185,10 +186,8 @@ struct pai_ctx {
   bool timing = false;
   // HIP events between the kernels of each chunk of the last encrypt / decrypt call; the stage times
   // are summed over its chunks (a call of more than CRT_CHUNK elements runs several)
-  static constexpr int EV_CHUNKS = 64;
-  hipEvent_t ev[EV_CHUNKS][4] = {};
+  std::vector<std::array<hipEvent_t, 4>> ev;   // per chunk of the timed call; grown on demand, read at the query
   int nev = 0, nchunk_ev = 0;
-  float ev_acc[3] = {0.f, 0.f, 0.f};   // stage times of chunks already folded (calls of more than EV_CHUNKS chunks)
   // host-buffer entry points (pai_encrypt / pai_decrypt / pai_add): device copies of the operands, a
   // compute and a copy stream, one event per chunk (host_pipe below)
   void* d_hostio = nullptr;
@@ -206,6 +205,30 @@ struct pai_ctx {
 };
 
 static std::atomic<int> g_contexts{0}, g_key_holders{0};
+
+// $FLEXPAI_SETUP_TRACE=1: wall time of each per-key setup step on stderr ("flexpai-trace <step> <ms>"), and the count
+// and time of the constant uploads (the fresh-key analysis of DESIGN §5; tools/fresh_key_trace.py)
+static bool setup_trace_on() {
+  static const bool on = getenv("FLEXPAI_SETUP_TRACE") != nullptr;
+  return on;
+}
+static std::atomic<long> g_upload_n{0};
+static std::atomic<long long> g_upload_ns{0};
+struct SetupTrace {
+  const char* name;
+  std::chrono::steady_clock::time_point t0;
+  explicit SetupTrace(const char* n) : name(n), t0(std::chrono::steady_clock::now()) {}
+  ~SetupTrace() {
+    if (setup_trace_on())
+      fprintf(stderr, "flexpai-trace %-32s %10.3f ms\n", name,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  }
+};
+static void trace_uploads(const char* where) {
+  if (!setup_trace_on()) return;
+  fprintf(stderr, "flexpai-trace %-32s %10.3f ms (%ld uploads)\n", where, (double)g_upload_ns.exchange(0) * 1e-6,
+          g_upload_n.exchange(0));
+}
 
 pai_ctx::~pai_ctx() {
   if (counted) --g_contexts;
@@ -268,11 +291,14 @@ struct CtxLock {
 
 template <typename T>
 static int upload(pai_ctx* c, const std::vector<T>& v, T** out) {
+  const auto t0 = std::chrono::steady_clock::now();
   void* p = nullptr;
   HIPCHK(hipMalloc(&p, std::max<size_t>(v.size(), 1) * sizeof(T)));
   (c->in_priv ? c->priv_allocs : c->allocs).push_back(p);
   if (!v.empty()) HIPCHK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
   *out = (T*)p;
+  ++g_upload_n;
+  g_upload_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
   return 0;
 }
 
@@ -484,28 +510,14 @@ static void stage_reset(pai_ctx* c) {
   if (c->stage_keep) return;   // inside a host-buffer call: its entry point reset once for all chunks
   c->nev = 0;
   c->nchunk_ev = 0;
-  for (float& a : c->ev_acc) a = 0.f;
 }
-// Elapsed times of the recorded chunks into ev_acc, freeing the event slots (waits for the last chunk).
-static void stage_fold(pai_ctx* c) {
-  if (c->nchunk_ev < 1 || c->nev < 2) {
-    c->nchunk_ev = 0;
-    return;
-  }
-  (void)hipEventSynchronize(c->ev[c->nchunk_ev - 1][c->nev - 1]);
-  for (int i = 0; i + 1 < c->nev && i < 3; ++i)
-    for (int ch = 0; ch < c->nchunk_ev; ++ch) {
-      float t = 0.f;
-      if (hipEventElapsedTime(&t, c->ev[ch][i], c->ev[ch][i + 1]) == hipSuccess) c->ev_acc[i] += t;
-    }
-  c->nchunk_ev = 0;
-}
-// The events of a new chunk (nullptr when timing is off); past EV_CHUNKS chunks the recorded ones are folded
-// into ev_acc first, so every chunk of a call is counted
+// The events of a new chunk (nullptr when timing is off). The event table grows with the chunks of a call and is
+// read only by pai_ctx_stage_times: recording a stage never waits on the device (folding the slots of a
+// long call synchronised mid-call and removed the copy/compute overlap being timed).
 static hipEvent_t* stage_chunk(pai_ctx* c) {
   if (!c->timing) return nullptr;
-  if (c->nchunk_ev >= pai_ctx::EV_CHUNKS) stage_fold(c);
-  hipEvent_t* e = c->ev[c->nchunk_ev++];
+  if (c->nchunk_ev >= (int)c->ev.size()) c->ev.push_back({nullptr, nullptr, nullptr, nullptr});
+  hipEvent_t* e = c->ev[c->nchunk_ev++].data();
   for (int i = 0; i < 4; ++i)
     if (!e[i]) (void)hipEventCreate(&e[i]);
   return e;
@@ -557,6 +569,7 @@ static int setup_pe(pai_ctx* c, const HBig& n);
 
 int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** out) {
   if (!n_le || !out || n_bytes == 0) return fail(PAI_ERR_ARG, "pai_ctx_create: null argument");
+  SetupTrace tr("pai_ctx_create");
   HBig n = HBig::from_le_bytes(n_le, n_bytes);
   if (!n.is_odd() || n.bits() < 64) return fail(PAI_ERR_KEY, "pai_ctx_create: n must be odd and >= 64 bits");
   auto* c = new pai_ctx();
@@ -610,7 +623,7 @@ int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** ou
   if ((rc = upload(c, rs, &c->d_RS)) || (rc = upload(c, c->N.limbs(c->S_e, LB), &c->d_N)) ||
       (rc = upload(c, R2.limbs(c->S_e, LB), &c->d_R2)) ||
       (rc = upload(c, n.limbs(c->S_e, LB), &c->d_nl)) || (rc = upload(c, prog, &c->d_prog)) ||
-      (rc = upload(c, oneR.limbs(c->S_e, LB), &c->d_oneR)) || (rc = setup_pe(c, n))) {
+      (rc = upload(c, oneR.limbs(c->S_e, LB), &c->d_oneR)) || (rc = (SetupTrace("  setup_pe"), setup_pe(c, n)))) {
     delete c;
     return rc;
   }
@@ -719,11 +732,14 @@ static int setup_pe(pai_ctx* c, const HBig& n) {
 
 template <typename T>
 static int upload_fb(pai_ctx* c, const std::vector<T>& v, T** out) {
+  const auto t0 = std::chrono::steady_clock::now();
   void* p = nullptr;
   HIPCHK(hipMalloc(&p, std::max<size_t>(v.size(), 1) * sizeof(T)));
   c->fb_mem.push_back(p);
   if (!v.empty()) HIPCHK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
   *out = (T*)p;
+  ++g_upload_n;
+  g_upload_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
   return 0;
 }
 
@@ -766,8 +782,8 @@ static bool fb_window_auto() {
 
 // Window of the key holder's tables: $FLEXPAI_FB_WINDOW, default 16 (2 x 1.07 GB at nb = 2048: a process may hold
 // several keys). "auto": a process whose only private key is this one asks for the largest window (24) and
-// gets the largest whose tables fit auto's share of the free HBM (fb_budget), i.e. W = 23 at nb = 2048 and
-// W = 21 at nb = 4096 on an otherwise empty MI355X; a process holding several keys gets 16.
+// gets the largest whose tables fit auto's share of the free HBM (fb_budget), i.e. W = 22 at nb = 2048 (2 x 88.3 GB of
+// 448-B Shoup rows) and W = 21 at nb = 4096 on an otherwise empty MI355X; a process holding several keys gets 16.
 static int fb_default_window() {
   if (fb_window_auto()) return g_key_holders.load() <= 1 ? 24 : 16;
   const char* e = getenv("FLEXPAI_FB_WINDOW");
@@ -854,7 +870,8 @@ static uint64_t fb_bytes(const pai_ctx* c, int W) {
 // the process) allocate after the tables: host-pipeline buffers for larger calls, decryption work and
 // scratch, k_add's schedule, a configs[3] shard with its all-gather receive buffers.
 // With FLEXPAI_FB_WINDOW=auto the budget is further capped at $FLEXPAI_FB_AUTO_FRAC (default 0.75) of the free
-// memory, so an automatic choice never takes the whole device (W = 23 at nb = 2048 is 193 GB of 287 GB free).
+// memory, so an automatic choice never takes the whole device (W = 22 at nb = 2048 is 177 GB of 287 GB free; W = 23's
+// Shoup rows, 338 GB, do not fit).
 static uint64_t fb_budget(const pai_ctx* c) {
   (void)c;
   if (const char* e = getenv("FLEXPAI_FB_MAX_BYTES")) return (uint64_t)strtod(e, nullptr);
@@ -983,6 +1000,7 @@ static int ensure_fb(pai_ctx* c) {
       break;
     }
   if (!W) return fb_unavailable(c, "tables do not fit the device memory budget");
+  SetupTrace tr_all("ensure_fb");
   const auto t0 = std::chrono::steady_clock::now();
   const size_t kb[2] = {sub(c->fb_p, HBig(1)).bits(), sub(c->fb_q, HBig(1)).bits()};
   const int raw_bits = (int)std::max(kb[0], kb[1]) + 64;
@@ -1021,7 +1039,11 @@ static int ensure_fb(pai_ctx* c) {
   uint32_t* gcval[2] = {nullptr, nullptr};
   uint32_t* pcval[2] = {nullptr, nullptr};
   for (int h = 0; h < 2; ++h) {
-    if (!c->fb_g[h] && !(c->fb_g[h] = fb_base(primes[h]))) return fb_unavailable(c, "no base found");
+    if (!c->fb_g[h]) {
+      SetupTrace tr_g("  fb_base (generator search)");
+      if (!(c->fb_g[h] = fb_base(primes[h]))) return fb_unavailable(c, "no base found");
+    }
+    SetupTrace tr_h("  host prep (one half)");
     const HBig& m2 = sq[h];
     HMont M2(m2);
     // B_k = G^(2^(W k)), G = g^n mod p_h^2
@@ -1054,8 +1076,11 @@ static int ensure_fb(pai_ctx* c) {
     if (hipMalloc(&lohi[h], (size_t)K * 2 * FB_LO * lohi_limbs * 4) != hipSuccess) return fb_unavailable(c, "table allocation failed");
     c->fb_mem.push_back(lohi[h]);
     dlohi = (uint32_t*)lohi[h];
-    if (hipMalloc(&t[h], ((size_t)K << W) * (fb_table_row_words(c) / 4) * sizeof(uint4)) != hipSuccess)
-      return fb_unavailable(c, "table allocation failed");
+    {
+      SetupTrace tr_m("  table hipMalloc (one half)");
+      if (hipMalloc(&t[h], ((size_t)K << W) * (fb_table_row_words(c) / 4) * sizeof(uint4)) != hipSuccess)
+        return fb_unavailable(c, "table allocation failed");
+    }
     c->fb_mem.push_back(t[h]);
     hv[h] = FbHalf{(const uint4*)t[h], dm, dR2, done, dbases, dlohi, dnm, dpbig, mont_prime(m2, LB)};
     if (pair_ok) {
@@ -1247,7 +1272,9 @@ static int ensure_fb(pai_ctx* c) {
       if ((rc = upload_fb(c, svv, &c->d_sgp_fb))) return fb_unavailable(c, pai_last_error());
     }
   }
+  trace_uploads("  fb uploads");
   if (gpair_ok || pair_ok) {   // factored rows: the chain products are inverted on the host between the two phases
+    SetupTrace tr_1("  phase 1 (lohi, inv_fwd) + host invert");
     const hipError_t e1 = gpair_ok ? fbgp_build_phase1(c->d_fbgp_halves, K, W, nullptr)
                                    : fbp_build_phase1(ps, c->d_fbp_halves, K, W, nullptr);
     if (e1 != hipSuccess || hipDeviceSynchronize() != hipSuccess) return fb_unavailable(c, "table construction failed");
@@ -1255,6 +1282,7 @@ static int ensure_fb(pai_ctx* c) {
       if (pair_host_invert(primes[h], gpair_ok ? gcval[h] : pcval[h], 2 * K, gpair_ok ? FBGP_S : ps))
         return fb_unavailable(c, pai_last_error());
   }
+  SetupTrace tr_2("  phase 2 (inv_bwd, fill) + frees");
 #if FLEXPAI_XCHECK
   const hipError_t be = gpair_ok  ? fbgp_build_phase2(c->d_fbgp_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
                         : grp     ? grp_build_tables(c->d_fb_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
@@ -1368,6 +1396,7 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
   const HBig sq[2] = {mul(p, p), mul(q, q)};
   CrtHalf ha[2], hb[2];
   int rc;
+  SetupTrace tr_ab("    crt stage A/B consts");
   for (int h = 0; h < 2; ++h) {
     const HBig& ph = primes[h];
     const HBig& other = primes[1 - h];
@@ -1411,6 +1440,7 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
   c->fb_q = q;
   // lane-engine decryption: x_h = c^(p_h - 1) mod p_h^2, L_h, m_h = L_h h_h mod p_h; CRT + decode
   {
+    SetupTrace tr_d("    lane decrypt consts");
     const int kd = (int)((32 * (size_t)c->ct_words + RB - 1) / RB);
     if (kd > KMAX_CHUNKS) return 0;
     DecLaneHalf dh[2];
@@ -1456,6 +1486,7 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
   bool pair = true;
   if (const char* e = xcheck_env("FLEXPAI_PAIR")) pair = atoi(e) != 0;
   if (pair && (size_t)LB * sa >= pb + 12) {
+    SetupTrace tr_p("    pair consts");
     const int S2 = 2 * sa;
     auto split = [&](const HBig& v, const HBig& P) {   // canonical pair of v < P^2
       const HBig qt = div_big(v, P), rm = sub(v, mul(qt, P));
@@ -1519,7 +1550,12 @@ int pai_ctx_set_private(pai_ctx* c, const uint8_t* p_le, const uint8_t* q_le, si
   if (cmp(q, p) < 0) std::swap(p, q);   // keypair.py:57-62
   if (c->has_priv) return 0;            // same key (p q == n): already set
   c->in_priv = true;
-  const int rc = set_private_impl(c, p, q);
+  int rc;
+  {
+    SetupTrace tr("pai_ctx_set_private");
+    rc = set_private_impl(c, p, q);
+  }
+  trace_uploads("  set_private uploads");
   c->in_priv = false;
   if (!rc && !c->holder) {
     c->holder = true;
@@ -1585,6 +1621,7 @@ static int set_private_impl(pai_ctx* c, HBig p, HBig q) {
   c->nprime_d = mont_prime(c->n, LB);
   c->n_limbs = (int)((c->n.bits() + LB - 1) / LB);
   c->has_priv = true;
+  SetupTrace tr("  setup_crt");
   if ((rc = setup_crt(c, p, q))) return rc;
 #if !FLEXPAI_XCHECK
   // a key outside the pair kernels' bounds (R = 2^(28 S) >= 2^12 p_h): CRT encryption and lane decryption would
@@ -1671,7 +1708,7 @@ int pai_ctx_stage_times(pai_ctx* c, float* ms_out, int max_out, int* count) {
   if (c->nchunk_ev > 0) HIPCHK(hipEventSynchronize(c->ev[c->nchunk_ev - 1][c->nev - 1]));
   const int k = std::min(c->nev - 1, max_out);
   for (int i = 0; i < k; ++i) {
-    ms_out[i] = i < 3 ? c->ev_acc[i] : 0.f;
+    ms_out[i] = 0.f;
     for (int ch = 0; ch < c->nchunk_ev; ++ch) {
       float t = 0.f;
       HIPCHK(hipEventElapsedTime(&t, c->ev[ch][i], c->ev[ch][i + 1]));
@@ -3392,8 +3429,9 @@ int pai_decrypt(pai_ctx* c, const uint32_t* ct, const int32_t* exp, size_t N, do
 // Copies the per-half sampler outputs (c0 G_h^a_h mod h^2) of the last fixed-base chunk: limbs [2][SB][n] (k_fb,
 // k_fbg), or canonical pairs [2][2S][n] with *sb = 2S for the pair tables (k_fbs/k_fbp; the p half times q^-2).
 extern "C" int pai_debug_fb_w(pai_ctx* c, uint32_t* out, size_t max_words, long long* n, int* sb) {
-  if (!c || !c->fb_last_w) return fail(PAI_ERR_ARG, "no fixed-base output");
+  if (!c) return fail(PAI_ERR_ARG, "null ctx");
   CtxLock lk(c);
+  if (!c->fb_last_w) return fail(PAI_ERR_ARG, "no fixed-base output");
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipDeviceSynchronize());
   const int rows = c->fb_pair_s ? 2 * c->fb_pair_s : c->crt_sb;

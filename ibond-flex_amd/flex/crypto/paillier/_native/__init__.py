@@ -8,7 +8,9 @@ from __future__ import annotations
 import collections
 import ctypes
 import os
+import sys
 import threading
+import warnings
 from typing import Optional, Sequence, Tuple
 
 import numpy as np
@@ -61,6 +63,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
             raise NativeError(f"flexpai native library not found at {path}; run __graft_entry__.build() "
                               f"(hipcc --offload-arch=gfx950). There is no CPU fallback.")
         _start_torch_runtime_first()
+        if "torch" not in sys.modules:
+            _watch_late_torch_import()
         lib = ctypes.CDLL(path)
         P, S, I, U64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
         lib.pai_device_count.argtypes = [P]
@@ -126,6 +130,68 @@ def _start_torch_runtime_first() -> None:
             torch.cuda.init()
     except Exception:   # noqa: BLE001 - torch without a usable GPU: flexpai's own runtime still works
         pass
+
+
+_runtime_started = False   # a context was created: libflexpai's HIP runtime holds the GPU
+_torch_watch = None
+
+
+class _LateTorchWatch:
+    """sys.meta_path finder armed when libflexpai loads before torch: when torch is imported later, after
+    libflexpai's runtime has opened the GPU, torch's own HIP runtime cannot (torch.cuda.is_available() is False).
+    Warn once at that import instead of leaving the caller to find the failure. One shot:
+    the finder removes itself at torch's import and never changes what is imported."""
+
+    def find_spec(self, name, path=None, target=None):
+        if name != "torch":
+            return None
+        _disarm_torch_watch()
+        import importlib.machinery
+        spec = importlib.machinery.PathFinder.find_spec(name, path)
+        loader = getattr(spec, "loader", None)
+        if loader is None or not hasattr(loader, "exec_module"):
+            return spec
+        inner = loader.exec_module
+
+        def exec_module(module):
+            inner(module)
+            _check_torch_after_flexpai(module)
+
+        loader.exec_module = exec_module   # (this loader instance only: it loads torch's __init__ and nothing else)
+        return spec
+
+
+def _watch_late_torch_import() -> None:
+    global _torch_watch
+    if _torch_watch is None and not os.environ.get("FLEXPAI_NO_TORCH_INIT"):
+        _torch_watch = _LateTorchWatch()
+        sys.meta_path.insert(0, _torch_watch)
+
+
+def _disarm_torch_watch() -> None:
+    global _torch_watch
+    if _torch_watch is not None:
+        try:
+            sys.meta_path.remove(_torch_watch)
+        except ValueError:
+            pass
+        _torch_watch = None
+
+
+def _check_torch_after_flexpai(torch) -> bool:
+    """True (and a RuntimeWarning) when torch was imported after libflexpai started the GPU and torch cannot see it."""
+    if not _runtime_started:
+        return False
+    try:
+        ok = bool(torch.cuda.is_available())
+    except Exception:   # noqa: BLE001 - a torch without a HIP build: nothing of ours to report
+        return False
+    if ok:
+        return False
+    warnings.warn("flexpai: torch was imported after libflexpai started the GPU, and torch.cuda now reports no GPU "
+                  "(two HIP runtimes in one process: the first to open the device keeps it). Import torch before "
+                  "the first Paillier call; see INTEGRATION.md (PyTorch).", RuntimeWarning, stacklevel=2)
+    return True
 
 
 def device_count() -> int:
@@ -210,6 +276,8 @@ class Context:
         buf = int_to_le(n, nbytes)
         h = ctypes.c_void_p()
         self._chk(self.lib.pai_ctx_create(buf, nbytes, device, ctypes.byref(h)))
+        global _runtime_started
+        _runtime_started = True
         self._h = h
         kb, cw, pw = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         self._chk(self.lib.pai_ctx_info(h, ctypes.byref(kb), ctypes.byref(cw), ctypes.byref(pw)))

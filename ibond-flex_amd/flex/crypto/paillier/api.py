@@ -1,3 +1,7 @@
+#  The three factory signatures below are the boundary contract of flex/crypto/paillier/api.py of iBond-flex, which
+#  callers reach unchanged: Copyright 2020 The FLEX Authors, licensed under the Apache License, Version 2.0
+#  (http://www.apache.org/licenses/LICENSE-2.0). Distributed on an "AS IS" BASIS, WITHOUT WARRANTIES OR
+#  CONDITIONS OF ANY KIND, either express or implied.
 """Factory API — same names and signatures as flex/crypto/paillier/api.py:17-34."""
 from .decryptor import PaillierDecryptor
 from .encryptor import PaillierEncryptor

@@ -306,6 +306,13 @@ def sub_encrypted(a, b):
     independent, so a scalar left operand is added on the right. NotImplemented when an operand is not
     entirely PaillierEncryptedNumber (or there is no GPU): the caller falls back to numpy's per-element loop."""
     if isinstance(b, PaillierEncryptedNumber):
+        # a must be an encrypted array under b's key before b's inverse is paid for (ADVICE r4): otherwise the
+        # caller's per-element loop recomputes everything
+        if isinstance(a, PaillierEncryptedNumber):
+            return NotImplemented
+        A, pk = _encrypted_operand(a)
+        if A is None or pk != b.public_key:
+            return NotImplemented
         neg = b * -1
     else:
         neg = mul_plain(b, -1)

@@ -123,6 +123,34 @@ __device__ __forceinline__ void mont_mul(uint32_t (&A)[S], uint32_t (&B)[S], Get
   lane::normalize<S>(P2, B);
 }
 
+// ---- (A, B) <- (A, B)(a, 0) R^-1 in lock-step (the factored decryption chain, kernels_pair.hpp decf_run): both rows
+// take the multiplier's one digit a_J, P1 += A a_J, P2 += B a_J (the A1 B2 term is gone), then red2 -- 4 S^2 MACs
+// against mont_mul's 5 S^2, one LDS word per digit instead of two, same registers and bounds. get(J) returns a_J.
+template <int S, int J, class Get>
+__device__ __forceinline__ void mul_b0_step(uint64_t (&P1)[S], uint64_t (&P2)[S], const uint32_t (&A)[S], const uint32_t (&B)[S],
+                                            Get& get, const uint32_t (&m)[S], uint32_t mprime) {
+  const uint32_t a = get(std::integral_constant<int, J>{});
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    P1[(i + J) % S] += (uint64_t)A[i] * a;
+    P2[(i + J) % S] += (uint64_t)B[i] * a;
+  }
+  red2<S, J>(P1, P2, m, mprime);
+}
+template <int S, class Get, int... Js>
+__device__ __forceinline__ void mul_b0_all(uint64_t (&P1)[S], uint64_t (&P2)[S], const uint32_t (&A)[S], const uint32_t (&B)[S],
+                                           Get& get, const uint32_t (&m)[S], uint32_t mprime, std::integer_sequence<int, Js...>) {
+  (mul_b0_step<S, Js>(P1, P2, A, B, get, m, mprime), ...);
+}
+template <int S, class Get>
+__device__ __forceinline__ void mont_mul_b0(uint32_t (&A)[S], uint32_t (&B)[S], Get&& get, const uint32_t (&m)[S], uint32_t mprime) {
+  uint64_t P1[S], P2[S];
+  zero2<S>(P1, P2);
+  mul_b0_all<S>(P1, P2, A, B, get, m, mprime, std::make_integer_sequence<int, S>{});
+  lane::normalize<S>(P1, A);
+  lane::normalize<S>(P2, B);
+}
+
 // ---- two B-free operands against two pair constants at once: (X1, 0) C1 + (X2, 0) C2, times R^-1 (k_fbp_fin's
 // w_q q^-2 = A_q q^-2 + B_q q^-1). Lock-step rows as in mont_mul: P1 += X1 c1a_J + X2 c2a_J, P2 += X1 c1b_J + X2 c2b_J,
 // one reduction for both products (6 S^2 MACs, against 4 S^2 + 4 S^2 for two products); per position and digit at most
@@ -222,6 +250,15 @@ __device__ __forceinline__ void mont_mul_a0(uint32_t (&A)[S], uint32_t (&B)[S], 
   for (int i = 0; i < S; ++i) P[i] = 0;
   a0_pass_b<S>(P, B, gb, m, mprime, std::make_integer_sequence<int, S>{});
   lane::normalize<S>(P, B);
+}
+
+// ---- one row: X <- REDC(init + X y) mod p with y's digits from get(J) (a uint32_t), P holding init on entry (< 2^56
+// per limb); the factored decryption's closing Horner sum (kernels_pair.hpp decf_run)
+template <int S, class Get>
+__device__ __forceinline__ void redc_row(uint64_t (&P)[S], uint32_t (&X)[S], Get&& get, const uint32_t (&m)[S], uint32_t mprime) {
+  auto nop = [](auto, uint32_t) {};
+  a0_pass_u<S>(P, X, get, nop, m, mprime, std::make_integer_sequence<int, S>{});
+  lane::normalize<S>(P, X);
 }
 
 // (A, B) with A, B < 2p -> the canonical pair A < p, B < p of the same residue mod p^2

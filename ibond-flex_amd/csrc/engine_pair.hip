@@ -1,4 +1,7 @@
 // Pair exponentiation kernels (kernels_pair.hpp): instantiations, launch geometry and launches.
+#ifndef FLEXPAI_XCHECK
+#define FLEXPAI_XCHECK 0   // 1: the test-only library, which also holds the general decryption chain (k_dec_pow_pair<s, false>)
+#endif
 #include "engine_pair.hpp"
 
 namespace fpai {
@@ -11,25 +14,30 @@ static int occupancy(K kernel) {
 }
 
 template <int S>
-static void geometry(int cus, long long chunk, DecLaneGeom* g) {
+static void geometry(int cus, long long chunk, DecLaneGeom* g, bool factored) {
   const long long blocks = (chunk + LANE_BLOCK - 1) / LANE_BLOCK;
   auto clamp = [&](long long cap) { return (int)std::max<long long>(1, std::min<long long>(blocks, cap)); };
   g->gx_pre = clamp((long long)occupancy(k_dec_pre_pair<S>) * cus / 2);
-  g->gx_pow = clamp((long long)occupancy(k_dec_pow_pair<S>) * cus / 2);
+#if FLEXPAI_XCHECK
+  if (!factored) g->gx_pow = clamp((long long)occupancy(k_dec_pow_pair<S, false>) * cus / 2);
+  else
+#endif
+    g->gx_pow = clamp((long long)occupancy(k_dec_pow_pair<S, true>) * cus / 2);
+  (void)factored;
   g->gx_fin = clamp((long long)occupancy(k_dec_fin_pair<S>) * cus);
   g->scratch_bytes = (size_t)2 * g->gx_pow * LANE_BLOCK * lane_scratch_words<2 * S>() * 4;
 }
 
-int dec_pair_geometry(int s, int cus, long long chunk, DecLaneGeom* g) {
-  if (s == 19) geometry<19>(cus, chunk, g);
-  else if (s == 37) geometry<37>(cus, chunk, g);
+int dec_pair_geometry(int s, int cus, long long chunk, DecLaneGeom* g, bool factored) {
+  if (s == 19) geometry<19>(cus, chunk, g, factored);
+  else if (s == 37) geometry<37>(cus, chunk, g, factored);
   else return -1;
   return 0;
 }
 
 template <int S>
 static hipError_t launch(const DecPairPreParams& pre, const CrtParams& pw, const DecPairFinParams& f, const DecLaneGeom& g,
-                         hipStream_t st, hipEvent_t* ev) {
+                         hipStream_t st, hipEvent_t* ev, bool factored) {
   const long long blocks = (f.n + LANE_BLOCK - 1) / LANE_BLOCK;
   auto clamp = [&](int gx) { return (int)std::min<long long>(gx, blocks); };
   if (ev && ev[0]) (void)hipEventRecord(ev[0], st);
@@ -37,7 +45,12 @@ static hipError_t launch(const DecPairPreParams& pre, const CrtParams& pw, const
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (ev && ev[1]) (void)hipEventRecord(ev[1], st);
-  hipLaunchKernelGGL(k_dec_pow_pair<S>, dim3(clamp(g.gx_pow), 2), dim3(LANE_BLOCK), 0, st, pw);
+#if FLEXPAI_XCHECK
+  if (!factored) hipLaunchKernelGGL((k_dec_pow_pair<S, false>), dim3(clamp(g.gx_pow), 2), dim3(LANE_BLOCK), 0, st, pw);
+  else
+#endif
+    hipLaunchKernelGGL((k_dec_pow_pair<S, true>), dim3(clamp(g.gx_pow), 2), dim3(LANE_BLOCK), 0, st, pw);
+  (void)factored;
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (ev && ev[2]) (void)hipEventRecord(ev[2], st);
   hipLaunchKernelGGL(k_dec_fin_pair<S>, dim3(clamp(g.gx_fin)), dim3(LANE_BLOCK), 0, st, f);
@@ -47,9 +60,9 @@ static hipError_t launch(const DecPairPreParams& pre, const CrtParams& pw, const
 }
 
 hipError_t dec_pair_launch(int s, const DecPairPreParams& pre, const CrtParams& pw, const DecPairFinParams& f,
-                           const DecLaneGeom& g, hipStream_t st, hipEvent_t* ev) {
-  if (s == 19) return launch<19>(pre, pw, f, g, st, ev);
-  if (s == 37) return launch<37>(pre, pw, f, g, st, ev);
+                           const DecLaneGeom& g, hipStream_t st, hipEvent_t* ev, bool factored) {
+  if (s == 19) return launch<19>(pre, pw, f, g, st, ev, factored);
+  if (s == 37) return launch<37>(pre, pw, f, g, st, ev, factored);
   return hipErrorInvalidValue;
 }
 

@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <sys/random.h>
@@ -100,7 +101,8 @@ struct pai_ctx {
   // the default for 1024/2048-bit keys ($FLEXPAI_PAIR=0 selects the 2S-limb lane kernels)
   bool dec_pair_ok = false, crt_pair_ok = false;
   DecPairHalf* d_decp_halves = nullptr;
-  CrtHalf* d_decp_pow = nullptr;
+  CrtHalf* d_decp_pow = nullptr;   // decryption halves; c0: the factored chain's K'_t ([16][S], decf)
+  bool decf = false;                // the factored (B-free) decryption chain (kernels_pair.hpp decf_run)
   CrtHalf* d_crtp_b = nullptr;
   uint32_t *d_decp_nl = nullptr, *d_decp_maxint = nullptr;
   int decp_kchunks = 0;
@@ -410,6 +412,69 @@ static bool build_lane_program(const HBig& e, std::vector<uint32_t>& prog) {
   return loaded;
 }
 
+// K_t: for each table entry t, the sum over the chain's multiplies by it of 2^(squares after that multiply)
+static std::vector<HBig> chain_weights(const HBig& ph, const std::vector<uint16_t>& sched) {
+  std::vector<HBig> K(LANE_NTILE, HBig(0));
+  size_t after = 0;
+  for (size_t i = sched.size(); i >= 2; i -= 2) {
+    const int nsq = sched[i - 2], idx = sched[i - 1];
+    if (idx != 0xFFFF) K[idx] = mod(add(K[idx], mul_pow2_mod(HBig(1), after, ph)), ph);
+    after += (size_t)nsq;
+  }
+  return K;
+}
+
+// Op list of the factored 1024/2048-bit decryption (decf_run, kernels_pair.hpp; tools/decf_model.py): the table of
+// full pairs as build_lane_program (x~^2 general, kept in the column; odd powers into tiles 0..15), the chain over
+// e = p_h - 2 with B-free multipliers (LOP_BFREE), then Y' (A~, 0) (iota put into the column before it) and the
+// product with (1, 0). kf: the closing Horner sum's K'_t = R (K_t + [t == 0]) mod p_h, S limbs each (entry 1's
+// weight + 1: the closing (A~, 0) drops its (1 + p b_1)).
+static bool build_decf_lane_program(const HBig& ph, size_t RS, int S, std::vector<uint32_t>& prog, std::vector<uint32_t>& kf) {
+  const HBig e = sub(ph, HBig(2));
+  if (e.bits() < 8) return false;
+  std::vector<uint16_t> sched;
+  int first = 0;
+  sliding_schedule(e, sched, first);
+  auto op = [](uint32_t flags, int bidx, int aidx, int sidx) {
+    return flags | ((uint32_t)bidx << 8) | ((uint32_t)aidx << 16) | ((uint32_t)sidx << 24);
+  };
+  prog.clear();
+  prog.push_back(op(LOP_SQR | LOP_B_SET, 0, 0, 0));                       // x~^2 -> LDS multiplier
+  prog.push_back(op(LOP_A_FROM_T | LOP_B_READY | LOP_STORE, 0, 0, 1));    // x~ * x~^2  -> T1
+  for (int k = 2; k < LANE_NTILE; ++k) prog.push_back(op(LOP_STORE | LOP_B_READY, 0, 0, k));
+  bool loaded = false;
+  size_t first_sq = SIZE_MAX;
+  for (size_t i = 0; i + 1 < sched.size(); i += 2) {
+    const int nsq = sched[i], idx = sched[i + 1];
+    for (int t = 0; t < nsq; ++t) {
+      if (first_sq == SIZE_MAX) first_sq = prog.size();
+      prog.push_back(loaded ? op(LOP_SQR, 0, 0, 0) : op(LOP_SQR | LOP_A_FROM_T, 0, first, 0));
+      loaded = true;
+    }
+    if (idx != 0xFFFF) {
+      if (first_sq != SIZE_MAX) {
+        prog[first_sq] |= LOP_PREFETCH | ((uint32_t)idx << 8);
+        prog.push_back(op(LOP_B_READY | LOP_BFREE, idx, 0, 0));
+      } else {
+        prog.push_back(loaded ? op(LOP_BFREE, idx, 0, 0) : op(LOP_A_FROM_T | LOP_BFREE, idx, first, 0));
+      }
+      loaded = true;
+      first_sq = SIZE_MAX;
+    }
+  }
+  if (!loaded) return false;
+  prog.push_back(op(LOP_IOTA | LOP_BFREE, 0, 0, 0));      // Z = Y' (A~, 0), iota = Y' mod p -> the column
+  prog.push_back(op(LOP_B_CONST | LOP_BFREE, 0, 0, 0));   // (1 + p G) = Z (1, 0)
+  std::vector<HBig> K = chain_weights(ph, sched);
+  K[0] = mod(add(K[0], HBig(1)), ph);
+  kf.clear();
+  for (int t = 0; t < LANE_NTILE; ++t) {
+    const std::vector<uint32_t> l = mul_pow2_mod(K[t], RS, ph).limbs(S, LB);
+    kf.insert(kf.end(), l.begin(), l.end());
+  }
+  return true;
+}
+
 // Op list of the factored 4096-bit decryption (d4f_run, kernels_dec4.hpp): the table's 30 one-pass products by the
 // kept (A~, 0) (odd powers stored in tiles 0..15), the sliding-window chain over e = p_h - 2 with B-free multipliers,
 // then Y' (A~, 0) (iota taken before it) and the product with (1, 0) into tile D4F_G. kf gets the closing sum's
@@ -449,13 +514,7 @@ static bool build_dec4f_program(const HBig& ph, size_t RS, std::vector<uint32_t>
   if (!loaded) return false;
   prog.push_back(op(LOP_IOTA, 0, 0, 0));                      // Z = Y' (A~, 0), A~ = tile 0's even component
   prog.push_back(op(LOP_B_CONST | LOP_STORE, 0, 0, D4F_G));   // (1 + p G) = Z (1, 0)
-  std::vector<HBig> K(LANE_NTILE, HBig(0));
-  size_t after = 0;
-  for (size_t i = sched.size(); i >= 2; i -= 2) {
-    const int nsq = sched[i - 2], idx = sched[i - 1];
-    if (idx != 0xFFFF) K[idx] = mod(add(K[idx], mul_pow2_mod(HBig(1), after, ph)), ph);
-    after += (size_t)nsq;
-  }
+  const std::vector<HBig> K = chain_weights(ph, sched);
   kf.clear();
   for (int t = 0; t < LANE_NTILE; ++t) {
     const HBig v = t == 0 ? sub(ph, mul_pow2_mod(HBig(1), RS, ph)) : mul_pow2_mod(K[t], RS, ph);
@@ -664,43 +723,77 @@ static int guard_collect(pai_ctx* c, hipStream_t st) {
 // P - 1 above the bound that g misses has probability about 1/l < 2^-24. G = g^n mod P^2.
 constexpr uint32_t FB_TRIAL_BOUND = 1u << 24;   // = oracle/paillier_oracle.py FB_TRIAL_BOUND
 
+// The primes below FB_TRIAL_BOUND in chunks of 4096 with each chunk's product (a product tree on GMP), built once
+// per process: the small prime factors of P - 1 are then found chunk by chunk as gcd(prod_j mod (P - 1), P - 1)
+// (~0.3 k GMP operations per key instead of 1.08 M single-precision remainders: 66 -> a few ms per half, round 5).
+struct PrimeChunks {
+  std::vector<uint32_t> primes;
+  std::vector<size_t> start;                  // chunk j = primes[start[j] .. start[j + 1])
+  std::vector<std::unique_ptr<Mpz>> prod;
+};
+static void prime_product(const std::vector<uint32_t>& pr, size_t lo, size_t hi, mpz_t out) {
+  if (hi - lo <= 16) {
+    mpz_set_ui(out, 1);
+    for (size_t i = lo; i < hi; ++i) mpz_mul_ui(out, out, pr[i]);
+    return;
+  }
+  const size_t mid = (lo + hi) / 2;
+  Mpz a, b;
+  prime_product(pr, lo, mid, a.v);
+  prime_product(pr, mid, hi, b.v);
+  mpz_mul(out, a.v, b.v);
+}
+static const PrimeChunks& prime_chunks() {
+  static const PrimeChunks pc = [] {
+    PrimeChunks c;
+    c.primes = small_primes(FB_TRIAL_BOUND);
+    constexpr size_t CH = 4096;
+    for (size_t s = 0; s < c.primes.size(); s += CH) {
+      c.start.push_back(s);
+      c.prod.emplace_back(new Mpz());
+      prime_product(c.primes, s, std::min(s + CH, c.primes.size()), c.prod.back()->v);
+    }
+    c.start.push_back(c.primes.size());
+    return c;
+  }();
+  return pc;
+}
+
 static uint32_t fb_base(const HBig& P) {
-  static const std::vector<uint32_t> primes = small_primes(FB_TRIAL_BOUND);
-  const HBig pm1 = sub(P, HBig(1));
-  std::vector<HBig> cof;
-  for (uint32_t l : primes)
-    if (mod_small(pm1, l) == 0) cof.push_back(div_small(pm1, l));
-  HMont M(P);
-  for (uint32_t g = 2; g < 1000000u; ++g) {
+  const PrimeChunks& pc = prime_chunks();
+  Mpz p(P), pm1, t, g;
+  mpz_sub_ui(pm1.v, p.v, 1);
+  std::vector<uint32_t> fac;
+  for (size_t j = 0; j < pc.prod.size(); ++j) {
+    mpz_mod(t.v, pc.prod[j]->v, pm1.v);
+    mpz_gcd(g.v, t.v, pm1.v);
+    if (mpz_cmp_ui(g.v, 1) == 0) continue;
+    for (size_t i = pc.start[j]; i < pc.start[j + 1]; ++i)
+      if (mpz_divisible_ui_p(g.v, pc.primes[i])) fac.push_back(pc.primes[i]);
+  }
+  std::vector<std::unique_ptr<Mpz>> cof;
+  for (uint32_t l : fac) {
+    cof.emplace_back(new Mpz());
+    mpz_divexact_ui(cof.back()->v, pm1.v, l);
+  }
+  Mpz gb, r;
+  for (uint32_t cand = 2; cand < 1000000u; ++cand) {
     bool ok = true;
-    for (const HBig& e : cof)
-      if (cmp(M.pow(HBig(g), e), HBig(1)) == 0) {
-        ok = false;
-        break;
+    for (size_t k = 0; k < fac.size() && ok; ++k) {
+      if (fac[k] == 2) {   // g^((P-1)/2) == 1 iff g is a square mod P (Euler's criterion)
+        mpz_set_ui(gb.v, cand);
+        ok = mpz_jacobi(gb.v, p.v) != 1;
+      } else {
+        mpz_set_ui(gb.v, cand);
+        mpz_powm(r.v, gb.v, cof[k]->v, p.v);
+        ok = mpz_cmp_ui(r.v, 1) != 0;
       }
-    if (ok) return g;
+    }
+    if (ok) return cand;
   }
   return 0;
 }
 
-// floor(a / m) by binary long division (host, one-time)
-static HBig div_big(const HBig& a, const HBig& m) {
-  HBig r, q;
-  q.w.assign(a.w.size() + 1, 0);
-  for (size_t i = a.bits(); i-- > 0;) {
-    r = shl1(r);
-    if (a.bit(i)) {
-      if (r.w.empty()) r.w.push_back(0);
-      r.w[0] |= 1;
-    }
-    if (cmp(r, m) >= 0) {
-      r = sub(r, m);
-      q.w[i / 32] |= 1u << (i % 32);
-    }
-  }
-  q.trim();
-  return q;
-}
 
 // Public-key encryption on split pairs (kernels_pe.hpp) for n of 1537..2048 bits: S = 74 limbs of n, R =
 // 2^(28 S) >= 2^24 n. Constants: n, (1 - R) and (1 - R^2) mod n, the pair of R^3 mod n^2, the op list for n.
@@ -1052,7 +1145,7 @@ static int ensure_fb(pai_ctx* c) {
     for (int k = 0; k < K; ++k) {
       const std::vector<uint32_t> v = M2.from(x).limbs(sb, LB);
       std::copy(v.begin(), v.end(), bl.begin() + (size_t)k * sb);
-      for (int q = 0; q < W; ++q) x = M2.mul(x, x);
+      x = M2.sqr_k(x, (size_t)W);
     }
     // c0 folding: n 2^(CB c) mod p_h^2 (c < NC) and 2^PB p_h^2 (the group kernel uses 74's geometry:
     // 16-bit chunks, PB = 20)
@@ -1100,9 +1193,9 @@ static int ensure_fb(pai_ctx* c) {
       for (int k = 0; k < K; ++k) {
         HBig z = y;
         split(mul_pow2_mod(M2.from(z), RS, m2), bases_p);                 // B_k R
-        for (int q = 0; q < LOb; ++q) z = M2.mul(z, z);
+        z = M2.sqr_k(z, (size_t)LOb);
         split(mul_pow2_mod(M2.from(z), RS, m2), bases_p);                 // B_k^(2^LO) R
-        for (int q = 0; q < W; ++q) y = M2.mul(y, y);
+        y = M2.sqr_k(y, (size_t)W);
       }
       const HBig other = primes[1 - h];
       std::vector<uint32_t> nmr_p;   // the same times R (k_fbs: gamma R joins the b sum)
@@ -1166,9 +1259,9 @@ static int ensure_fb(pai_ctx* c) {
       for (int k = 0; k < K; ++k) {
         HBig z = y;
         split(mul_pow2_mod(M2.from(z), RS, m2), bases_p);
-        for (int q = 0; q < LOb; ++q) z = M2.mul(z, z);
+        z = M2.sqr_k(z, (size_t)LOb);
         split(mul_pow2_mod(M2.from(z), RS, m2), bases_p);
-        for (int q = 0; q < W; ++q) y = M2.mul(y, y);
+        y = M2.sqr_k(y, (size_t)W);
       }
       for (int k = 0; k < 4; ++k) {
         const std::vector<uint32_t> v = mul_pow2_mod(mod(primes[1 - h], P), (size_t)16 * k, P).limbs(FBGP_S, LB);
@@ -1299,6 +1392,7 @@ static int ensure_fb(pai_ctx* c) {
     return fb_unavailable(c, "table construction failed");
   if (guard_collect(c, nullptr)) return fb_unavailable(c, pai_last_error());
   for (void* p : lohi) fb_scratch.push_back(p);
+  SetupTrace tr_f("  scratch frees");
   for (void* p : fb_scratch) {
     c->fb_mem.erase(std::find(c->fb_mem.begin(), c->fb_mem.end(), p));
     (void)hipFree(p);
@@ -1503,22 +1597,27 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
       const HBig& ph = primes[h];
       const HBig& other = primes[1 - h];
       const HBig& m2 = sq[h];
-      std::vector<uint32_t> pd, pe;
-      if (!build_lane_program(sub(ph, HBig(1)), pd) || !build_lane_program(ph, pe)) return 0;
+      std::vector<uint32_t> pd, pe, kf;
+      const bool decf = !(xcheck_env("FLEXPAI_DECF") && atoi(xcheck_env("FLEXPAI_DECF")) == 0);
+      if (!(decf ? build_decf_lane_program(ph, RA, sa, pd, kf) : build_lane_program(sub(ph, HBig(1)), pd)) ||
+          !build_lane_program(ph, pe))
+        return 0;
+      c->decf = decf;
       HBig oi = inv_mod(mod(other, ph), ph);
       HBig coef = inv_mod(sq[1 - h], m2);
       if (oi.is_zero() || coef.is_zero()) return 0;
       const uint32_t mp1 = mont_prime(ph, LB);
-      uint32_t *dph, *dck, *dhR, *dpm1, *done, *dprog, *dr2, *dcoef, *dpe;
+      uint32_t *dph, *dck, *dhR, *dpm1, *done, *dprog, *dr2, *dcoef, *dpe, *dkf = nullptr;
       if ((rc = upload(c, ph.limbs(sa, LB), &dph)) ||
           (rc = upload(c, split(mul_pow2_mod(HBig(1), RA * (kp + 1), m2), ph), &dck)) ||
           (rc = upload(c, mul_pow2_mod(sub(ph, oi), RA, ph).limbs(sa, LB), &dhR)) ||
           (rc = upload(c, sub(ph, HBig(1)).limbs(sa, LB), &dpm1)) || (rc = upload(c, one, &done)) ||
           (rc = upload(c, pd, &dprog)) || (rc = upload(c, split(mul_pow2_mod(HBig(1), 2 * RA, m2), ph), &dr2)) ||
-          (rc = upload(c, split(coef, ph), &dcoef)) || (rc = upload(c, pe, &dpe)))
+          (rc = upload(c, split(coef, ph), &dcoef)) || (rc = upload(c, pe, &dpe)) ||
+          (!kf.empty() && (rc = upload(c, kf, &dkf))))
         return rc;
       dp[h] = DecPairHalf{dph, dck, dhR, dpm1, mp1, 0u};
-      pw[h] = CrtHalf{dph, nullptr, done, dprog, (int)pd.size(), mp1};
+      pw[h] = CrtHalf{dph, dkf, done, dprog, (int)pd.size(), mp1};
       pbh[h] = CrtHalf{dph, dr2, dcoef, dpe, (int)pe.size(), mp1};
     }
     std::vector<DecPairHalf> dpv(dp, dp + 2);
@@ -2591,7 +2690,7 @@ static int launch_dec_pair(pai_ctx* c, const DecParams& d, hipStream_t st) {
   const long long chunk = std::min(N, CRT_CHUNK);
   const int S = c->crt_sa;
   DecLaneGeom g;
-  if (dec_pair_geometry(S, c->cus, chunk, &g)) return fail(PAI_ERR_KEY, "pair decrypt: unsupported size");
+  if (dec_pair_geometry(S, c->cus, chunk, &g, c->decf)) return fail(PAI_ERR_KEY, "pair decrypt: unsupported size");
   int rc = ensure_scratch(c, g.scratch_bytes);
   if (rc) return rc;
   if ((rc = ensure_work(c, (size_t)4 * S * chunk * 4))) return rc;
@@ -2623,7 +2722,7 @@ static int launch_dec_pair(pai_ctx* c, const DecParams& d, hipStream_t st) {
     f.status = d.status + off;
     f.raw = d.raw ? d.raw + (size_t)off * c->pt_words : nullptr;
     f.pt_words = c->pt_words;
-    HIPCHK(dec_pair_launch(S, pre, pw, f, g, st, ev));
+    HIPCHK(dec_pair_launch(S, pre, pw, f, g, st, ev, c->decf));
   }
   return 0;
 }

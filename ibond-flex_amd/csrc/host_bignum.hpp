@@ -1,6 +1,10 @@
-// Minimal host-side big integer helpers for one-time key setup (Montgomery constants,
-// CRT constants, exponent schedules). Not on any per-element path.
+// Host-side big integers for the per-key setup (Montgomery constants, CRT constants, exponent schedules, the
+// fixed-base tables' bases and generators). Not on any per-element path -- but on the re-keying caller's path
+// (HE_SA_FT draws a keypair per exchange, he_sa_ft/train.py:38-39), so the arithmetic is GMP's (round 5: the
+// earlier bit-serial division and shift loops cost ~0.25 s per fresh key). HBig stays a little-endian
+// word vector; the operations convert through mpz_t.
 #pragma once
+#include <gmp.h>
 #include <stdint.h>
 
 #include <algorithm>
@@ -39,10 +43,11 @@ struct HBig {
   // `lb`-bit limbs (device limb width), zero padded to n limbs
   std::vector<uint32_t> limbs(size_t n, int lb) const {
     std::vector<uint32_t> out(n, 0);
+    const uint32_t mask = lb >= 32 ? 0xFFFFFFFFu : (1u << lb) - 1u;
     for (size_t k = 0; k < n; ++k) {
-      uint32_t v = 0;
-      for (int b = 0; b < lb; ++b) v |= (uint32_t)bit((size_t)lb * k + b) << b;
-      out[k] = v;
+      const size_t b = (size_t)lb * k, i = b / 32, o = b % 32;
+      const uint64_t lo = i < w.size() ? w[i] : 0u, hi = i + 1 < w.size() ? w[i + 1] : 0u;
+      out[k] = (uint32_t)(((hi << 32) | lo) >> o) & mask;
     }
     return out;
   }
@@ -50,6 +55,29 @@ struct HBig {
     std::vector<uint32_t> out(n, 0);
     for (size_t i = 0; i < std::min(n, w.size()); ++i) out[i] = w[i];
     return out;
+  }
+};
+
+// RAII mpz_t and the conversions HBig <-> mpz
+struct Mpz {
+  mpz_t v;
+  Mpz() { mpz_init(v); }
+  explicit Mpz(const HBig& a) {
+    mpz_init(v);
+    if (!a.w.empty()) mpz_import(v, a.w.size(), -1, sizeof(uint32_t), 0, 0, a.w.data());
+  }
+  ~Mpz() { mpz_clear(v); }
+  Mpz(const Mpz&) = delete;
+  Mpz& operator=(const Mpz&) = delete;
+  HBig big() const {
+    HBig r;
+    if (mpz_sgn(v) == 0) return r;
+    r.w.assign((mpz_sizeinbase(v, 2) + 31) / 32, 0);
+    size_t cnt = 0;
+    mpz_export(r.w.data(), &cnt, -1, sizeof(uint32_t), 0, 0, v);
+    r.w.resize(cnt);
+    r.trim();
+    return r;
   }
 };
 
@@ -87,20 +115,9 @@ inline HBig sub(const HBig& a, const HBig& b) {
   return r;
 }
 inline HBig mul(const HBig& a, const HBig& b) {
-  HBig r;
-  if (a.is_zero() || b.is_zero()) return r;
-  r.w.assign(a.w.size() + b.w.size(), 0);
-  for (size_t i = 0; i < a.w.size(); ++i) {
-    uint64_t c = 0;
-    for (size_t j = 0; j < b.w.size(); ++j) {
-      c += (uint64_t)a.w[i] * b.w[j] + r.w[i + j];
-      r.w[i + j] = (uint32_t)c;
-      c >>= 32;
-    }
-    r.w[i + b.w.size()] = (uint32_t)c;
-  }
-  r.trim();
-  return r;
+  Mpz x(a), y(b), r;
+  mpz_mul(r.v, x.v, y.v);
+  return r.big();
 }
 inline HBig shl1(const HBig& a) {
   HBig r;
@@ -120,49 +137,36 @@ inline HBig shr1(const HBig& a) {
   r.trim();
   return r;
 }
-// a mod m by binary long division
+// a mod m
 inline HBig mod(const HBig& a, const HBig& m) {
-  HBig r;
-  for (size_t i = a.bits(); i-- > 0;) {
-    r = shl1(r);
-    if (a.bit(i)) {
-      if (r.w.empty()) r.w.push_back(0);
-      r.w[0] |= 1;
-    }
-    if (cmp(r, m) >= 0) r = sub(r, m);
-  }
-  return r;
+  Mpz x(a), y(m), r;
+  mpz_mod(r.v, x.v, y.v);
+  return r.big();
+}
+// floor(a / m)
+inline HBig div_big(const HBig& a, const HBig& m) {
+  Mpz x(a), y(m), r;
+  mpz_fdiv_q(r.v, x.v, y.v);
+  return r.big();
 }
 // (a * 2^k) mod m, a < m
 inline HBig mul_pow2_mod(HBig a, size_t k, const HBig& m) {
-  for (size_t i = 0; i < k; ++i) {
-    a = shl1(a);
-    if (cmp(a, m) >= 0) a = sub(a, m);
-  }
-  return a;
+  Mpz x(a), y(m), r;
+  mpz_mul_2exp(r.v, x.v, k);
+  mpz_mod(r.v, r.v, y.v);
+  return r.big();
 }
-// a^{-1} mod m for odd m (binary extended Euclid); returns empty HBig if not invertible
+// a^{-1} mod m; returns empty HBig if not invertible
 inline HBig inv_mod(const HBig& a0, const HBig& m) {
-  HBig u = mod(a0, m), v = m, x1(1), x2(0);
-  if (u.is_zero()) return HBig();
-  auto half = [&](HBig& x) {
-    if (x.is_odd()) x = add(x, m);
-    x = shr1(x);
-  };
-  HBig one(1);
-  while (cmp(u, one) != 0 && cmp(v, one) != 0) {
-    while (!u.is_odd()) { u = shr1(u); half(x1); }
-    while (!v.is_odd()) { v = shr1(v); half(x2); }
-    if (cmp(u, v) >= 0) {
-      u = sub(u, v);
-      x1 = cmp(x1, x2) >= 0 ? sub(x1, x2) : sub(add(x1, m), x2);
-    } else {
-      v = sub(v, u);
-      x2 = cmp(x2, x1) >= 0 ? sub(x2, x1) : sub(add(x2, m), x1);
-    }
-    if (u.is_zero() || v.is_zero()) return HBig();
-  }
-  return cmp(u, one) == 0 ? mod(x1, m) : mod(x2, m);
+  Mpz x(a0), y(m), r;
+  if (!mpz_invert(r.v, x.v, y.v)) return HBig();
+  return r.big();
+}
+// a^e mod m
+inline HBig pow_mod(const HBig& a, const HBig& e, const HBig& m) {
+  Mpz x(a), y(e), z(m), r;
+  mpz_powm(r.v, x.v, y.v, z.v);
+  return r.big();
 }
 // -m^{-1} mod 2^lb for odd m
 inline uint32_t mont_prime(const HBig& m, int lb) {
@@ -204,62 +208,32 @@ inline uint32_t mod_small(const HBig& a, uint32_t d) {
   return (uint32_t)r;
 }
 
-// Word-level (32-bit) Montgomery arithmetic modulo an odd m, for the one-time host work that needs
-// real modular exponentiations (fixed-base obfuscation setup): ~1000x faster than mod().
+// Modular arithmetic modulo m for the one-time host work that needs real exponentiations (fixed-base setup, batch
+// inversion). The interface of a Montgomery domain (to / mul / from, r2 the domain's R^2), implemented in the plain
+// domain on GMP: to(a) = a mod m, from(a) = a, r2 = 1, mul = a b mod m -- every caller's to/mul/from sequence means
+// the same value.
 struct HMont {
   HBig m;
-  size_t s = 0;          // words
-  uint32_t mp = 0;       // -m^-1 mod 2^32
-  HBig r2;               // R^2 mod m, R = 2^(32 s)
-  explicit HMont(const HBig& mod_) : m(mod_), s(mod_.w.size()) {
-    uint32_t x = 1;
-    for (int i = 0; i < 6; ++i) x *= 2u - m.w[0] * x;
-    mp = 0u - x;
-    r2 = mul_pow2_mod(HBig(1), 64 * s, m);
-  }
-  // CIOS: a b R^-1 mod m (a, b < m)
+  HBig r2{1};
+  explicit HMont(const HBig& mod_) : m(mod_) {}
   HBig mul(const HBig& a, const HBig& b) const {
-    std::vector<uint64_t> t(s + 2, 0);
-    for (size_t i = 0; i < s; ++i) {
-      const uint64_t ai = i < a.w.size() ? a.w[i] : 0;
-      uint64_t c = 0;
-      for (size_t j = 0; j < s; ++j) {
-        const uint64_t v = t[j] + ai * (j < b.w.size() ? b.w[j] : 0) + c;
-        t[j] = (uint32_t)v;
-        c = v >> 32;
-      }
-      uint64_t v = t[s] + c;
-      t[s] = (uint32_t)v;
-      t[s + 1] = v >> 32;
-      const uint64_t q = (uint32_t)((uint32_t)t[0] * mp);
-      v = t[0] + q * m.w[0];
-      c = v >> 32;
-      for (size_t j = 1; j < s; ++j) {
-        v = t[j] + q * m.w[j] + c;
-        t[j - 1] = (uint32_t)v;
-        c = v >> 32;
-      }
-      v = t[s] + c;
-      t[s - 1] = (uint32_t)v;
-      t[s] = t[s + 1] + (v >> 32);
-    }
-    HBig r;
-    r.w.assign(s + 1, 0);
-    for (size_t i = 0; i <= s; ++i) r.w[i] = (uint32_t)t[i];
-    r.trim();
-    if (cmp(r, m) >= 0) r = sub(r, m);
-    return r;
+    Mpz x(a), y(b), z(m), r;
+    mpz_mul(r.v, x.v, y.v);
+    mpz_mod(r.v, r.v, z.v);
+    return r.big();
   }
-  HBig to(const HBig& a) const { return mul(mod(a, m), r2); }
-  HBig from(const HBig& a) const { return mul(a, HBig(1)); }
+  HBig to(const HBig& a) const { return mod(a, m); }
+  HBig from(const HBig& a) const { return a; }
   // a^e mod m (plain in, plain out)
-  HBig pow(const HBig& a, const HBig& e) const {
-    HBig x = to(a), acc = to(HBig(1));
-    for (size_t i = e.bits(); i-- > 0;) {
-      acc = mul(acc, acc);
-      if (e.bit(i)) acc = mul(acc, x);
+  HBig pow(const HBig& a, const HBig& e) const { return pow_mod(a, e, m); }
+  // x^(2^k) mod m
+  HBig sqr_k(const HBig& x0, size_t k) const {
+    Mpz x(x0), z(m);
+    for (size_t i = 0; i < k; ++i) {
+      mpz_mul(x.v, x.v, x.v);
+      mpz_mod(x.v, x.v, z.v);
     }
-    return from(acc);
+    return x.big();
   }
 };
 

@@ -38,6 +38,29 @@ struct FbsGeom<37> {   // 2048-bit keys: p_h < 2^1024, R = 2^1036
 };
 template <int S>
 constexpr int fbs_row_quads() { return FbsGeom<S>::QA + FbsGeom<S>::QAP + FbsGeom<S>::QB; }
+
+// Row-layout A/B (round 5; tools/ab_fbs_rows.sh): builds of this header with FBS_AB set are
+// measurement-only libraries, never the product. FBS_AB & 1 ("T", traffic): rows addressed at a 384-B stride (three
+// aligned 128-B lines) and only the b R quads that fit in them fetched (the rest zero) -- the bytes of packed 384-B
+// rows, wrong ciphertexts; FBS_AB & 2 ("I", instructions): every digit of a and a' costs the v_alignbit + v_and that
+// cutting a 28-bit digit out of packed 32-bit words costs (on the same digit: same ciphertexts).
+#ifndef FBS_AB
+#define FBS_AB 0
+#endif
+template <int S>
+constexpr int fbs_row_stride() { return (FBS_AB & 1) && S == 37 ? 24 : fbs_row_quads<S>(); }   // quads between rows
+template <int S>
+constexpr int fbs_b_fetch() { return (FBS_AB & 1) ? FbsGeom<S>::QB / 4 : FbsGeom<S>::QB / 2; }   // b R quads per lane
+__device__ __forceinline__ uint32_t fbs_ab_extract(uint32_t d) {
+#if FBS_AB & 2
+  uint32_t r, z = 0;
+  asm volatile("v_alignbit_b32 %0, %1, %2, %3" : "=v"(r) : "v"(d), "v"(d), "v"(z));
+  asm volatile("v_and_b32 %0, 0x0fffffff, %0" : "+v"(r));
+  return r;
+#else
+  return d;
+#endif
+}
 template <int S>
 constexpr int fbs_lds_quads() { return FbsGeom<S>::QA + FbsGeom<S>::QAP; }
 
@@ -217,7 +240,7 @@ struct FbsPairReader {
       static_assert(pending >= 0 && pending <= 15, "lgkmcnt range");
       asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(q[g]) : "i"(pending));
     }
-    return quad_word<J % 4>(q[g]);
+    return fbs_ab_extract(quad_word<J % 4>(q[g]));
   }
 };
 
@@ -233,10 +256,10 @@ __device__ __forceinline__ void fbs_row_fetch(const uint4* row, uint32_t lb, int
     asm volatile("" : "+s"(dst));
     __builtin_amdgcn_global_load_lds((const void*)(src + 2 * g), (__attribute__((address_space(3))) void*)(size_t)dst, 16, 0, 0);
   }
-  constexpr int QH = G::QB / 2;
-  const fbp_u32x4* b = reinterpret_cast<const fbp_u32x4*>(row + G::QA + G::QAP + QH * tig);
+  constexpr int QH = G::QB / 2, QF = fbs_b_fetch<S>();
+  const fbp_u32x4* b = reinterpret_cast<const fbp_u32x4*>(row + G::QA + G::QAP + QF * tig);
 #pragma unroll
-  for (int q = 0; q < QH; ++q) bv[q] = b[q];
+  for (int q = 0; q < QH; ++q) bv[q] = q < QF ? b[q] : fbp_u32x4{0u, 0u, 0u, 0u};
 }
 
 #if FLEXPAI_XCHECK
@@ -256,7 +279,7 @@ __device__ __forceinline__ uint32_t fbs_guard_digit(const FbpParams& p, int h, i
 template <int S>
 __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbs(FbpParams p) {
   using G = FbsGeom<S>;
-  constexpr int PW = G::PW, TQ = fbs_row_quads<S>(), WB = fbs_wave_buf_bytes<S>();
+  constexpr int PW = G::PW, TQ = fbs_row_stride<S>(), WB = fbs_wave_buf_bytes<S>();
   static_assert(PW == 32 || PW == 16, "b sum halves");
   constexpr int HW = PW / 2;   // b sum words per lane
   __shared__ __attribute__((aligned(16))) uint8_t lbuf[(LANE_BLOCK / 64) * 2 * WB];

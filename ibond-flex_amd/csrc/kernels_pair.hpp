@@ -195,8 +195,165 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_dec_pre_pair(DecPairPreParams p)
   }
 }
 
-// x_h = c~^(p_h - 1) * (1, 0) R^-1: the plain pair of c^(p_h - 1) mod p_h^2
+// ---- the factored chain (round 5; tools/decf_model.py restates the algebra, tests/test_decf_model.py checks it)
+// The window table keeps FULL pairs (a general pair product costs 5 S^2 here against 4 S^2 for a B-free one, so the
+// 15 table products stay general), but the chain's multipliers are B-free: entry P_t = a_t (1 + p b_t), the chain
+// multiplies by (a_t, 0) (mont_mul_b0) and the dropped factors, 1 + p s with s = sum_t K_t b_t, are restored at the end
+// from the chain's own Fermat inverse -- it runs p - 2, so its result's A component is iota = A~^-1 R^2 mod p:
+//   Y'       chain over p - 2, multipliers (a_t, 0) (the first load takes the full pair)
+//   1 + p G  = mm(mm(Y', (A~, 0)), (1, 0))      (the closing (A~, 0) drops (1 + p u) = (1 + p b_1): slot 1's weight + 1)
+//   delta    = REDC(acc iota), acc = Horner over j = 15..0 of c_j = REDC(H_{2j+1} K'_{2j+1}) in w = REDC(iota iota)
+//   output   (A, G + delta), B reduced below 2p
+// Per 1024-bit p_h: ~170 chain multiplies at 4 S^2 instead of 5 S^2, against 34 one-row passes (2 S^2) of the Horner
+// sum and one more product. iota and w live in the lane's LDS column (the multiplier digits read only its A half
+// once the chain is over: w at words 0 .. S-1, iota at DECF_IOTA ..), K'_t comes from global memory (uniform), the
+// pair (1 + p G) waits in the spare tile DECF_G.
+constexpr uint32_t LOP_BFREE = 1u << 15;   // MUL op: the multiplier is the B-free (a_t, 0) of the tile in the column
+constexpr int DECF_G = LANE_NTILE;         // spare tile (the lane scratch's staging area): the pair (1 + p G)
 template <int S>
+constexpr int decf_iota() { return S + 1; }   // column word of iota's limb 0 (limb S - 1 of the A half stays intact)
+static_assert(tile_quads<2 * 37>() * 4 >= 37 + 1 + 37 && tile_quads<2 * 19>() * 4 >= 19 + 1 + 19, "iota fits the column");
+
+template <int S>
+struct PairLdsDigitA {   // the multiplier's A digits a_J from this lane's LDS column (word J), one ahead
+  const uint4* bcol;
+  int off;
+  uint32_t na;
+  __device__ __forceinline__ uint32_t word(int t) const {
+    return reinterpret_cast<const uint32_t*>(bcol + (t >> 2) * LANE_BLOCK)[t & 3];
+  }
+  __device__ __forceinline__ PairLdsDigitA(const uint4* c, int o) : bcol(c), off(o) { na = word(off); }
+  template <int J>
+  __device__ __forceinline__ uint32_t operator()(std::integral_constant<int, J>) {
+    const uint32_t r = na;
+    if constexpr (J + 1 < S) na = word(off + J + 1);
+    return r;
+  }
+};
+template <int S>
+__device__ __forceinline__ void col_put(uint4* bcol, int off, const uint32_t (&x)[S]) {
+#pragma unroll
+  for (int j = 0; j < S; ++j) reinterpret_cast<uint32_t*>(bcol + ((off + j) >> 2) * LANE_BLOCK)[(off + j) & 3] = x[j];
+}
+template <int S, int G0, int... Gs>   // the B limbs of a pair tile (limbs S .. 2S-1 of its 2S-limb image)
+__device__ __forceinline__ void ptile_load_b(const LaneScratch& t, int k, uint32_t (&B)[S], std::integer_sequence<int, Gs...>) {
+  constexpr int TQ = tile_quads<2 * S>();
+  uint32_t A[S];
+  (unpack_pair_quad<S, G0 + Gs>(t.quad(k * TQ + G0 + Gs), A, B), ...);
+}
+
+template <int S>
+__device__ __forceinline__ void decf_run(uint32_t (&A)[S], uint32_t (&B)[S], const LaneScratch& t, const uint32_t* __restrict__ prog,
+                                         int nprog, const uint32_t* __restrict__ kf, const uint32_t (&m)[S], uint32_t mprime) {
+  constexpr int TQ = tile_quads<2 * S>();
+  constexpr int IO = decf_iota<S>();
+  using Q = std::make_integer_sequence<int, TQ>;
+  __shared__ uint4 ldsb[TQ * LANE_BLOCK];
+  uint4* bcol = ldsb + threadIdx.x;
+  uint4* brow = ldsb + (threadIdx.x & ~63u);
+  // the table (ops 0 .. LANE_NTILE - 1: x~^2 into the column, then general products by it), then the chain and the two
+  // closing products (squares and B-free products only) -- two loops, so that neither holds three product bodies
+  int i = 0;
+  for (; i < LANE_NTILE && i < nprog; ++i) {
+    const uint32_t op = lane_op(prog, i);
+    if (op & LOP_A_FROM_T) {
+      ptile_load<S>(t, (op >> 16) & 0xFF, A, B, Q{});
+#pragma unroll
+      for (int j = 0; j < S; ++j) asm volatile("" : "+v"(A[j]), "+v"(B[j]));
+    }
+    if (op & LOP_SQR) {
+      pair::mont_sqr<S>(A, B, m, mprime);
+    } else {
+      lds_dma_wait();
+      pair::mont_mul<S>(A, B, PairLdsDigits<S>(bcol), m, mprime);
+    }
+    if (op & LOP_STORE) ptile_store<S>(t, op >> 24, A, B, Q{});
+    if (op & LOP_B_SET) pcol_store<S>(bcol, A, B, Q{});
+  }
+  for (; i < nprog; ++i) {
+    const uint32_t op = lane_op(prog, i);
+    const int bidx = (op >> 8) & 0x7F;
+    if (op & LOP_A_FROM_T) {
+      ptile_load<S>(t, (op >> 16) & 0xFF, A, B, Q{});
+#pragma unroll
+      for (int j = 0; j < S; ++j) asm volatile("" : "+v"(A[j]), "+v"(B[j]));
+    }
+    if (op & LOP_SQR) {
+      if (op & LOP_PREFETCH) ltile_to_lds<2 * S>(t, bidx, brow);
+      pair::mont_sqr<S>(A, B, m, mprime);
+    } else {
+      if (op & LOP_B_CONST) {   // (1, 0): the A half only (iota sits above it)
+        uint32_t one[S];
+#pragma unroll
+        for (int j = 0; j < S; ++j) one[j] = j == 0 ? 1u : 0u;
+        col_put<S>(bcol, 0, one);
+      } else if (!(op & LOP_B_READY)) {
+        ltile_to_lds<2 * S>(t, bidx, brow);
+      }
+      lds_dma_wait();
+      if (op & LOP_IOTA) col_put<S>(bcol, IO, A);   // iota = Y' mod p (after the DMA of the multiplier's tile)
+      pair::mont_mul_b0<S>(A, B, PairLdsDigitA<S>(bcol, 0), m, mprime);   // every product here is by a B-free (a_t, 0)
+    }
+  }
+  ptile_store<S>(t, DECF_G, A, B, Q{});   // 1 + p G
+  // w = REDC(iota iota) -> the column's A half
+  {
+    uint32_t X[S];
+    PairLdsDigitA<S> rd(bcol, IO);
+#pragma unroll
+    for (int j = 0; j < S; ++j) X[j] = rd.word(IO + j);
+    uint64_t P[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) P[j] = 0;
+    pair::redc_row<S>(P, X, rd, m, mprime);
+    col_put<S>(bcol, 0, X);
+  }
+  // acc = Horner over j = 15 .. 0 of c_j = REDC(H_{2j+1} K'_j) in w; A holds acc
+#pragma unroll 1
+  for (int j = LANE_NTILE - 1; j >= 0; --j) {
+    uint64_t P[S];
+    {
+      ptile_load_b<S, S / 4>(t, j, B, std::make_integer_sequence<int, TQ - S / 4>{});
+#pragma unroll
+      for (int i = 0; i < S; ++i) P[i] = 0;
+      const uint32_t* kj = kf + (size_t)j * S;
+      pair::redc_row<S>(P, B, [&](auto J) { return kj[decltype(J)::value]; }, m, mprime);   // c_j
+    }
+#pragma unroll
+    for (int i = 0; i < S; ++i) P[i] = B[i];
+    if (j == LANE_NTILE - 1) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) A[i] = 0;
+    }
+    pair::redc_row<S>(P, A, PairLdsDigitA<S>(bcol, 0), m, mprime);   // acc = REDC(c_j + acc w)
+  }
+  {   // delta = REDC(acc iota)
+    uint64_t P[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) P[i] = 0;
+    pair::redc_row<S>(P, A, PairLdsDigitA<S>(bcol, IO), m, mprime);
+  }
+  // (A_G, G + delta): G, delta < 2p; B reduced below 2p for k_dec_fin_pair
+  {
+    uint32_t ga[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) ga[j] = A[j];
+    ptile_load<S>(t, DECF_G, A, B, Q{});
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const uint32_t v = B[j] + ga[j] + c;
+      B[j] = v & lane::LMASK;
+      c = v >> lane::LB;
+    }
+    lane::cond_sub<S>(B, m);
+    lane::cond_sub<S>(B, m);
+  }
+}
+
+// x_h = c~^(p_h - 1) * (1, 0) R^-1: the plain pair of c^(p_h - 1) mod p_h^2. FACTORED: the B-free chain (decf_run, the
+// product); otherwise the general chain (run_pair_program; the test build's cross-check)
+template <int S, bool FACTORED>
 __global__ __launch_bounds__(LANE_BLOCK, LANE_OCC) void k_dec_pow_pair(CrtParams p) {
   const int half = blockIdx.y;
   const CrtHalf* H = p.halves + half;
@@ -218,7 +375,8 @@ __global__ __launch_bounds__(LANE_BLOCK, LANE_OCC) void k_dec_pow_pair(CrtParams
       B[j] = p.yin[((size_t)half * 2 * S + S + j) * p.n + ii];
     }
     ptile_store<S>(tl, 0, A, B, std::make_integer_sequence<int, tile_quads<2 * S>()>{});
-    run_pair_program<S>(A, B, tl, prog, nprog, c1, m, mprime);
+    if constexpr (FACTORED) decf_run<S>(A, B, tl, prog, nprog, H->c0, m, mprime);
+    else run_pair_program<S>(A, B, tl, prog, nprog, c1, m, mprime);
     if (i < p.n) {
 #pragma unroll
       for (int j = 0; j < S; ++j) {

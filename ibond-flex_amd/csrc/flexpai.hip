@@ -112,6 +112,7 @@ struct pai_ctx {
   int dec4_kchunks = 0;
   // public-key encryption on split pairs (kernels_pe.hpp): 2048-bit n, the default ($FLEXPAI_PAIR=0: k_encrypt)
   bool pe_ok = false;
+  bool pef_ok = false;          // the factored public-key chain (k_pe_pow_f) is set up ($FLEXPAI_PEF=0, test build: off)
   PeConst* d_pe = nullptr;
   CrtHalf* d_dec_pow = nullptr;   // [2] exponentiation halves: p_h^2, op list for p_h - 1
   uint32_t *d_dec_p = nullptr, *d_dec_q = nullptr, *d_dec_qinvR = nullptr, *d_dec_nl = nullptr, *d_dec_maxint = nullptr;
@@ -475,6 +476,50 @@ static bool build_decf_lane_program(const HBig& ph, size_t RS, int S, std::vecto
   return true;
 }
 
+// Op list of the factored public-key chain (d4f_run<S, true>, kernels_pe.hpp k_pe_pow_f): the table's 30 one-pass
+// products by the kept (A_r, 0) (odd powers into tiles 0..15, tile 0 = (A_r, 0)), the sliding-window chain over n with
+// B-free multipliers, then the product with (1, 0) into tile D4F_G. kf: K'_t = R K_t mod n (entry 1 is B-free: H_1 = 0).
+static bool build_pef_program(const HBig& n, size_t RS, std::vector<uint32_t>& prog, std::vector<uint32_t>& kf) {
+  if (n.bits() < 8) return false;
+  std::vector<uint16_t> sched;
+  int first = 0;
+  sliding_schedule(n, sched, first);
+  auto op = [](uint32_t flags, int bidx, int aidx, int sidx) {
+    return flags | ((uint32_t)bidx << 8) | ((uint32_t)aidx << 16) | ((uint32_t)sidx << 24);
+  };
+  prog.clear();
+  for (int t = 2; t < 2 * LANE_NTILE; ++t) prog.push_back(op(LOP_B_READY | ((t & 1) ? LOP_STORE : 0u), 0, 0, (t - 1) / 2));
+  bool loaded = false;
+  size_t first_sq = SIZE_MAX;
+  for (size_t i = 0; i + 1 < sched.size(); i += 2) {
+    const int nsq = sched[i], idx = sched[i + 1];
+    for (int t = 0; t < nsq; ++t) {
+      if (first_sq == SIZE_MAX) first_sq = prog.size();
+      prog.push_back(loaded ? op(LOP_SQR, 0, 0, 0) : op(LOP_SQR | LOP_A_FROM_T, 0, first, 0));
+      loaded = true;
+    }
+    if (idx != 0xFFFF) {
+      if (first_sq != SIZE_MAX) {
+        prog[first_sq] |= LOP_PREFETCH | ((uint32_t)idx << 8);
+        prog.push_back(op(LOP_B_READY, idx, 0, 0));
+      } else {
+        prog.push_back(loaded ? op(0, idx, 0, 0) : op(LOP_A_FROM_T, idx, first, 0));
+      }
+      loaded = true;
+      first_sq = SIZE_MAX;
+    }
+  }
+  if (!loaded) return false;
+  prog.push_back(op(LOP_B_CONST | LOP_STORE, 0, 0, D4F_G));   // Z = Y' (1, 0)
+  const std::vector<HBig> K = chain_weights(n, sched);
+  kf.clear();
+  for (int t = 0; t < LANE_NTILE; ++t) {
+    const std::vector<uint32_t> l = mul_pow2_mod(K[t], RS, n).limbs(D4_S, LB);
+    kf.insert(kf.end(), l.begin(), l.end());
+  }
+  return true;
+}
+
 // Op list of the factored 4096-bit decryption (d4f_run, kernels_dec4.hpp): the table's 30 one-pass products by the
 // kept (A~, 0) (odd powers stored in tiles 0..15), the sliding-window chain over e = p_h - 2 with B-free multipliers,
 // then Y' (A~, 0) (iota taken before it) and the product with (1, 0) into tile D4F_G. kf gets the closing sum's
@@ -818,6 +863,25 @@ static int setup_pe(pai_ctx* c, const HBig& n) {
       (rc = upload(c, ck, &dck)) || (rc = upload(c, prog, &dprog)))
     return rc;
   std::vector<PeConst> pc{PeConst{dn, dx1, dxk, dck, dprog, (int)prog.size(), mont_prime(n, LB)}};
+  // the factored chain (kernels_pe.hpp k_pe_pow_f): its program and Horner weights, R^2 mod n, the pair of R^4 mod n^2
+  std::vector<uint32_t> progf, kf;
+  const bool pef = !(xcheck_env("FLEXPAI_PEF") && atoi(xcheck_env("FLEXPAI_PEF")) == 0);
+  if (pef && build_pef_program(n, RS, progf, kf)) {
+    const HBig r4 = mul_pow2_mod(HBig(1), 4 * RS, n2);
+    const HBig q4 = div_big(r4, n), m4 = sub(r4, mul(q4, n));
+    std::vector<uint32_t> ck4 = m4.limbs(D4_S, LB), b4 = q4.limbs(D4_S, LB);
+    ck4.insert(ck4.end(), b4.begin(), b4.end());
+    uint32_t *dpf, *dkf, *dr2, *dck4;
+    if ((rc = upload(c, progf, &dpf)) || (rc = upload(c, kf, &dkf)) ||
+        (rc = upload(c, mul_pow2_mod(HBig(1), 2 * RS, n).limbs(D4_S, LB), &dr2)) || (rc = upload(c, ck4, &dck4)))
+      return rc;
+    pc[0].progf = dpf;
+    pc[0].nprogf = (int)progf.size();
+    pc[0].kf = dkf;
+    pc[0].r2n = dr2;
+    pc[0].cK4 = dck4;
+    c->pef_ok = true;
+  }
   if ((rc = upload(c, pc, &c->d_pe))) return rc;
   c->pe_ok = true;
   return 0;
@@ -2270,8 +2334,11 @@ static int ensure_pfb(pai_ctx* c) {
   return 1;
 }
 
-// Break-even of the public tables: build ~0.08 s + ~9 ns per row (76-limb pair products, 4x a 37-limb row of the
-// key holder's tables), saving 1/415 k - 1/2.5 M s = 2.0 us per element against k_pe_* 
+// Break-even of the public tables, from measurements on one MI355X (round 5, tools/pfb_breakeven.py,
+// profiles/r05_pfb_breakeven_before.json): the build takes 0.114 s + 1.91 ns per row (0.117 / 0.155 / 0.648 s at
+// W = 12 / 16 / 20), and each element then costs 1 / rate(W) on k_sgp (3.05 M / 4.00 M / 4.84 M enc/s) instead of
+// 1 / 503 k on k_pe_* -- 1.99 us -- so the break-even is ~89 k elements at the default W = 16 (the earlier
+// constants were round 3's 415 k and 2.5 M)
 static long long pfb_threshold(pai_ctx* c) {
   if (c->pfb_state != pai_ctx::FB_UNTRIED || !pfb_supported(c)) return 0;
   if (const char* e = getenv("FLEXPAI_PFB_MIN_ELEMS")) return atoll(e);
@@ -2279,8 +2346,10 @@ static long long pfb_threshold(pai_ctx* c) {
   if (!W) return 0;
   int K0, KS;
   pfb_digit_counts(c, W, &K0, &KS);
-  const double build_s = 0.08 + (double)(K0 + PFB_SHORT * KS) * (double)(1ull << W) * 9e-9;
-  return (long long)(build_s / 2.0e-6) + 1;
+  const double build_s = 0.114 + (double)(K0 + PFB_SHORT * KS) * (double)(1ull << W) * 1.91e-9;
+  const double rate = W >= 20 ? 4.84e6 : W >= 16 ? 4.00e6 : 3.05e6;
+  const double save_s = 1.0 / 5.03e5 - 1.0 / rate;
+  return (long long)(build_s / save_s) + 1;
 }
 
 static bool pfb_wanted(pai_ctx* c, long long n) {
@@ -2410,6 +2479,8 @@ int pai_ctx_public_fb_policy(pai_ctx* c, long long* seen, long long* threshold) 
 }
 
 // public-key encryption on split pairs (kernels_pe.hpp, engine_pe.hip), in chunks of CRT_CHUNK elements
+static int batch_invert(pai_ctx* c, uint32_t* x, const uint8_t* flag, long long n, hipStream_t st);
+
 static int launch_pe(pai_ctx* c, const EncParams& e, hipStream_t st) {
   const long long N = e.n;
   const long long chunk = std::min(N, CRT_CHUNK);
@@ -2418,7 +2489,8 @@ static int launch_pe(pai_ctx* c, const EncParams& e, hipStream_t st) {
   int rc = ensure_scratch(c, g.scratch_bytes);
   if (rc) return rc;
   const size_t xbytes = (size_t)2 * D4_S * 4;   // per element, + 8 for M
-  if ((rc = ensure_work(c, (xbytes + 8) * chunk))) return rc;
+  const size_t awbytes = c->pef_ok ? (size_t)c->ct_words * 4 : 0, iobytes = c->pef_ok ? (size_t)D4_S * 4 : 0;
+  if ((rc = ensure_work(c, (xbytes + 8 + awbytes + iobytes) * chunk))) return rc;
   const size_t esz = e.dtype == PAI_F32 ? 4 : 8;
   for (long long off = 0; off < N; off += chunk) {
     const long long n = std::min(chunk, N - off);
@@ -2445,7 +2517,21 @@ static int launch_pe(pai_ctx* c, const EncParams& e, hipStream_t st) {
     p.ct_words = c->ct_words;
     p.exp = e.exp + off;
     p.status = e.status ? e.status + off : nullptr;
-    HIPCHK(pe_launch(p, g, st, ev));
+    if (!c->pef_ok) {
+      HIPCHK(pe_launch(p, g, st, ev));
+      continue;
+    }
+    // the factored chain: A_r's batch inversion (one host inversion mod n^2 per chunk), iota, k_pe_pow_f
+    p.aw = (uint32_t*)((char*)c->d_work + (xbytes + 8) * chunk);
+    p.iota = (uint32_t*)((char*)p.aw + awbytes * chunk);
+    HIPCHK(pe_launch_pre_aw(p, g, st, ev));
+    rc = batch_invert(c, p.aw, nullptr, n, st);
+    if (rc == PAI_ERR_NOINV) {   // an A_r shares a factor with n (probability ~2^-1023): the general chain for this chunk
+      HIPCHK(pe_launch_pow_fin(p, g, st, ev));
+      continue;
+    }
+    if (rc) return rc;
+    HIPCHK(pe_launch_iota_pow_f(p, g, st, ev));
   }
   return 0;
 }

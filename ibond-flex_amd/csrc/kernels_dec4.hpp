@@ -319,19 +319,40 @@ __device__ __forceinline__ void d4f_mult_load(const LaneScratch& t, int k, uint3
   d4_fence();
 }
 
-template <int S>
+// The public-key encryption's inputs to the factored chain (k_pe_pow_f, kernels_pe.hpp; PE = true below): the chain
+// runs the exponent n over the B-free base (A_r, 0) -- x^n mod n^2 depends on x mod n only, so the base's B part is
+// dropped outright -- iota = A_r^-1 R^2 mod n comes from a batch inversion instead of a Fermat chain (n's factors are
+// not known), and the closing multiplies by c0 = 1 + n M: the output is (A_Z, B_Z + A_Z (delta + M)) mod n.
+struct PefIn {
+  const uint32_t* iota;    // [S][n] limbs of A_r^-1 R^2 mod n
+  const uint32_t* r2n;     // R^2 mod n, S limbs (t R = REDC(t R^2))
+  const uint32_t* nl;      // n, S limbs
+  long long n, ee;         // elements, this element
+  int64_t M;               // the encoding: c0 = 1 + n M
+};
+
+template <int S, bool PE = false>
 __device__ __forceinline__ void d4f_run(uint32_t (&a)[S], uint32_t* st, uint32_t* kb, const LaneScratch& tl,
                                         const uint32_t* __restrict__ prog, int nprog, const uint32_t* __restrict__ kf,
-                                        const uint32_t* x1, const uint32_t (&m)[S], uint32_t mprime, int tig) {
+                                        const uint32_t* x1, const uint32_t (&m)[S], uint32_t mprime, int tig,
+                                        const PefIn& pe = PefIn{}) {
   constexpr int TQ = tile_quads<S>();
   using Q = std::make_integer_sequence<int, TQ>;
   const bool odd = tig != 0;
+  if constexpr (PE) {   // (A_r, B_r) -> (A_r, 0): the base's B part does not change x^n mod n^2
+#pragma unroll
+    for (int j = 0; j < S; ++j) a[j] = odd ? 0u : a[j];
+  }
   // the table's base (A~, 0), the multiplier A~ kept in the LDS A row by the table's products (LOP_B_READY)
   d4r_tile_store<S>(tl, 0, a, Q{});
   d4_fence();
   if (!odd) {
 #pragma unroll
     for (int j = 0; j < S; ++j) st[j] = a[j];
+    if constexpr (PE) {   // iota into the B row now (the chain's B-free multipliers use only the A row)
+#pragma unroll
+      for (int j = 0; j < S; ++j) st[S + j] = pe.iota[(size_t)j * pe.n + pe.ee];
+    }
   }
 #pragma unroll
   for (int j = 0; j < S; ++j) a[j] = odd ? 0u : a[j];
@@ -431,13 +452,53 @@ __device__ __forceinline__ void d4f_run(uint32_t (&a)[S], uint32_t* st, uint32_t
       d4r_tile_store<S>(tl, D4F_ACC, a, Q{});
     }
   }
-  // output (A, G + delta): G < 2p, delta < 2p
-  {
+  if constexpr (!PE) {   // output (A, G + delta): G < 2p, delta < 2p
     uint32_t g[S];
     d4r_tile_load<S>(tl, D4F_G, g, Q{});
     uint32_t c = 0;
 #pragma unroll
     for (int i = 0; i < S; ++i) {
+      const uint32_t v = g[i] + (odd ? a[i] : 0u) + c;
+      a[i] = v & lane::LMASK;
+      c = v >> lane::LB;
+    }
+  } else {   // (A_Z, B_Z + A_Z t), t = delta + M mod n: u = REDC(t R^2) = t R over R^2's digits (kb), then REDC(u A_Z)
+    {
+      const int64_t M = pe.M;
+      const bool neg = M < 0;
+      const uint64_t mag = neg ? (uint64_t)0 - (uint64_t)M : (uint64_t)M;
+      int64_t c = 0;
+#pragma unroll
+      for (int j = 0; j < S; ++j) {   // a (the odd lane's delta < 2n) + M, or + n - |M|: < 3n
+        const uint32_t mj = j < 3 ? (uint32_t)(mag >> (lane::LB * j)) & lane::LMASK : 0u;
+        const int64_t v = (int64_t)a[j] + (neg ? (int64_t)pe.nl[j] - (int64_t)mj : (int64_t)mj) + c;
+        a[j] = (uint32_t)v & lane::LMASK;
+        c = v >> lane::LB;
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < S; i += blockDim.x) kb[i] = pe.r2n[i];
+    __syncthreads();
+    uint64_t P[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) P[i] = 0;
+    d4_pass<S>(P, a, kb, 0, m, mprime, false, std::make_integer_sequence<int, S>{});
+    lane::normalize<S>(P, a);            // u = t R (< 2n)
+    uint32_t g[S];
+    d4r_tile_load<S>(tl, D4F_G, g, Q{});   // (A_Z, B_Z)
+    d4_fence();
+    if (!odd) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) st[i] = g[i];   // A_Z's digits for the odd lane's last pass
+    }
+    d4_fence();
+#pragma unroll
+    for (int i = 0; i < S; ++i) P[i] = 0;
+    d4_pass<S>(P, a, st, 0, m, mprime, false, std::make_integer_sequence<int, S>{});
+    lane::normalize<S>(P, a);            // t A_Z (< 2n)
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {         // even: A_Z; odd: B_Z + t A_Z (< 4n)
       const uint32_t v = g[i] + (odd ? a[i] : 0u) + c;
       a[i] = v & lane::LMASK;
       c = v >> lane::LB;

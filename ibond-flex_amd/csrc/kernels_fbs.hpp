@@ -444,9 +444,57 @@ __device__ __forceinline__ void fbs_store_limbs(uint4* __restrict__ dst, const u
    ...);
 }
 
-template <int S>
-__global__ __launch_bounds__(LANE_BLOCK) void k_fbs_fill(const FbpHalf* halves, const FbsConst* cst, int K, int W, uint4* table0,
-                                                         uint4* table1, GuardArgs g) {
+// a' = floor(a mu / R) by product scanning (fbs_fill_body): column T of A mu, A: S limbs, mu: S + 1 limbs, one running
+// 64-bit sum (at most S + 1 products < 2^56 per column plus a carry < 2^36); columns S .. 2S are a'. Compile-time
+// columns (a loop over 2S + 1 x S candidate products is too long for the unroller, which then left a branch per MAC).
+template <int S, int T, int I>
+__device__ __forceinline__ void fbs_ap_mac(uint64_t& acc, const uint32_t (&A)[S], const uint32_t* mu) {
+  if constexpr (T - I >= 0 && T - I < S + 1) acc += (uint64_t)A[I] * mu[T - I];
+}
+template <int S, int T, int... Is>
+__device__ __forceinline__ void fbs_ap_column(uint64_t& acc, const uint32_t (&A)[S], const uint32_t* mu,
+                                              std::integer_sequence<int, Is...>) {
+  (fbs_ap_mac<S, T, Is>(acc, A, mu), ...);
+}
+template <int S, int T>
+__device__ __forceinline__ void fbs_ap_step(uint64_t& acc, uint32_t (&ap)[S + 1], const uint32_t (&A)[S], const uint32_t* mu) {
+  fbs_ap_column<S, T>(acc, A, mu, std::make_integer_sequence<int, S>{});
+  if constexpr (T >= S) ap[T - S] = (uint32_t)acc & lane::LMASK;
+  acc >>= lane::LB;
+}
+template <int S, int... Ts>
+__device__ __forceinline__ void fbs_ap_all(uint32_t (&ap)[S + 1], const uint32_t (&A)[S], const uint32_t* mu,
+                                           std::integer_sequence<int, Ts...>) {
+  uint64_t acc = 0;
+  (fbs_ap_step<S, Ts>(acc, ap, A, mu), ...);
+}
+// the low S + 1 limbs of a R - a' p (signed running sum: at most S + 1 products < 2^56 subtracted per column)
+template <int S, int T, int I>
+__device__ __forceinline__ void fbs_apt_mac(int64_t& acc, const uint32_t (&ap)[S + 1], const uint32_t (&m)[S]) {
+  if constexpr (T - I >= 0 && T - I < S) acc -= (int64_t)((uint64_t)ap[I] * m[T - I]);
+}
+template <int S, int T, int... Is>
+__device__ __forceinline__ void fbs_apt_step(int64_t& acc, uint32_t (&tl)[S + 1], const uint32_t (&ap)[S + 1],
+                                             const uint32_t (&A)[S], const uint32_t (&m)[S], std::integer_sequence<int, Is...>) {
+  if constexpr (T == S) acc += (int64_t)A[0];
+  (fbs_apt_mac<S, T, Is>(acc, ap, m), ...);
+  tl[T] = (uint32_t)acc & lane::LMASK;
+  acc >>= lane::LB;
+}
+template <int S, int... Ts>
+__device__ __forceinline__ void fbs_apt_all(uint32_t (&tl)[S + 1], const uint32_t (&ap)[S + 1], const uint32_t (&A)[S],
+                                            const uint32_t (&m)[S], std::integer_sequence<int, Ts...>) {
+  int64_t acc = 0;
+  (fbs_apt_step<S, Ts>(acc, tl, ap, A, m, std::make_integer_sequence<int, S + 1>{}), ...);
+}
+
+// One row per thread. UNI: every thread of the block shares the hi entry (2^(W/2) >= LANE_BLOCK, i.e. W >= 16), whose
+// pair and inverse, with mu and R^2, the block stages once in LDS (sh); otherwise they come from global memory (round 5:
+// a global load per digit of the hi entry, each waited, had made the fill latency-bound at 4.0 ns per row -- 34 ms of a
+// fresh key's 95 ms at W = 16, 1.57 s of the W = 22 build).
+template <int S, bool UNI>
+__device__ __forceinline__ void fbs_fill_body(const FbpHalf* halves, const FbsConst* cst, int W, uint4* table0, uint4* table1,
+                                              const GuardArgs& g, const uint32_t* sh) {
   using G = FbsGeom<S>;
   constexpr int TQ = fbs_row_quads<S>();
   const int ent = 1 << W;
@@ -462,77 +510,29 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_fbs_fill(const FbpHalf* halves, 
   const int dl = (int)FPAI_GUARD_IDX(g, GS_FILL_LOHI, (unsigned)(d & ((1 << LO) - 1)), FB_LO, d),
             dh = (int)FPAI_GUARD_IDX(g, GS_FILL_LOHI, (unsigned)(d >> LO), FB_LO, d);
   const uint32_t* lo = H->lohi + (((size_t)k * 2 + 0) * FB_LO + dl) * 2 * S;
-  const uint32_t* hi = H->lohi + (((size_t)k * 2 + 1) * FB_LO + dh) * 2 * S;
+  const uint32_t* hi = UNI ? sh : H->lohi + (((size_t)k * 2 + 1) * FB_LO + dh) * 2 * S;
+  const uint32_t* ih = UNI ? sh + 2 * S : H->inv + (((size_t)k * 2 + 1) * FB_LO + dh) * S;
+  const uint32_t* mu = UNI ? sh + 3 * S : C->mu;
+  const uint32_t* r2 = UNI ? sh + 4 * S + 2 : C->r2;
   uint32_t m[S], A[S], B[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) {
-    m[i] = H->p[i];
+    m[i] = (uint32_t)__builtin_amdgcn_readfirstlane(H->p[i]);   // uniform: SGPRs, not 37 VGPRs of the pair product's budget
     A[i] = lo[i];
     B[i] = lo[S + i];
   }
   pair::mont_mul<S>(A, B, [&](auto J) { return make_uint2(hi[decltype(J)::value], hi[S + decltype(J)::value]); }, m, H->mprime);
   pair::mont_mul<S>(A, B, [&](auto J) { return make_uint2(decltype(J)::value == 0 ? 1u : 0u, 0u); }, m, H->mprime);   // T R -> T
   pair::canon<S>(A, B, m);
-  uint32_t bR[S];
-  {
-    const uint32_t* il = H->inv + (((size_t)k * 2 + 0) * FB_LO + dl) * S;
-    const uint32_t* ih = H->inv + (((size_t)k * 2 + 1) * FB_LO + dh) * S;
-    uint32_t X[S], Y[S];
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-      X[i] = il[i];
-      Y[i] = ih[i];
-      bR[i] = B[i];
-    }
-    lane::mont_mul<S>(X, Y, m, H->mprime);               // A_T^-1 R
-    lane::mont_mul<S>(bR, X, m, H->mprime);              // b = B_T A_T^-1
-#pragma unroll
-    for (int i = 0; i < S; ++i) Y[i] = C->r2[i];
-    lane::mont_mul<S>(bR, Y, m, H->mprime);              // b R
-    lane::cond_sub<S>(bR, m);
-  }
-  // a' = floor(a R / p): the high part of a mu, then one correction
+  // a' = floor(a R / p): the high part of a mu, then one correction. Product scanning, one running 64-bit column sum
+  // (a column takes at most S + 1 products < 2^56 plus a carry < 2^36: below 2^63), so no 2S-column array is live
+  // (round 5: the row-scanning form kept 2S + 2 64-bit columns and spilled 624 B)
   uint32_t ap[S + 1];
   {
-    uint64_t P[2 * S + 2];
-#pragma unroll
-    for (int c = 0; c < 2 * S + 2; ++c) P[c] = 0;
-#pragma unroll
-    for (int j = 0; j < S + 1; ++j) {
-      const uint32_t mj = C->mu[j];
-#pragma unroll
-      for (int i = 0; i < S; ++i) P[i + j] += (uint64_t)A[i] * mj;
-      if ((j & 7) == 7) {   // keep the columns below 2^63: carry the finished low columns up
-#pragma unroll
-        for (int c = 0; c + 1 < 2 * S + 2; ++c) {
-          P[c + 1] += P[c] >> lane::LB;
-          P[c] &= lane::LMASK;
-        }
-      }
-    }
-    uint64_t c = 0;
-#pragma unroll
-    for (int t = 0; t < 2 * S + 2; ++t) {
-      const uint64_t v = P[t] + c;
-      if (t >= S && t - S < S + 1) ap[t - S] = (uint32_t)v & lane::LMASK;
-      c = v >> lane::LB;
-    }
+    fbs_ap_all<S>(ap, A, mu, std::make_integer_sequence<int, 2 * S + 1>{});
     // t = a R - a' p over the low S + 1 limbs (exact: 0 <= t < 2 p); a' += 1 when t >= p
-    int64_t T[S + 1];
-#pragma unroll
-    for (int t2 = 0; t2 < S + 1; ++t2) T[t2] = t2 == S ? (int64_t)A[0] : 0;
-#pragma unroll
-    for (int j = 0; j < S; ++j)
-#pragma unroll
-      for (int i = 0; i + j < S + 1; ++i) T[i + j] -= (int64_t)((uint64_t)ap[i] * m[j]);
     uint32_t tl[S + 1];
-    int64_t cc = 0;
-#pragma unroll
-    for (int t2 = 0; t2 < S + 1; ++t2) {
-      const int64_t v = T[t2] + cc;
-      tl[t2] = (uint32_t)v & lane::LMASK;
-      cc = v >> lane::LB;
-    }
+    fbs_apt_all<S>(tl, ap, A, m, std::make_integer_sequence<int, S + 1>{});
     // t >= p ?
     int32_t bw = 0;
 #pragma unroll
@@ -551,7 +551,47 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_fbs_fill(const FbpHalf* halves, 
   uint4* dst = table + FPAI_GUARD_IDX(g, GS_FILL_ROW, (size_t)k * ent + d, g.rows, d) * TQ;
   fbs_store_limbs<S>(dst, A, std::make_integer_sequence<int, G::QA>{});
   fbs_store_limbs<S>(dst + G::QA, ap, std::make_integer_sequence<int, G::QAP>{});   // a' < R: limb S is zero
+  // b = B_T A_T^-1, b R: after a and a' are stored (their registers free again)
+  uint32_t bR[S];
+  {
+    const uint32_t* il = H->inv + (((size_t)k * 2 + 0) * FB_LO + dl) * S;
+    uint32_t X[S], Y[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      X[i] = il[i];
+      Y[i] = ih[i];
+      bR[i] = B[i];
+    }
+    lane::mont_mul<S>(X, Y, m, H->mprime);               // A_T^-1 R
+    lane::mont_mul<S>(bR, X, m, H->mprime);              // b = B_T A_T^-1
+#pragma unroll
+    for (int i = 0; i < S; ++i) Y[i] = r2[i];
+    lane::mont_mul<S>(bR, Y, m, H->mprime);              // b R
+    lane::cond_sub<S>(bR, m);
+  }
   fbs_store_words<S>(dst + G::QA + G::QAP, bR, std::make_integer_sequence<int, G::QB>{});
+}
+
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbs_fill(const FbpHalf* halves, const FbsConst* cst, int K, int W, uint4* table0,
+                                                         uint4* table1, GuardArgs g) {
+  __shared__ uint32_t sh[5 * S + 2];   // hi pair [2S], its inverse [S], mu [S + 2], R^2 mod p [S]
+  (void)K;
+  const int LO = W / 2;
+  if ((1 << LO) >= LANE_BLOCK) {   // block-uniform (W is a kernel argument)
+    const int per = (1 << W) / LANE_BLOCK, k = blockIdx.x / per;
+    const int dh = (int)FPAI_GUARD_IDX(g, GS_FILL_LOHI, (unsigned)(((blockIdx.x % per) * LANE_BLOCK) >> LO), FB_LO, k);
+    const FbpHalf* H = halves + blockIdx.y;
+    const FbsConst* C = cst + blockIdx.y;
+    const uint32_t* hi = H->lohi + (((size_t)k * 2 + 1) * FB_LO + dh) * 2 * S;
+    const uint32_t* ih = H->inv + (((size_t)k * 2 + 1) * FB_LO + dh) * S;
+    for (int i = threadIdx.x; i < 5 * S + 2; i += LANE_BLOCK)
+      sh[i] = i < 2 * S ? hi[i] : i < 3 * S ? ih[i - 2 * S] : i < 4 * S + 2 ? C->mu[i - 3 * S] : C->r2[i - 4 * S - 2];
+    __syncthreads();
+    fbs_fill_body<S, true>(halves, cst, W, table0, table1, g, sh);
+  } else {
+    fbs_fill_body<S, false>(halves, cst, W, table0, table1, g, nullptr);
+  }
 }
 
 }  // namespace fpai

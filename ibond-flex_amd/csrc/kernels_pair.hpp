@@ -316,8 +316,11 @@ __device__ __forceinline__ void decf_run(uint32_t (&A)[S], uint32_t (&B)[S], con
       ptile_load_b<S, S / 4>(t, j, B, std::make_integer_sequence<int, TQ - S / 4>{});
 #pragma unroll
       for (int i = 0; i < S; ++i) P[i] = 0;
+      uint32_t kd[S];   // K'_j: all S words requested at once (a load per digit would expose S memory latencies)
       const uint32_t* kj = kf + (size_t)j * S;
-      pair::redc_row<S>(P, B, [&](auto J) { return kj[decltype(J)::value]; }, m, mprime);   // c_j
+#pragma unroll
+      for (int i = 0; i < S; ++i) kd[i] = kj[i];
+      pair::redc_row<S>(P, B, [&](auto J) { return kd[decltype(J)::value]; }, m, mprime);   // c_j
     }
 #pragma unroll
     for (int i = 0; i < S; ++i) P[i] = B[i];

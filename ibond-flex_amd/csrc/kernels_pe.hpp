@@ -10,6 +10,17 @@
 //   k_pe_pow   (r R)^n by the lane machine's op list for the exponent n, the final product with the pair of
 //              c0 = 1 + n M, i.e. (1, M mod n): the plain pair of c
 //   k_pe_fin   the canonical pair -> c = A + n B (< n^2) -> ciphertext words
+//
+// Round 5, the factored chain (kernels_dec4.hpp d4f_run<S, true>): x^n mod n^2 depends on x mod n
+// only, so the base is the B-free (A_r, 0) and the window table its 30 one-pass mm-powers; the chain over n multiplies
+// by the entries' A parts (a_t, 0) only (one pass instead of two) and the dropped factors (1 + n b_t), b_t = H_t / a_t,
+// are restored at the end by the closing Horner sum in iota = A_r^-1 R^2 mod n. There is no Fermat chain for that
+// inverse (n's factors are secret), so it comes from ONE batch inversion per chunk (Montgomery's trick on the group
+// engine, kernels_mul.hpp k_inv_up/down, one host inversion mod n^2):
+//   k_pe_awords  A_r (the pair's A limbs) -> words [n][W] for the batch inversion
+//   k_pe_iota    iota = A component of pair(R^4) x (A_r^-1 mod n^2) R^-2 -- k_pe_pre's long CIOS over the inverse's digits
+//   k_pe_pow_f   the factored chain, then (A_Z, B_Z + A_Z (delta + M)): the plain pair of c, as k_pe_pow's
+// A chunk whose A_r has no inverse (probability ~2^-1023) takes k_pe_pow instead (flexpai.hip launch_pe).
 #pragma once
 #include "kernels_dec4.hpp"
 
@@ -23,6 +34,12 @@ struct PeConst {
   const uint32_t* prog;    // op list for the exponent n
   int nprog;
   uint32_t mprime;         // -n^-1 mod 2^28
+  // the factored chain (k_pe_pow_f)
+  const uint32_t* progf;   // op list: the table of (A_r, 0), the chain over n with B-free multipliers, (1, 0) -> D4F_G
+  int nprogf;
+  const uint32_t* kf;      // [16][S] K'_t of the closing Horner sum
+  const uint32_t* r2n;     // R^2 mod n
+  const uint32_t* cK4;     // pair of R^4 mod n^2 (k_pe_iota)
 };
 
 struct PeParams {
@@ -37,6 +54,8 @@ struct PeParams {
   long long n;
   uint32_t* xw;            // [2S][n] pairs
   int64_t* M;              // [n] encodings (k_pe_pre -> k_pe_pow)
+  uint32_t* aw;            // [n][ct_words] A_r as words, then its inverse mod n^2 (k_pe_awords -> batch inversion -> k_pe_iota)
+  uint32_t* iota;          // [S][n] A_r^-1 R^2 mod n (k_pe_iota -> k_pe_pow_f)
   uint32_t* scratch;
   uint32_t* ct;
   int ct_words;
@@ -164,6 +183,106 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_pe_pow(PeParams p) {
         }
       }
     });
+    if (valid) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) p.xw[((size_t)tig * S + i) * p.n + e] = a[i];
+    }
+  }
+}
+
+// A_r -> words [n][ct_words] (the value < 2n zero-extended) for the batch inversion mod n^2
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK) void k_pe_awords(PeParams p) {
+  for (long long i = (long long)blockIdx.x * LANE_BLOCK + threadIdx.x; i < p.n; i += (long long)gridDim.x * LANE_BLOCK) {
+    uint32_t a[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) a[j] = p.xw[(size_t)j * p.n + i];
+    uint32_t* w = p.aw + (size_t)i * p.ct_words;
+#pragma unroll
+    for (int k = 0; k < (S * lane::LB + 31) / 32; ++k) {
+      const int bit = 32 * k, j = bit / lane::LB, sh = bit - j * lane::LB;
+      uint64_t v = (uint64_t)a[j] >> sh;
+      if (j + 1 < S) v |= (uint64_t)a[j + 1] << (lane::LB - sh);
+      if (j + 2 < S && 2 * lane::LB - sh < 32) v |= (uint64_t)a[j + 2] << (2 * lane::LB - sh);
+      w[k] = (uint32_t)v;
+    }
+    for (int k = (S * lane::LB + 31) / 32; k < p.ct_words; ++k) w[k] = 0u;
+  }
+}
+
+// iota = A component of (pair of R^4) x inv R^-2 = inv R^2 mod n, inv = A_r^-1 mod n^2 from p.aw: k_pe_pre's long
+// split CIOS over the inverse's 2S digits (staged in LDS), the even lane's row
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK, 1) void k_pe_iota(PeParams p) {
+  __shared__ uint32_t lds[D4_PAIRS * D4_SLOT];
+  const PeConst* K = p.k;
+  uint32_t m[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) m[j] = K->nl[j];
+  const uint32_t mprime = K->mprime;
+  const int tig = threadIdx.x & 1;
+  const bool odd = tig != 0;
+  const int pib = threadIdx.x >> 1;
+  uint32_t* sx = lds + pib * D4_SLOT;
+  for (long long base = (long long)blockIdx.x * D4_PAIRS; base < p.n; base += (long long)gridDim.x * D4_PAIRS) {
+    const long long e = base + pib;
+    const bool valid = e < p.n;
+    const long long ee = valid ? e : p.n - 1;
+    uint32_t* wbuf = sx + 2 * S;
+    const int nw = p.ct_words;
+    d4_fence();
+    for (int w = tig; w < nw; w += 2) wbuf[w] = p.aw[(size_t)ee * nw + w];
+    d4_fence();
+    for (int k = tig * S; k < (tig + 1) * S; ++k) {
+      const int bit = k * lane::LB, wi = bit >> 5, sh = bit & 31;
+      const uint64_t lo = wi < nw ? (uint64_t)wbuf[wi] : 0ull;
+      const uint64_t hi = wi + 1 < nw ? (uint64_t)wbuf[wi + 1] : 0ull;
+      sx[k] = (uint32_t)(((hi << 32) | lo) >> sh) & lane::LMASK;
+    }
+    d4_fence();
+    uint32_t a[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) a[i] = K->cK4[tig * S + i];
+    uint64_t P[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) P[i] = 0;
+#pragma unroll 1
+    for (int k = 0; k < 2; ++k) d4_pass<S>(P, a, sx + k * S, 0, m, mprime, odd, std::make_integer_sequence<int, S>{});
+    uint32_t y[S];
+    lane::normalize<S>(P, y);
+    if (valid && !odd) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) p.iota[(size_t)i * p.n + e] = y[i];
+    }
+  }
+}
+
+// the factored chain (d4f_run<S, true>): the plain pair of c = c0 r^n, as k_pe_pow
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK, 2) void k_pe_pow_f(PeParams p) {
+  __shared__ uint32_t lds[D4_PAIRS * D4R_SLOT + 2 * S];
+  const PeConst* K = p.k;
+  uint32_t m[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) m[j] = K->nl[j];
+  const uint32_t mprime = K->mprime;
+  uint32_t* x1 = lds + D4_PAIRS * D4R_SLOT;   // (1 - R) mod n: the odd row's start in squares
+  uint32_t* kb = x1 + S;                       // K'_t of the current Horner step, then R^2 mod n (block-wide)
+  for (int i = threadIdx.x; i < S; i += blockDim.x) x1[i] = K->X1[i];
+  __syncthreads();
+  const int tig = threadIdx.x & 1;
+  const int pib = threadIdx.x >> 1;
+  uint32_t* st = lds + pib * D4R_SLOT;
+  const LaneScratch tl = lane_scratch(p.scratch);
+  for (long long base = (long long)blockIdx.x * D4_PAIRS; base < p.n; base += (long long)gridDim.x * D4_PAIRS) {
+    const long long e = base + pib;
+    const bool valid = e < p.n;
+    const long long ee = valid ? e : p.n - 1;
+    uint32_t a[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) a[i] = p.xw[((size_t)tig * S + i) * p.n + ee];
+    const PefIn pe{p.iota, K->r2n, K->nl, p.n, ee, p.M[ee]};
+    d4f_run<S, true>(a, st, kb, tl, opaque_uniform(K->progf), K->nprogf, opaque_uniform(K->kf), x1, m, mprime, tig, pe);
     if (valid) {
 #pragma unroll
       for (int i = 0; i < S; ++i) p.xw[((size_t)tig * S + i) * p.n + e] = a[i];

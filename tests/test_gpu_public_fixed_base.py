@@ -170,3 +170,20 @@ def test_split_sampler_matches_group_engine(pub, golden_pfb, monkeypatch, xlib):
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
     val, _, st, _ = dec.decrypt(outs[0][0], outs[0][1])
     assert np.array_equal(np.asarray(val, dtype=np.float64), x.astype(np.float64))
+
+
+def test_public_break_even_follows_the_measured_model(golden, monkeypatch):
+    """pai_ctx_public_fb_policy's threshold is the measured round-5 model (tools/pfb_breakeven.py): build 0.114 s +
+    1.91 ns per row, saving 1/503 k - 1/rate(W) s per element (rate 4.00 M enc/s at the default W = 16)."""
+    N = _native()
+    monkeypatch.delenv("FLEXPAI_PFB_MIN_ELEMS", raising=False)
+    k = golden["keys"]["2048"]
+    ctx = N.Context(int(k["n"], 16), 0)
+    try:
+        _, thr = ctx.public_fixed_base_policy()
+        K0, KS = O.pfb_layout(2048, 16)
+        rows = (K0 + O.PFB_SHORT * KS) << 16
+        want = int((0.114 + rows * 1.91e-9) / (1 / 5.03e5 - 1 / 4.00e6)) + 1
+        assert abs(thr - want) <= 1 and 80_000 < thr < 100_000
+    finally:
+        ctx.close()

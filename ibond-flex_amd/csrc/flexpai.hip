@@ -2481,6 +2481,14 @@ int pai_ctx_public_fb_policy(pai_ctx* c, long long* seen, long long* threshold) 
 // public-key encryption on split pairs (kernels_pe.hpp, engine_pe.hip), in chunks of CRT_CHUNK elements
 static int batch_invert(pai_ctx* c, uint32_t* x, const uint8_t* flag, long long n, hipStream_t st);
 
+// Chunks below this many elements take the general chain: the factored one saves ~0.2 us per element (k_pe_pow_f
+// against k_pe_pow) and costs the batch inversion's fixed ~1-2 ms of short dependent launches. $FLEXPAI_PEF_MIN
+// overrides (the parity tests force both chains on the same inputs).
+static long long pef_min_elems() {
+  if (const char* e = getenv("FLEXPAI_PEF_MIN")) return atoll(e);
+  return 16384;
+}
+
 static int launch_pe(pai_ctx* c, const EncParams& e, hipStream_t st) {
   const long long N = e.n;
   const long long chunk = std::min(N, CRT_CHUNK);
@@ -2517,7 +2525,7 @@ static int launch_pe(pai_ctx* c, const EncParams& e, hipStream_t st) {
     p.ct_words = c->ct_words;
     p.exp = e.exp + off;
     p.status = e.status ? e.status + off : nullptr;
-    if (!c->pef_ok) {
+    if (!c->pef_ok || n < pef_min_elems()) {
       HIPCHK(pe_launch(p, g, st, ev));
       continue;
     }
@@ -2965,9 +2973,15 @@ static int inv_grid(pai_ctx* c, long long nseg) {
 // host step synchronises `st` once. Not invertible -> PAI_ERR_NOINV ("no inverse exists").
 static int batch_invert(pai_ctx* c, uint32_t* x, const uint8_t* flag, long long n, hipStream_t st) {
   const int S = c->S_e, W = c->ct_words;
+  // segment length per level: INV_SEG where there are values enough to fill the chip with segments, down to 4 on the
+  // upper levels, whose few groups would otherwise walk chains of 64 dependent products (round 5: the 1M-value
+  // inversion's levels above the first took ~22 of its 37 ms as 64-long chains over 16 k, 256 and 4 values)
   std::vector<long long> ns{n};
-  do ns.push_back((ns.back() + INV_SEG - 1) / INV_SEG);
-  while (ns.back() > 1);
+  std::vector<int> seg;
+  do {
+    seg.push_back((int)std::max<long long>(4, std::min<long long>(INV_SEG, ns.back() / 4096)));
+    ns.push_back((ns.back() + seg.back() - 1) / seg.back());
+  } while (ns.back() > 1);
   const int levels = (int)ns.size() - 1;
   std::vector<size_t> pre_off(levels), seg_off(levels);
   size_t off = 0;
@@ -2992,6 +3006,7 @@ static int batch_invert(pai_ctx* c, uint32_t* x, const uint8_t* flag, long long 
     p.oneR = c->d_oneR;
     p.mprime = c->mprime_N;
     p.ct_words = W;
+    p.seg_len = seg[l];
     return p;
   };
   for (int l = 0; l < levels; ++l) HIPCHK(inv_launch(c->tpi_e, true, params(l), inv_grid(c, ns[l + 1]), st));

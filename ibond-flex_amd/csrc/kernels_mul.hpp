@@ -7,7 +7,7 @@
 //                   out = c^|M| mod n^2, exponent e_c + e_s, flag = (M < 0). The reference computes
 //                   invert(c)^|M| for M < 0 (:100-106); that equals invert(c^|M|), so the flagged terms
 //                   are finished by ONE batch inversion (k_inv_*) instead of one inversion each.
-//   k_inv_up<TPI>   Montgomery's batch inversion, up-sweep: prefix products over segments of INV_SEG
+//   k_inv_up<TPI>   Montgomery's batch inversion, up-sweep: prefix products over segments of p.seg_len values
 //   k_inv_down<TPI> down-sweep: x_j^-1 = (x_0 .. x_j)^-1 (x_0 .. x_(j-1)), written in place
 //
 // Lane-group engine (bn_group.hpp), one element per group of TPI lanes, like k_add. A matrix product
@@ -17,7 +17,7 @@
 
 namespace fpai {
 
-constexpr int INV_SEG = 64;   // values per segment of the batch inversion
+constexpr int INV_SEG = 64;   // values per segment of the batch inversion's first level (flexpai.hip batch_invert)
 
 struct MulParams {
   const uint32_t* ct;     // ciphertext words [*][W]
@@ -236,12 +236,13 @@ struct InvParams {
   const uint8_t* flag;    // [n] (nullable: all flagged)
   long long n;
   uint32_t* pre;          // [n][S] Montgomery prefix products (limbs, group layout)
-  uint32_t* seg;          // [ceil(n / INV_SEG)][W]: up: segment products; down: their inverses
+  uint32_t* seg;          // [ceil(n / seg_len)][W]: up: segment products; down: their inverses
   const uint32_t* N;
   const uint32_t* R2;
   const uint32_t* oneR;
   uint32_t mprime;
   int ct_words;
+  int seg_len;            // values per segment at this level (<= INV_SEG)
 };
 
 // x~ = (flagged ? x : 1) R mod n^2
@@ -266,13 +267,13 @@ __global__ __launch_bounds__(BLOCK, 2) void k_inv_up(InvParams p) {
   uint32_t* slot = smem + gib * S;
   uint32_t m[L];
   load_limbs_g<TPI>(p.N, m, tig);
-  const long long nseg = (p.n + INV_SEG - 1) / INV_SEG;
+  const long long nseg = (p.n + p.seg_len - 1) / p.seg_len;
   for (long long base = (long long)blockIdx.x * GPB; base < nseg; base += (long long)gridDim.x * GPB) {
     const long long sg = base + gib;
     const bool valid = sg < nseg;
     const long long sv = valid ? sg : nseg - 1;
-    const long long s0 = sv * INV_SEG;
-    const int cnt = (int)min((long long)INV_SEG, p.n - s0);
+    const long long s0 = sv * p.seg_len;
+    const int cnt = (int)min((long long)p.seg_len, p.n - s0);
     int wcnt = cnt;
 #pragma unroll
     for (int s = 32; s >= 1; s >>= 1) wcnt = max(wcnt, __shfl_xor(wcnt, s));
@@ -304,13 +305,13 @@ __global__ __launch_bounds__(BLOCK, 2) void k_inv_down(InvParams p) {
   uint32_t* slot = smem + gib * S;
   uint32_t m[L];
   load_limbs_g<TPI>(p.N, m, tig);
-  const long long nseg = (p.n + INV_SEG - 1) / INV_SEG;
+  const long long nseg = (p.n + p.seg_len - 1) / p.seg_len;
   for (long long base = (long long)blockIdx.x * GPB; base < nseg; base += (long long)gridDim.x * GPB) {
     const long long sg = base + gib;
     const bool valid = sg < nseg;
     const long long sv = valid ? sg : nseg - 1;
-    const long long s0 = sv * INV_SEG;
-    const int cnt = (int)min((long long)INV_SEG, p.n - s0);
+    const long long s0 = sv * p.seg_len;
+    const int cnt = (int)min((long long)p.seg_len, p.n - s0);
     int wcnt = cnt;
 #pragma unroll
     for (int s = 32; s >= 1; s >>= 1) wcnt = max(wcnt, __shfl_xor(wcnt, s));

@@ -1,7 +1,12 @@
 """GPU parity of the public-key encryption on split pairs (kernels_pe.hpp: k_pe_pre / k_pe_pow / k_pe_fin, the
 path of every party that holds only the public key, 2048-bit n) against the reference golden vectors
 (explicit r: encryptor.py:48-69 with random_value), the CPU oracle (device ChaCha20 obfuscators) and the
-group-engine kernel it replaces (k_encrypt, $FLEXPAI_PAIR=0 in the test build): bit-identical ciphertexts, exponents, statuses."""
+group-engine kernel it replaces (k_encrypt, $FLEXPAI_PAIR=0 in the test build): bit-identical ciphertexts, exponents, statuses.
+
+Every case runs twice: on the general chain (k_pe_pow) and on the factored one (k_pe_pow_f: B-free multipliers, a batch
+inversion of the bases, the closing Horner sum; round 5), the latter forced at small sizes by $FLEXPAI_PEF_MIN=0. The
+edge obfuscators include non-units (r = 0, n, 5p): the batch inversion then finds no inverse and the chunk falls back
+to the general chain -- same ciphertexts."""
 import numpy as np
 import pytest
 
@@ -21,6 +26,12 @@ def key2048(golden):
     return O.Key(int(k["n"], 16), int(k["p"], 16), int(k["q"], 16))
 
 
+@pytest.fixture(params=["general", "factored"])
+def chain(request, monkeypatch):
+    monkeypatch.setenv("FLEXPAI_PEF_MIN", "0" if request.param == "factored" else str(1 << 40))
+    return request.param
+
+
 def _pub(monkeypatch, key, pair):
     from flex.crypto.paillier import _native as N
     monkeypatch.setenv("FLEXPAI_PAIR", "1" if pair else "0")
@@ -29,7 +40,7 @@ def _pub(monkeypatch, key, pair):
     return ctx
 
 
-def test_pe_given_r_matches_reference_goldens(golden, key2048, monkeypatch):
+def test_pe_given_r_matches_reference_goldens(golden, key2048, monkeypatch, chain):
     N = _native()
     ctx = _pub(monkeypatch, key2048, True)
     recs = golden["encrypt"]["2048"]
@@ -43,7 +54,7 @@ def test_pe_given_r_matches_reference_goldens(golden, key2048, monkeypatch):
 
 
 @pytest.mark.parametrize("n", [1, 127, 129, 300])
-def test_pe_matches_k_encrypt_and_oracle(key2048, monkeypatch, n):
+def test_pe_matches_k_encrypt_and_oracle(key2048, monkeypatch, n, chain):
     N = _native()
     a = _pub(monkeypatch, key2048, True)
     b = _pub(monkeypatch, key2048, False)
@@ -62,7 +73,7 @@ def test_pe_matches_k_encrypt_and_oracle(key2048, monkeypatch, n):
         assert (got[i], int(ea[i])) == (c, e), f"element {i}"
 
 
-def test_pe_edge_obfuscators(key2048, monkeypatch):
+def test_pe_edge_obfuscators(key2048, monkeypatch, chain):
     """r = 0, 1, n - 1, n, n + 1, a multiple of p, r >= n^2 (explicit, like random_value)."""
     N = _native()
     a = _pub(monkeypatch, key2048, True)
@@ -76,3 +87,29 @@ def test_pe_edge_obfuscators(key2048, monkeypatch):
     got = N.words_to_ints(ca)
     for i, r in enumerate(rs):
         assert got[i] == O.encrypt_value(x[i], k, r)[0], f"r #{i}"
+
+
+def test_pe_factored_chain_above_threshold_matches_general(key2048, monkeypatch):
+    """At the default threshold a 20 000-element call runs the factored chain; the test build's general chain
+    ($FLEXPAI_PEF=0) on the same device RNG gives the same ciphertexts, and both decrypt to the input."""
+    N = _native()
+    monkeypatch.delenv("FLEXPAI_PEF_MIN", raising=False)
+    a = _pub(monkeypatch, key2048, True)
+    monkeypatch.setenv("FLEXPAI_PEF", "0")
+    b = N.Context(key2048.n, 0, lib=N.load_library(N.XCHECK_LIB_PATH))
+    monkeypatch.delenv("FLEXPAI_PEF")
+    a.set_public_fixed_base(False)
+    b.set_public_fixed_base(False)
+    n = 20000
+    x = (np.random.default_rng(5).standard_normal(n) * 1000).astype(np.float32)
+    kw = dict(obf_mode=N.PAI_OBF_RNG, rng_key=bytes(range(3, 35)), index_base=2 ** 34)
+    ca, ea, _ = a.encrypt(x, **kw)
+    cb, eb, _ = b.encrypt(x, **kw)
+    assert np.array_equal(ca, cb) and np.array_equal(ea, eb)
+    got = N.words_to_ints(ca[[0, n // 2, n - 1]])
+    rb = ((2048 + 64 + 31) // 32) * 4
+    for j, i in enumerate([0, n // 2, n - 1]):
+        assert got[j] == O.encrypt_value(x[i], key2048, O.device_r(bytes(range(3, 35)), 2 ** 34 + i, rb))[0]
+    d = N.Context(key2048.n, 0, key2048.p, key2048.q)
+    val, _, _, _ = d.decrypt(ca, ea)
+    assert np.array_equal(val, x.astype(np.float64))

@@ -114,6 +114,8 @@ struct pai_ctx {
   bool pe_ok = false;
   bool pef_ok = false;          // the factored public-key chain (k_pe_pow_f) is set up ($FLEXPAI_PEF=0, test build: off)
   PeConst* d_pe = nullptr;
+  uint32_t *d_pe_n = nullptr, *d_pe_r2 = nullptr, *d_pe_oneR = nullptr;   // n, R^2, R mod n (R = 2^(28 74)): the batch
+  uint32_t pe_mprime = 0;                                                 //   inversion of the bases mod n (TPI = 2)
   CrtHalf* d_dec_pow = nullptr;   // [2] exponentiation halves: p_h^2, op list for p_h - 1
   uint32_t *d_dec_p = nullptr, *d_dec_q = nullptr, *d_dec_qinvR = nullptr, *d_dec_nl = nullptr, *d_dec_maxint = nullptr;
   uint32_t dec_pprime = 0;
@@ -863,23 +865,24 @@ static int setup_pe(pai_ctx* c, const HBig& n) {
       (rc = upload(c, ck, &dck)) || (rc = upload(c, prog, &dprog)))
     return rc;
   std::vector<PeConst> pc{PeConst{dn, dx1, dxk, dck, dprog, (int)prog.size(), mont_prime(n, LB)}};
-  // the factored chain (kernels_pe.hpp k_pe_pow_f): its program and Horner weights, R^2 mod n, the pair of R^4 mod n^2
+  // the factored chain (kernels_pe.hpp k_pe_pow_f): its program and Horner weights, R^2 mod n; R mod n for the batch
+  // inversion of the bases mod n on the TPI = 2 group engine (same radix R = 2^(28 74))
   std::vector<uint32_t> progf, kf;
   const bool pef = !(xcheck_env("FLEXPAI_PEF") && atoi(xcheck_env("FLEXPAI_PEF")) == 0);
-  if (pef && build_pef_program(n, RS, progf, kf)) {
-    const HBig r4 = mul_pow2_mod(HBig(1), 4 * RS, n2);
-    const HBig q4 = div_big(r4, n), m4 = sub(r4, mul(q4, n));
-    std::vector<uint32_t> ck4 = m4.limbs(D4_S, LB), b4 = q4.limbs(D4_S, LB);
-    ck4.insert(ck4.end(), b4.begin(), b4.end());
-    uint32_t *dpf, *dkf, *dr2, *dck4;
+  if (pef && tpi_for_bits((size_t)c->nb + 3, 1) == 2 && build_pef_program(n, RS, progf, kf)) {
+    uint32_t *dpf, *dkf, *dr2, *done;
     if ((rc = upload(c, progf, &dpf)) || (rc = upload(c, kf, &dkf)) ||
-        (rc = upload(c, mul_pow2_mod(HBig(1), 2 * RS, n).limbs(D4_S, LB), &dr2)) || (rc = upload(c, ck4, &dck4)))
+        (rc = upload(c, mul_pow2_mod(HBig(1), 2 * RS, n).limbs(D4_S, LB), &dr2)) ||
+        (rc = upload(c, mul_pow2_mod(HBig(1), RS, n).limbs(D4_S, LB), &done)))
       return rc;
     pc[0].progf = dpf;
     pc[0].nprogf = (int)progf.size();
     pc[0].kf = dkf;
     pc[0].r2n = dr2;
-    pc[0].cK4 = dck4;
+    c->d_pe_n = dn;
+    c->d_pe_r2 = dr2;
+    c->d_pe_oneR = done;
+    c->pe_mprime = mont_prime(n, LB);
     c->pef_ok = true;
   }
   if ((rc = upload(c, pc, &c->d_pe))) return rc;
@@ -2479,6 +2482,15 @@ int pai_ctx_public_fb_policy(pai_ctx* c, long long* seen, long long* threshold) 
 }
 
 // public-key encryption on split pairs (kernels_pe.hpp, engine_pe.hip), in chunks of CRT_CHUNK elements
+// the modulus of a batch inversion on the group engine: n^2 (ciphertexts, TPI = tpi_e) or n (the public-key chain's
+// bases, TPI = 2)
+struct InvMod {
+  int tpi, W, S;             // group size, words per value, limbs (TPI L)
+  const uint32_t *N, *R2, *oneR;
+  uint32_t mprime;
+  const HBig* mod;
+};
+static int batch_invert(pai_ctx* c, uint32_t* x, const uint8_t* flag, long long n, hipStream_t st, const InvMod& md);
 static int batch_invert(pai_ctx* c, uint32_t* x, const uint8_t* flag, long long n, hipStream_t st);
 
 // Chunks below this many elements take the general chain: the factored one saves ~0.2 us per element (k_pe_pow_f
@@ -2497,7 +2509,7 @@ static int launch_pe(pai_ctx* c, const EncParams& e, hipStream_t st) {
   int rc = ensure_scratch(c, g.scratch_bytes);
   if (rc) return rc;
   const size_t xbytes = (size_t)2 * D4_S * 4;   // per element, + 8 for M
-  const size_t awbytes = c->pef_ok ? (size_t)c->ct_words * 4 : 0, iobytes = c->pef_ok ? (size_t)D4_S * 4 : 0;
+  const size_t awbytes = c->pef_ok ? (size_t)c->pt_words * 4 : 0, iobytes = c->pef_ok ? (size_t)D4_S * 4 : 0;
   if ((rc = ensure_work(c, (xbytes + 8 + awbytes + iobytes) * chunk))) return rc;
   const size_t esz = e.dtype == PAI_F32 ? 4 : 8;
   for (long long off = 0; off < N; off += chunk) {
@@ -2529,11 +2541,13 @@ static int launch_pe(pai_ctx* c, const EncParams& e, hipStream_t st) {
       HIPCHK(pe_launch(p, g, st, ev));
       continue;
     }
-    // the factored chain: A_r's batch inversion (one host inversion mod n^2 per chunk), iota, k_pe_pow_f
+    // the factored chain: A_r's batch inversion mod n (one host inversion per chunk), iota, k_pe_pow_f
     p.aw = (uint32_t*)((char*)c->d_work + (xbytes + 8) * chunk);
+    p.aw_words = c->pt_words;
     p.iota = (uint32_t*)((char*)p.aw + awbytes * chunk);
     HIPCHK(pe_launch_pre_aw(p, g, st, ev));
-    rc = batch_invert(c, p.aw, nullptr, n, st);
+    rc = batch_invert(c, p.aw, nullptr, n, st,
+                      InvMod{2, c->pt_words, 2 * L, c->d_pe_n, c->d_pe_r2, c->d_pe_oneR, c->pe_mprime, &c->n});
     if (rc == PAI_ERR_NOINV) {   // an A_r shares a factor with n (probability ~2^-1023): the general chain for this chunk
       HIPCHK(pe_launch_pow_fin(p, g, st, ev));
       continue;
@@ -2960,10 +2974,10 @@ struct DevScope {
 
 // ------------------------------------------------------------------ ciphertext x plaintext
 
-static int inv_grid(pai_ctx* c, long long nseg) {
+static int inv_grid(pai_ctx* c, int tpi, long long nseg) {
   int occ = 1;
-  if (mul_occupancy(c->tpi_e, &occ)) occ = 1;
-  const int gpb = BLOCK / c->tpi_e;
+  if (mul_occupancy(tpi, &occ)) occ = 1;
+  const int gpb = BLOCK / tpi;
   return (int)std::max<long long>(1, std::min<long long>((nseg + gpb - 1) / gpb, (long long)occ * c->cus));
 }
 
@@ -2972,7 +2986,10 @@ static int inv_grid(pai_ctx* c, long long nseg) {
 // modular inversion mod n^2; gmpy_math.invert, gmpy_math.py:66-74), and expanded back down. The
 // host step synchronises `st` once. Not invertible -> PAI_ERR_NOINV ("no inverse exists").
 static int batch_invert(pai_ctx* c, uint32_t* x, const uint8_t* flag, long long n, hipStream_t st) {
-  const int S = c->S_e, W = c->ct_words;
+  return batch_invert(c, x, flag, n, st, InvMod{c->tpi_e, c->ct_words, c->S_e, c->d_N, c->d_R2, c->d_oneR, c->mprime_N, &c->N});
+}
+static int batch_invert(pai_ctx* c, uint32_t* x, const uint8_t* flag, long long n, hipStream_t st, const InvMod& md) {
+  const int S = md.S, W = md.W;
   // segment length per level: INV_SEG where there are values enough to fill the chip with segments, down to 4 on the
   // upper levels, whose few groups would otherwise walk chains of 64 dependent products (round 5: the 1M-value
   // inversion's levels above the first took ~22 of its 37 ms as 64-long chains over 16 k, 256 and 4 values)
@@ -3001,15 +3018,15 @@ static int batch_invert(pai_ctx* c, uint32_t* x, const uint8_t* flag, long long 
     p.n = ns[l];
     p.pre = (uint32_t*)(base + pre_off[l]);
     p.seg = (uint32_t*)(base + seg_off[l]);
-    p.N = c->d_N;
-    p.R2 = c->d_R2;
-    p.oneR = c->d_oneR;
-    p.mprime = c->mprime_N;
+    p.N = md.N;
+    p.R2 = md.R2;
+    p.oneR = md.oneR;
+    p.mprime = md.mprime;
     p.ct_words = W;
     p.seg_len = seg[l];
     return p;
   };
-  for (int l = 0; l < levels; ++l) HIPCHK(inv_launch(c->tpi_e, true, params(l), inv_grid(c, ns[l + 1]), st));
+  for (int l = 0; l < levels; ++l) HIPCHK(inv_launch(md.tpi, true, params(l), inv_grid(c, md.tpi, ns[l + 1]), st));
   uint32_t* top = (uint32_t*)(base + seg_off[levels - 1]);
   c->inv_host.assign(W, 0);
   HIPCHK(hipMemcpyAsync(c->inv_host.data(), top, (size_t)W * 4, hipMemcpyDeviceToHost, st));
@@ -3017,11 +3034,11 @@ static int batch_invert(pai_ctx* c, uint32_t* x, const uint8_t* flag, long long 
   HBig v;
   v.w = c->inv_host;
   v.trim();
-  HBig inv = inv_mod(v, c->N);
+  HBig inv = inv_mod(v, *md.mod);
   if (inv.is_zero()) return fail(PAI_ERR_NOINV, "invert() no inverse exists");
   c->inv_host = inv.words(W);
   HIPCHK(hipMemcpyAsync(top, c->inv_host.data(), (size_t)W * 4, hipMemcpyHostToDevice, st));
-  for (int l = levels - 1; l >= 0; --l) HIPCHK(inv_launch(c->tpi_e, false, params(l), inv_grid(c, ns[l + 1]), st));
+  for (int l = levels - 1; l >= 0; --l) HIPCHK(inv_launch(md.tpi, false, params(l), inv_grid(c, md.tpi, ns[l + 1]), st));
   return 0;
 }
 

@@ -17,8 +17,9 @@
 // are restored at the end by the closing Horner sum in iota = A_r^-1 R^2 mod n. There is no Fermat chain for that
 // inverse (n's factors are secret), so it comes from ONE batch inversion per chunk (Montgomery's trick on the group
 // engine, kernels_mul.hpp k_inv_up/down, one host inversion mod n^2):
-//   k_pe_awords  A_r (the pair's A limbs) -> words [n][W] for the batch inversion
-//   k_pe_iota    iota = A component of pair(R^4) x (A_r^-1 mod n^2) R^-2 -- k_pe_pre's long CIOS over the inverse's digits
+//   k_pe_awords  A_r mod n (the pair's A limbs, reduced) -> words [n][W] for the batch inversion mod n (round 5, later: it
+//                had run mod n^2 on the TPI = 4 engine, 4x the work for the same iota)
+//   k_pe_iota    iota = REDC(R^3 A_r^-1) = A_r^-1 R^2 mod n -- one split CIOS over the inverse's S digits
 //   k_pe_pow_f   the factored chain, then (A_Z, B_Z + A_Z (delta + M)): the plain pair of c, as k_pe_pow's
 // A chunk whose A_r has no inverse (probability ~2^-1023) takes k_pe_pow instead (flexpai.hip launch_pe).
 #pragma once
@@ -39,7 +40,6 @@ struct PeConst {
   int nprogf;
   const uint32_t* kf;      // [16][S] K'_t of the closing Horner sum
   const uint32_t* r2n;     // R^2 mod n
-  const uint32_t* cK4;     // pair of R^4 mod n^2 (k_pe_iota)
 };
 
 struct PeParams {
@@ -54,7 +54,8 @@ struct PeParams {
   long long n;
   uint32_t* xw;            // [2S][n] pairs
   int64_t* M;              // [n] encodings (k_pe_pre -> k_pe_pow)
-  uint32_t* aw;            // [n][ct_words] A_r as words, then its inverse mod n^2 (k_pe_awords -> batch inversion -> k_pe_iota)
+  uint32_t* aw;            // [n][aw_words] A_r mod n as words, then its inverse mod n (k_pe_awords -> batch inversion -> k_pe_iota)
+  int aw_words;            // words of n
   uint32_t* iota;          // [S][n] A_r^-1 R^2 mod n (k_pe_iota -> k_pe_pow_f)
   uint32_t* scratch;
   uint32_t* ct;
@@ -194,24 +195,29 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_pe_pow(PeParams p) {
 template <int S>
 __global__ __launch_bounds__(LANE_BLOCK) void k_pe_awords(PeParams p) {
   for (long long i = (long long)blockIdx.x * LANE_BLOCK + threadIdx.x; i < p.n; i += (long long)gridDim.x * LANE_BLOCK) {
-    uint32_t a[S];
+    uint32_t a[S], m[S];
 #pragma unroll
-    for (int j = 0; j < S; ++j) a[j] = p.xw[(size_t)j * p.n + i];
-    uint32_t* w = p.aw + (size_t)i * p.ct_words;
+    for (int j = 0; j < S; ++j) {
+      a[j] = p.xw[(size_t)j * p.n + i];
+      m[j] = p.k->nl[j];
+    }
+    lane::cond_sub<S>(a, m);   // A < 2n -> A mod n (the inverse mod n is what iota needs)
+    lane::cond_sub<S>(a, m);
+    uint32_t* w = p.aw + (size_t)i * p.aw_words;
 #pragma unroll
     for (int k = 0; k < (S * lane::LB + 31) / 32; ++k) {
       const int bit = 32 * k, j = bit / lane::LB, sh = bit - j * lane::LB;
       uint64_t v = (uint64_t)a[j] >> sh;
       if (j + 1 < S) v |= (uint64_t)a[j + 1] << (lane::LB - sh);
       if (j + 2 < S && 2 * lane::LB - sh < 32) v |= (uint64_t)a[j + 2] << (2 * lane::LB - sh);
-      w[k] = (uint32_t)v;
+      if (k < p.aw_words) w[k] = (uint32_t)v;   // (A mod n < n: the words past n's are zero)
     }
-    for (int k = (S * lane::LB + 31) / 32; k < p.ct_words; ++k) w[k] = 0u;
+    for (int k = (S * lane::LB + 31) / 32; k < p.aw_words; ++k) w[k] = 0u;
   }
 }
 
-// iota = A component of (pair of R^4) x inv R^-2 = inv R^2 mod n, inv = A_r^-1 mod n^2 from p.aw: k_pe_pre's long
-// split CIOS over the inverse's 2S digits (staged in LDS), the even lane's row
+// iota = REDC(R^3 inv) = inv R^2 mod n, inv = A_r^-1 mod n from p.aw: one split CIOS over the inverse's S digits
+// (staged in LDS) by the pair of R^3 (k_pe_pre's constant), the even lane's row (the A component: R^3 mod n)
 template <int S>
 __global__ __launch_bounds__(LANE_BLOCK, 1) void k_pe_iota(PeParams p) {
   __shared__ uint32_t lds[D4_PAIRS * D4_SLOT];
@@ -229,7 +235,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_pe_iota(PeParams p) {
     const bool valid = e < p.n;
     const long long ee = valid ? e : p.n - 1;
     uint32_t* wbuf = sx + 2 * S;
-    const int nw = p.ct_words;
+    const int nw = p.aw_words;
     d4_fence();
     for (int w = tig; w < nw; w += 2) wbuf[w] = p.aw[(size_t)ee * nw + w];
     d4_fence();
@@ -242,12 +248,11 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_pe_iota(PeParams p) {
     d4_fence();
     uint32_t a[S];
 #pragma unroll
-    for (int i = 0; i < S; ++i) a[i] = K->cK4[tig * S + i];
+    for (int i = 0; i < S; ++i) a[i] = K->cK[tig * S + i];
     uint64_t P[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) P[i] = 0;
-#pragma unroll 1
-    for (int k = 0; k < 2; ++k) d4_pass<S>(P, a, sx + k * S, 0, m, mprime, odd, std::make_integer_sequence<int, S>{});
+    d4_pass<S>(P, a, sx, 0, m, mprime, odd, std::make_integer_sequence<int, S>{});
     uint32_t y[S];
     lane::normalize<S>(P, y);
     if (valid && !odd) {

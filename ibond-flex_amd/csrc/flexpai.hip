@@ -152,6 +152,9 @@ struct pai_ctx {
   long long fb_last_n = 0;
   uint64_t fb_table_bytes = 0;
   GuardRec* d_guard = nullptr;  // test build: the address guards' record (guard.hpp); null in the product
+#if defined(FBS_AB) && (FBS_AB & 4)
+  FbDigitParams* d_abdig = nullptr;   // measurement build: k_fbs's digit parameters
+#endif
   // public-key fixed-base obfuscators (kernels_pfb.hpp): device-RNG encryption without the private key.
   // Built lazily past the break-even count (or pai_ctx_public_fb_prepare); never needed for correctness.
   int pfb_state = FB_UNTRIED;
@@ -2037,7 +2040,11 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     pd.g = guard_args(c, 0, dig_words, 0, 0);
     const int gD = (int)std::min<long long>((long long)8 * c->cus, (n + FB_DIG_BLOCK - 1) / FB_DIG_BLOCK);
     stage_mark(c, 0, st);
+#if defined(FBS_AB) && (FBS_AB & 4)
+    if (!c->fb_shoup) HIPCHK(fb_launch_digits(pd, gD, st));   // (k_fbs draws its own)
+#else
     HIPCHK(fb_launch_digits(pd, gD, st));
+#endif
     stage_mark(c, 1, st);
     FbParams pf{};
     pf.halves = c->d_fb_halves;
@@ -2056,6 +2063,11 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     if (c->fb_pair_s) {
       FbpParams pp{c->d_fbp_halves, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
       pp.g = guard_args(c, (unsigned long long)pf.K << pf.W, dig_words, w_words, 0);
+#if defined(FBS_AB) && (FBS_AB & 4)
+      if (!c->d_abdig && hipMalloc((void**)&c->d_abdig, sizeof(FbDigitParams)) != hipSuccess) return fail(PAI_ERR_HIP, "abD");
+      HIPCHK(hipMemcpyAsync(c->d_abdig, &pd, sizeof(pd), hipMemcpyHostToDevice, st));
+      pp.dig = c->d_abdig;
+#endif
 #if FLEXPAI_XCHECK
       if (!c->fb_shoup) HIPCHK(fbp_launch(c->fb_pair_s, pp, gF, st));
 #endif

@@ -118,19 +118,35 @@ struct FbFinParams {
 // otherwise push the modulus out of the SGPRs of k_fb.
 // ROW (odd, >= raw words + 3): LDS words per lane, sized to the key (21 / 37 / 69 at nb = 1024 / 2048 / 4096) so
 // that the LDS of a block does not cap the occupancy (the 83-word rows of every key size allowed 1.5 waves per SIMD).
+// the per-key constants of the digit extraction, read once per kernel
+struct FbDigitKey {
+  const FbRed* R;
+  int rb, rw, nblk, dw, kb;
+  uint32_t mask, mu0, mu1, mu2;
+};
+__device__ __forceinline__ FbDigitKey fb_digit_key(const FbDigitParams& p, int half) {
+  FbDigitKey k;
+  k.R = p.red + half;
+  k.rb = p.raw_bits;
+  k.rw = (k.rb + 31) / 32;
+  k.nblk = (k.rw + 15) / 16;
+  k.dw = k.R->dwords;
+  k.kb = k.R->kbits;
+  k.mask = (1u << p.W) - 1u;
+  k.mu0 = k.R->mu[0];
+  k.mu1 = k.R->mu[1];
+  k.mu2 = k.R->mu[2];
+  return k;
+}
+
+// element i of half `half`: its raw stream staged in the LDS row a (ROW words), reduced modulo D_h in place, cut into
+// the K digits (k_fb_digits; and, in a measurement build, k_fbs's prologue, kernels_fbs.hpp FBS_AB & 4)
 template <int ROW>
-__global__ __launch_bounds__(FB_DIG_BLOCK) void k_fb_digits(FbDigitParams p) {
-  static_assert(ROW % 2 == 1 && ROW <= FB_RAW_MAX + 3, "row");
-  __shared__ uint32_t wb[FB_DIG_BLOCK * ROW];
-  uint32_t* a = wb + threadIdx.x * ROW;
-  const int half = blockIdx.y;
-  const FbRed* R = p.red + half;
-  const int rb = p.raw_bits, rw = (rb + 31) / 32, nblk = (rw + 15) / 16;
-  const int dw = R->dwords, kb = R->kbits;
-  const uint32_t mask = (1u << p.W) - 1u;
-  const uint32_t mu0 = R->mu[0], mu1 = R->mu[1], mu2 = R->mu[2];
-  for (long long i = (long long)blockIdx.x * FB_DIG_BLOCK + threadIdx.x; i < p.n;
-       i += (long long)gridDim.x * FB_DIG_BLOCK) {
+__device__ __forceinline__ void fb_digits_elem(const FbDigitParams& p, const FbDigitKey& dk, int half, long long i, uint32_t* a) {
+  const FbRed* R = dk.R;
+  const int rb = dk.rb, rw = dk.rw, nblk = dk.nblk, dw = dk.dw, kb = dk.kb;
+  const uint32_t mask = dk.mask;
+  {
     const unsigned long long g = p.index_base + (unsigned long long)i;
     for (int b = 0; b < nblk; ++b) {
       uint32_t blk[16];
@@ -153,7 +169,7 @@ __global__ __launch_bounds__(FB_DIG_BLOCK) void k_fb_digits(FbDigitParams p) {
     }
     uint32_t q2[7] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
     {
-      const uint32_t mu[3] = {mu0, mu1, mu2};
+      const uint32_t mu[3] = {dk.mu0, dk.mu1, dk.mu2};
 #pragma unroll
       for (int x = 0; x < 3; ++x) {
         uint64_t c = 0;
@@ -217,6 +233,17 @@ __global__ __launch_bounds__(FB_DIG_BLOCK) void k_fb_digits(FbDigitParams p) {
       p.digits[FPAI_GUARD_IDX(p.g, GS_DIG_OUT, ((size_t)half * p.K + k) * p.n + i, p.g.digits, i)] = (uint32_t)(v & mask);
     }
   }
+}
+
+template <int ROW>
+__global__ __launch_bounds__(FB_DIG_BLOCK) void k_fb_digits(FbDigitParams p) {
+  static_assert(ROW % 2 == 1 && ROW <= FB_RAW_MAX + 3, "row");
+  __shared__ uint32_t wb[FB_DIG_BLOCK * ROW];
+  uint32_t* a = wb + threadIdx.x * ROW;
+  const int half = blockIdx.y;
+  const FbDigitKey dk = fb_digit_key(p, half);
+  for (long long i = (long long)blockIdx.x * FB_DIG_BLOCK + threadIdx.x; i < p.n; i += (long long)gridDim.x * FB_DIG_BLOCK)
+    fb_digits_elem<ROW>(p, dk, half, i, a);
 }
 
 // ---------------------------------------------------------------- products with a word row in LDS

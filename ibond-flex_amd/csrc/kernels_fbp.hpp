@@ -71,6 +71,9 @@ struct FbpParams {
   int32_t* exp;
   int32_t* status;
   GuardArgs g;             // test build (guard.hpp): rows = K 2^W, digits = 2 K n, out = the pair tiles' words
+#if defined(FBS_AB) && (FBS_AB & 4)
+  const FbDigitParams* dig;   // measurement build (kernels_fbs.hpp FBS_AB & 4): k_fbs draws its own digits
+#endif
 };
 
 // LDS words at a byte offset from this lane's row base (offsets past the 16-bit immediate take a second base)

@@ -44,6 +44,10 @@ constexpr int fbs_row_quads() { return FbsGeom<S>::QA + FbsGeom<S>::QAP + FbsGeo
 // aligned 128-B lines) and only the b R quads that fit in them fetched (the rest zero) -- the bytes of packed 384-B
 // rows, wrong ciphertexts; FBS_AB & 2 ("I", instructions): every digit of a and a' costs the v_alignbit + v_and that
 // cutting a 28-bit digit out of packed 32-bit words costs (on the same digit: same ciphertexts).
+// FBS_AB & 4 ("D"): k_fb_digits fused into k_fbs -- each element-half's even lane draws and reduces
+// its exponent and cuts the digits in a prologue (kernels_fb.hpp fb_digits_elem, staged in the wave's second row
+// buffer), stores them, and the product loop reads them back from L2 (agent-scope loads: another block may hold the
+// line in its L1); the host launches no k_fb_digits. Same digits, same ciphertexts.
 #ifndef FBS_AB
 #define FBS_AB 0
 #endif
@@ -271,6 +275,9 @@ __device__ __forceinline__ uint32_t fbs_guard_digit(const FbpParams& p, int h, i
 }
 #define FBS_DIGIT(k) fbs_guard_digit(p, half, (k), ee, GS_FBS_DIGIT, GS_FBS_DVAL)
 #define FBS_ROW(k, d) FPAI_GUARD_IDX(p.g, GS_FBS_ROW, ((size_t)(k) << W) + (d), p.g.rows, ee)
+#elif FBS_AB & 4
+#define FBS_DIGIT(k) __hip_atomic_load(const_cast<uint32_t*>(dg + (size_t)(k) * p.n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+#define FBS_ROW(k, d) (((size_t)(k) << W) + (d))
 #else
 #define FBS_DIGIT(k) dg[(size_t)(k) * p.n]
 #define FBS_ROW(k, d) (((size_t)(k) << W) + (d))
@@ -321,6 +328,17 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbs(FbpParams p) {
     static_assert(G::QB / 2 == HW / 4, "b R quads per lane");
     fbp_u32x4 bv[G::QB / 2];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous element's reads of both buffers are done
+#if FBS_AB & 4
+    {   // this element-half's digits (the even lane; staged in the wave's second row buffer), stored and waited
+      // (the parameters from device memory through an opaque pointer: held in registers across the element loop, they
+      // had spilled 140 VGPRs, 15 scratch accesses of them inside the product loop)
+      const FbDigitParams* dp = reinterpret_cast<const FbDigitParams*>(opaque_uniform(reinterpret_cast<const uint32_t*>(p.dig)));
+      const FbDigitKey dk = fb_digit_key(*dp, half);
+      uint32_t* arow = reinterpret_cast<uint32_t*>(lbuf + (threadIdx.x >> 6) * 2 * WB + WB) + (lane >> 1) * 37;
+      if (!odd) fb_digits_elem<37>(*dp, dk, half, ee, arow);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+#endif
     fbs_row_fetch<S>(table + (size_t)FBS_ROW(0, FBS_DIGIT(0)) * TQ, wbase, tig, bv);
     uint32_t dn = K > 1 ? FBS_DIGIT(1) : 0u;
     for (int k = 0; k < K; ++k) {

@@ -151,6 +151,14 @@ def work_fbgp(nb: int, digits: int) -> dict:
             "k_fbg_fin": float(2 * _M(nb // 32) + _M(nb // 32) + _M(nb // 16))}
 
 
+def work_sgp_fin(nb: int) -> float:
+    """The 4096-bit split-pair path's fin stage (round 5): k_sgp_w's plain product p_h B per half ((nb/64)^2 each),
+    k_fbg_garner's product mod p^2 (M(nb/32)) and k_sgp_fin's two plain products by q (q h: (nb/64)(nb/32), q t:
+    (nb/64)(3 nb/64)), canonical 32-bit limbs."""
+    s = nb // 64
+    return float(2 * s * s + _M(nb // 32) + s * (2 * s) + s * (3 * s))
+
+
 def work_pfb(nb: int, digits: int) -> float:
     """Public fixed bases (kernels_pfb.hpp): K products by factored rows over the nb/32 32-bit limbs of n, plus the
     correction (one Montgomery product mod n)."""
@@ -1156,9 +1164,12 @@ def main():
     else:
         if grp_fb and fb_pair:
             names, works = ["k_fb_digits", "k_fbgp", "k_fbg_fin"], work_fbgp(nb, fb_info[2])
-            if fb_split:   # same tables, same count, the split-pair kernel
+            if fb_split:   # same tables, same count, the split-pair kernel; Garner on lanes (k_sgp_w, k_sgp_fin)
                 names[1] = "k_sgp"
                 works["k_sgp"] = works.pop("k_fbgp")
+                names[2] = "k_sgp_w+garner+fin"
+                works.pop("k_fbg_fin")
+                works[names[2]] = work_sgp_fin(nb)
         elif grp_fb:
             names, works = ["k_fb_digits", "k_fbg", "k_fbg_fin"], work_fbg(nb, fb_info[2])
         elif use_crt and use_fb and fb_pair and fb_shoup:

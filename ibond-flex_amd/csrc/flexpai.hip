@@ -140,6 +140,7 @@ struct pai_ctx {
   FbgpHalf* d_fbgp_halves = nullptr;  // 4096-bit keys: pair-group tables (kernels_grp_pair.hpp)
   bool fb_gpair = false;
   SgpHalf* d_sgp_fb = nullptr;  // 4096-bit keys: the split-pair sampler over the same tables (kernels_sgp.hpp)
+  const uint32_t* d_sgp_q = nullptr;   //   q's S limbs (k_sgp_fin)
   FbRed* d_fb_red = nullptr;
   uint32_t *d_fb_m8 = nullptr, *d_fb_coefR = nullptr, *d_fb_q2 = nullptr, *d_fb_m0 = nullptr;
   uint32_t* d_fb_q2Rn = nullptr;  // 4096-bit keys: q^2 R mod n^2 (k_fbg_fin)
@@ -913,6 +914,11 @@ static bool sgp_enabled() {
   const char* e = xcheck_env("FLEXPAI_SGP");
   return !e || atoi(e) != 0;
 }
+// Garner's last step on lanes (k_sgp_fin); the test build's $FLEXPAI_SGP_FIN=0 keeps the group kernel k_fbg_fin
+static bool sgp_fin_enabled() {
+  const char* e = xcheck_env("FLEXPAI_SGP_FIN");
+  return !e || atoi(e) != 0;
+}
 
 template <class Upload>
 static int sgp_make_half(const HBig& P, const HBig& w, int K, const void* table, Upload&& up, SgpHalf* out) {
@@ -1433,6 +1439,7 @@ static int ensure_fb(pai_ctx* c) {
     if (sgp_enabled()) {
       std::vector<SgpHalf> svv(sv, sv + 2);
       if ((rc = upload_fb(c, svv, &c->d_sgp_fb))) return fb_unavailable(c, pai_last_error());
+      c->d_sgp_q = sv[1].p;
     }
   }
   trace_uploads("  fb uploads");
@@ -2097,7 +2104,13 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     if (grp) {   // w_h = c0 G_h^(a_h) mod p_h^2 -> Garner: h mod p^2 (S = 148), c = w_q + q^2 h mod n^2 (S = 296)
       int occH = 1, occC = 1;
       grp_fin_occupancy(&occH, &occC);
-      if (c->fb_gpair) {   // the pairs -> w_h = A + p_h B mod p_h^2 (timed with the fin stage)
+      if (c->fb_gpair && c->d_sgp_fb) {   // the pairs -> w_h = A + p_h B mod p_h^2 (timed with the fin stage)
+        SgpParams sw{};
+        sw.halves = c->d_sgp_fb;
+        sw.n = n;
+        sw.out = w;
+        HIPCHK(sgp_launch_w(sw, 2, c->cus, st));
+      } else if (c->fb_gpair) {
         const FbgpParams pg{c->d_fbgp_halves, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
         const long long gb4 = (n + BLOCK / 4 - 1) / (BLOCK / 4);
         HIPCHK(fbgp_launch_w(pg, (int)std::max<long long>(1, std::min<long long>(gb4, (long long)occH * c->cus / 2)), st));
@@ -2105,8 +2118,15 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
       const long long gb4 = (n + BLOCK / GRP_TPI - 1) / (BLOCK / GRP_TPI), gb8 = (n + BLOCK / 8 - 1) / (BLOCK / 8);
       FbgGarnerParams gh{w, n, c->d_fb_m0, c->d_fb_m8, c->d_fb_coefR, c->fb_mprime0};
       HIPCHK(grp_launch_garner(gh, (int)std::max<long long>(1, std::min<long long>(gb4, (long long)occH * c->cus)), st));
-      FbgFinParams gf{w, SB, n, c->d_N, c->d_fb_q2Rn, c->mprime_N, e.ct + (size_t)off * c->ct_words, c->ct_words};
-      HIPCHK(grp_launch_fin(gf, (int)std::max<long long>(1, std::min<long long>(gb8, (long long)occC * c->cus)), st));
+      // c = w_q + q^2 h on lanes (kernels_sgp.hpp k_sgp_fin): its intermediates' top 2S rows go to the digit buffer
+      // (2K rows, dead by now; K >= S at every window the ladder has)
+      if (c->d_sgp_q && c->ct_words == SGPF_CT_WORDS && pf.K >= SGP_S && sgp_fin_enabled()) {
+        const SgpFinParams sf{w, digits, n, c->d_sgp_q, e.ct + (size_t)off * c->ct_words, c->ct_words};
+        HIPCHK(sgp_launch_fin(sf, c->cus, st));
+      } else {
+        FbgFinParams gf{w, SB, n, c->d_N, c->d_fb_q2Rn, c->mprime_N, e.ct + (size_t)off * c->ct_words, c->ct_words};
+        HIPCHK(grp_launch_fin(gf, (int)std::max<long long>(1, std::min<long long>(gb8, (long long)occC * c->cus)), st));
+      }
       stage_mark(c, 3, st);
       continue;
     }

@@ -316,4 +316,281 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_sgp(SgpParams p) {
   }
 }
 
+// ---------------------------------------------------------------- the pairs -> w_h for Garner (nb = 4096)
+// w_h = A + p_h B mod p_h^2 from k_sgp's pair (A < 2p, B < 4p), in place in the [half][2S][n] rows: the pair made
+// canonical (A < p, B < p: A's multiple of p moved into B, then B mod p), then A + p_h B < p_h^2 by product scanning
+// -- one lane per element-half, p_h and B in VGPRs, A's limbs read as their columns come (A - f p_h, f = [A >= p_h],
+// with its borrow chain on the way), the limbs of w written as they complete (row c of w replaces row c of the pair,
+// read by then). S^2 plain MACs per element-half (round 5: in place of k_fbgp_w's Montgomery product mod p_h^2 on the
+// TPI = 4 group engine, 4 S^2 plus cross-lane traffic).
+template <int S, int C, int I>
+__device__ __forceinline__ void sgpw_mac(uint64_t& acc, const uint32_t (&b)[S], const uint32_t (&m)[S]) {
+  if constexpr (C - I >= 0 && C - I < S) acc += (uint64_t)b[I] * m[C - I];
+}
+template <int S, int C, int... Is>
+__device__ __forceinline__ void sgpw_col(uint64_t& acc, const uint32_t (&b)[S], const uint32_t (&m)[S], std::integer_sequence<int, Is...>) {
+  (sgpw_mac<S, C, Is>(acc, b, m), ...);
+}
+typedef __attribute__((address_space(1))) uint32_t sgpw_g32;   // (global, not flat: a pointer through an asm stays global)
+template <int S, int C>
+__device__ __forceinline__ void sgpw_step(uint64_t& acc, int32_t& br, uint32_t fm, const uint32_t (&b)[S], const uint32_t (&m)[S],
+                                          sgpw_g32*& out, size_t stride) {
+  if constexpr (C < S) {   // limb C of A - f p_h (>= 0 as a whole), read from the row that w's limb C replaces
+    const int32_t v = (int32_t)*out - (int32_t)(m[C] & fm) + br;
+    br = v >> LB;
+    acc += (uint32_t)v & LMASK;
+  }
+  sgpw_col<S, C>(acc, b, m, std::make_integer_sequence<int, S>{});
+  *out = (uint32_t)acc & LMASK;
+  out += stride;
+  asm volatile("" : "+v"(out));   // (one running address: 2S precomputed 64-bit offsets would not fit)
+  acc >>= LB;
+}
+template <int S, int... Cs>
+__device__ __forceinline__ void sgpw_all(uint32_t fm, const uint32_t (&b)[S], const uint32_t (&m)[S], sgpw_g32* out, size_t stride,
+                                         std::integer_sequence<int, Cs...>) {
+  uint64_t acc = 0;
+  int32_t br = 0;
+  (sgpw_step<S, Cs>(acc, br, fm, b, m, out, stride), ...);
+}
+// x >= m over S canonical limbs
+template <int S>
+__device__ __forceinline__ bool sgpw_ge(const uint32_t (&x)[S], const uint32_t (&m)[S]) {
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < S; ++i) c = ((int32_t)x[i] - (int32_t)m[i] + c) >> LB;
+  return c == 0;
+}
+
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK, 2) void k_sgp_w(SgpParams p) {
+  const int half = blockIdx.y;
+  const SgpHalf* H = p.halves + half;
+  uint32_t m[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    m[j] = H->p[j];
+    asm volatile("" : "+v"(m[j]));   // VGPRs (in SGPRs, with the rest, 53 spilled and every use became a readlane)
+  }
+  const size_t stride = (size_t)p.n;
+  for (long long e = (long long)blockIdx.x * LANE_BLOCK + threadIdx.x; e < p.n; e += (long long)gridDim.x * LANE_BLOCK) {
+    sgpw_g32* col = (sgpw_g32*)(p.out + (size_t)half * 2 * S * stride + e);
+    // the pair's rows, all loads issued before the first use; f = [A >= p_h] (A then dropped: its limbs are read
+    // again, from L1/L2, as the product's columns come)
+    uint32_t b[S];
+    uint32_t f;
+    {
+      const sgpw_g32* r = col;
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        b[i] = *r;
+        r += stride;
+        asm volatile("" : "+v"(r));
+      }
+      int32_t c = 0;
+#pragma unroll
+      for (int i = 0; i < S; ++i) c = ((int32_t)b[i] - (int32_t)m[i] + c) >> LB;
+      f = c == 0 ? 1u : 0u;
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        b[i] = *r;
+        r += stride;
+        asm volatile("" : "+v"(r));
+      }
+    }
+    {   // B + f, then B mod p_h (B + f <= 4 p_h)
+      uint32_t cy = f;
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        const uint32_t v = b[i] + cy;
+        b[i] = v & LMASK;
+        cy = v >> LB;
+      }
+    }
+#pragma unroll 1
+    for (int rep = 0; rep < 4; ++rep) {
+      const uint32_t fm = sgpw_ge<S>(b, m) ? LMASK : 0u;
+      int32_t br = 0;
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        const int32_t v = (int32_t)b[i] - (int32_t)(m[i] & fm) + br;
+        b[i] = (uint32_t)v & LMASK;
+        br = v >> LB;
+      }
+    }
+    sgpw_all<S>(f ? LMASK : 0u, b, m, col, stride, std::make_integer_sequence<int, 2 * S>{});
+  }
+}
+
+// ---------------------------------------------------------------- Garner's last step (nb = 4096)
+// c = w_q + q^2 h (exact: < n^2), h < p^2 and w_q < q^2 from k_fbg_garner / k_sgp_w, as two plain products by q on
+// one lane per element: t = q h (74 x 148 limbs), then u = q t (74 x 222), each by operand scanning with a rotating
+// window of S = 74 64-bit column accumulators (q in VGPRs: 74 + 148 registers; column J is complete after operand limb
+// J and leaves the window then -- the lazy-CIOS shape of bn_lane.hpp without a reduction), the operand's limbs loaded
+// SGPF_D limbs ahead; then c = w_q + u, cut into words. The intermediates go through memory, limb J of a product over
+// limb J of its operand once that was read: t over h's rows (and the digit buffer, dead by then, for t's top S rows),
+// u over t's (and the digit buffer's next S rows). 27.4 k plain MACs per element (round 5: in place of k_fbg_fin's
+// Montgomery product at S = 296 on the TPI = 8 group engine, 175 k).
+struct SgpFinParams {
+  uint32_t* w;             // [2][2S][n]: h (half 0's rows, < p^2), w_q (half 1's rows, < q^2)
+  uint32_t* t_hi;          // [2S][n]: the digit buffer (dead after k_sgp): t's rows 2S .. 3S-1, u's rows 3S .. 4S-1
+  long long n;
+  const uint32_t* q;       // S limbs
+  uint32_t* ct;
+  int ct_words;
+};
+constexpr int SGPF_D = 4;   // operand limbs in flight
+constexpr int SGPF_CT_WORDS = 256;   // words of a ciphertext (c < n^2, nb = 4096; the host checks ct_words)
+
+typedef __attribute__((address_space(1))) uint32_t sgpf_g32;
+// a limb this lane stored earlier in the kernel: read at device scope (sc1: from L2, where the write-through store
+// went, not from a vector-L1 line the lane may have fetched before the store -- ordering the kernel does not want to
+// rest on the L1's store-hit policy)
+template <bool COH>
+__device__ __forceinline__ uint32_t sgpf_ld(const sgpf_g32* p) {
+  if constexpr (COH) return __scoped_atomic_load_n(p, __ATOMIC_RELAXED, __MEMORY_SCOPE_DEVICE);
+  else return *p;
+}
+template <class T>
+__device__ __forceinline__ T* sgpf_adv(T* p, size_t n) {   // one running row address (precomputed ones would not fit)
+  p += n;
+  asm volatile("" : "+v"(p));
+  return p;
+}
+
+// operand limb JJ of a block (x), its S MACs into the window, column JJ leaves: its limb -> *ks; the next load issued
+template <int S, bool COH, int JJ>
+__device__ __forceinline__ void sgpf_step(uint64_t (&P)[S], uint32_t (&q)[S], uint32_t (&ring)[SGPF_D], const sgpf_g32*& xs,
+                                          sgpf_g32*& ks, size_t n) {
+#pragma unroll
+  for (int i = 0; i < S; ++i) asm volatile("" : "+s"(q[i]));   // (else LLVM hoists the 64-bit zero-extended q: 148 registers)
+  const uint32_t x = ring[JJ % SGPF_D];
+  if constexpr (JJ + SGPF_D < S) {
+    ring[JJ % SGPF_D] = sgpf_ld<COH>(xs);   // limb JJ + D
+    xs = sgpf_adv(xs, n);
+  }
+#pragma unroll
+  for (int i = 0; i < S; ++i) P[(i + JJ) % S] += (uint64_t)q[i] * x;
+  const uint64_t v = P[JJ % S];
+  P[(JJ + 1) % S] += v >> LB;
+  P[JJ % S] = 0;
+  *ks = (uint32_t)v & LMASK;
+  ks = sgpf_adv(ks, n);
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+    if (i != JJ % S) asm volatile("" : "+v"(P[i]));
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int S, bool COH, int... Js>
+__device__ __forceinline__ void sgpf_block(uint64_t (&P)[S], uint32_t (&q)[S], const sgpf_g32* xs, sgpf_g32* ks, size_t n,
+                                           std::integer_sequence<int, Js...>) {
+  uint32_t ring[SGPF_D];
+#pragma unroll
+  for (int d = 0; d < SGPF_D; ++d) {
+    ring[d] = sgpf_ld<COH>(xs);
+    xs = sgpf_adv(xs, n);
+  }
+  (sgpf_step<S, COH, Js>(P, q, ring, xs, ks, n), ...);
+}
+// the last S columns: no operand limb
+template <int S>
+__device__ __forceinline__ void sgpf_tail(uint64_t (&P)[S], sgpf_g32* ks, size_t n) {
+#pragma unroll
+  for (int jj = 0; jj < S; ++jj) {
+    const uint64_t v = P[jj];
+    if (jj + 1 < S) P[jj + 1] += v >> LB;
+    *ks = (uint32_t)v & LMASK;
+    ks = sgpf_adv(ks, n);
+  }
+}
+
+// c = w_q + u (limbs of u: rows at a (2S), b (S), b2 (S); w_q: 2S rows) -> the NW ciphertext words (compile-time
+// packing; the 4S limbs span NW + 3 words, the top ones zero since c < n^2 -- and not stored: they are the next
+// element's first words). The limbs are loaded SGPF_WD ahead (a load right before its use waited out an L2 round
+// trip per limb: 441 waits per element).
+constexpr int SGPF_WD = 8;
+template <int S>
+struct SgpfWordSrc {
+  const sgpf_g32 *ua, *ub, *uc, *wq;
+  size_t n;
+  template <int J>
+  __device__ __forceinline__ uint32_t u() {   // limb J of u (in order)
+    const sgpf_g32*& p = J < 2 * S ? ua : (J < 3 * S ? ub : uc);
+    const uint32_t v = sgpf_ld<true>(p);
+    p = sgpf_adv(p, n);
+    return v;
+  }
+  template <int J>
+  __device__ __forceinline__ uint32_t w() {   // limb J of w_q (J < 2S)
+    const uint32_t v = *wq;
+    wq = sgpf_adv(wq, n);
+    return v;
+  }
+};
+template <int S, int NW, int J>
+__device__ __forceinline__ void sgpf_word_step(SgpfWordSrc<S>& src, uint32_t (&ru)[SGPF_WD], uint32_t (&rw)[SGPF_WD], uint64_t& buf,
+                                               uint64_t& cy, sgpf_g32* ct) {
+  constexpr int NB = (LB * J) % 32;   // bits in buf before this limb
+  uint64_t v = (uint64_t)ru[J % SGPF_WD] + cy;
+  if constexpr (J < 2 * S) v += rw[J % SGPF_WD];
+  if constexpr (J + SGPF_WD < 4 * S) ru[J % SGPF_WD] = src.template u<J + SGPF_WD>();
+  if constexpr (J + SGPF_WD < 2 * S) rw[J % SGPF_WD] = src.template w<J + SGPF_WD>();
+  cy = v >> LB;
+  buf |= (v & LMASK) << NB;
+  if constexpr (NB + LB >= 32) {
+    constexpr int WI = (LB * J) / 32;   // word completed by this limb
+    if constexpr (WI < NW) ct[WI] = (uint32_t)buf;
+    buf >>= 32;
+  }
+}
+template <int S, int NW, int... Js>
+__device__ __forceinline__ void sgpf_words_all(SgpfWordSrc<S>& src, sgpf_g32* ct, std::integer_sequence<int, Js...>) {
+  uint32_t ru[SGPF_WD], rw[SGPF_WD];
+#pragma unroll
+  for (int d = 0; d < SGPF_WD; ++d) {
+    ru[d] = sgpf_ld<true>(src.ua);
+    src.ua = sgpf_adv(src.ua, src.n);
+    rw[d] = *src.wq;
+    src.wq = sgpf_adv(src.wq, src.n);
+  }
+  uint64_t buf = 0, cy = 0;
+  (sgpf_word_step<S, NW, Js>(src, ru, rw, buf, cy, ct), ...);
+}
+
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK, 2) void k_sgp_fin(SgpFinParams p) {
+  static_assert(S == SGP_S, "n^2 of a 4096-bit key: 4 S limbs, 256 words");
+  uint32_t q[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) q[i] = (uint32_t)__builtin_amdgcn_readfirstlane(p.q[i]);   // SGPRs
+  const size_t n = (size_t)p.n;
+  using Js = std::make_integer_sequence<int, S>;
+  for (long long e = (long long)blockIdx.x * LANE_BLOCK + threadIdx.x; e < p.n; e += (long long)gridDim.x * LANE_BLOCK) {
+    sgpf_g32* h = (sgpf_g32*)(p.w + e);                 // rows 0 .. 2S-1
+    sgpf_g32* th = (sgpf_g32*)(p.t_hi + e);             // rows 2S .. 3S-1
+    sgpf_g32* th2 = (sgpf_g32*)(p.t_hi + S * n + e);    // rows 3S .. 4S-1
+    uint64_t P[S];
+    // t = q h: h's 2S limbs (two blocks), t's 3S limbs
+#pragma unroll
+    for (int i = 0; i < S; ++i) P[i] = 0;
+#pragma unroll 1
+    for (int blk = 0; blk < 2; ++blk) sgpf_block<S, false>(P, q, h + (size_t)blk * S * n, h + (size_t)blk * S * n, n, Js{});
+    sgpf_tail<S>(P, th, n);
+    // u = q t: t's 3S limbs, u's 4S limbs
+#pragma unroll
+    for (int i = 0; i < S; ++i) P[i] = 0;
+#pragma unroll 1
+    for (int blk = 0; blk < 3; ++blk) {
+      sgpf_g32* rows = blk < 2 ? h + (size_t)blk * S * n : th;
+      sgpf_block<S, true>(P, q, rows, rows, n, Js{});
+    }
+    sgpf_tail<S>(P, th2, n);
+    // c = w_q + u -> words
+    {
+      SgpfWordSrc<S> src{h, th, th2, (const sgpf_g32*)(p.w + (size_t)2 * S * n + e), n};
+      sgpf_words_all<S, SGPF_CT_WORDS>(src, (sgpf_g32*)(p.ct + (size_t)e * SGPF_CT_WORDS), std::make_integer_sequence<int, 4 * S>{});
+    }
+  }
+}
+
 }  // namespace fpai

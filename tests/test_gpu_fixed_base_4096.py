@@ -7,6 +7,9 @@ engine, recombined by k_crt_fin<8>), SURVEY.md §8 row (f) nb = 4096 / BASELINE 
   bases and ragged sizes, identical across windows, decryptable;
 * the split-pair sampler (kernels_sgp.hpp: k_sgp, the default) and the pair-group k_fbgp (FLEXPAI_SGP=0) give
   identical ciphertexts from the same tables;
+* round 5's lane kernels for the pairs -> w_h step and Garner's last product (k_sgp_w, k_sgp_fin) against the group
+  kernels they replace (k_fbgp_w, k_fbg_fin; $FLEXPAI_SGP_FIN=0 in the test build) at counts 1, 2, 63, 129, 1000
+  -- every element, so a store past an element's 256 words into its neighbour's shows;
 * with the table memory capped, device-RNG encryption falls back to the public-key path (r = the ChaCha20
   stream, bit-identical to the explicit-r reference path) and decryption is unaffected."""
 import numpy as np
@@ -142,3 +145,26 @@ def test_split_sampler_matches_group_engine(ctx4096, golden, monkeypatch, xlib):
     ct2, ex2, _ = ref.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=2 ** 32 - 3)
     assert ref.fb_ready and not ref.split_sampler & 1
     assert np.array_equal(ct, ct2) and np.array_equal(ex, ex2)
+
+
+@pytest.mark.parametrize("count", [1, 2, 63, 129, 1000])
+def test_lane_garner_matches_group_garner(golden, monkeypatch, xlib, count):
+    N = _native()
+    key = _key(golden)
+    rk = bytes(range(3, 35))
+    x = (np.random.default_rng(count).standard_normal(count) * 1e3).astype(np.float32)
+    out = []
+    for fin in ("1", "0"):
+        monkeypatch.setenv("FLEXPAI_SGP_FIN", fin)
+        ctx = N.Context(key.n, 0, key.p, key.q, lib=xlib)
+        try:
+            ctx.set_fb_window(8)
+            ctx.prepare_fixed_base()
+            assert ctx.split_sampler & 1
+            out.append(ctx.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=7)[:2])
+        finally:
+            ctx.close()
+    (ca, ea), (cb, eb) = out
+    assert np.array_equal(ca, cb) and np.array_equal(ea, eb)
+    got = N.words_to_ints(ca[[0, count - 1]])
+    assert got[0] < key.n * key.n and got[-1] < key.n * key.n

@@ -356,8 +356,13 @@ __device__ __forceinline__ void decf_run(uint32_t (&A)[S], uint32_t (&B)[S], con
 
 // x_h = c~^(p_h - 1) * (1, 0) R^-1: the plain pair of c^(p_h - 1) mod p_h^2. FACTORED: the B-free chain (decf_run, the
 // product); otherwise the general chain (run_pair_program; the test build's cross-check)
+// Two waves per SIMD (round 5): the allocator then spills ~20 values per chain step that one wave per SIMD keeps in 386
+// registers, and the second wave covers those reloads and the reduction digits' dependency chains -- measured on one
+// box, 443 -> 412 ms per 1M, 2.31 -> 2.48 M dec/s (profiles/r05_ab_dec_pair_occupancy.txt; k_crt_b_pair, with heavier
+// spills, lost 5 % the same way and keeps LANE_OCC).
+constexpr int DEC_PAIR_OCC = 2;
 template <int S, bool FACTORED>
-__global__ __launch_bounds__(LANE_BLOCK, LANE_OCC) void k_dec_pow_pair(CrtParams p) {
+__global__ __launch_bounds__(LANE_BLOCK, DEC_PAIR_OCC) void k_dec_pow_pair(CrtParams p) {
   const int half = blockIdx.y;
   const CrtHalf* H = p.halves + half;
   uint32_t m[S];

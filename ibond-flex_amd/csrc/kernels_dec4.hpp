@@ -507,7 +507,10 @@ __device__ __forceinline__ void d4f_run(uint32_t (&a)[S], uint32_t* st, uint32_t
 }
 
 template <int S>
-__global__ __launch_bounds__(LANE_BLOCK, 2) void k_dec4_pow(Dec4Params p) {
+#ifndef FPAI_DEC4_OCC
+#define FPAI_DEC4_OCC 2   // waves per SIMD (measurement builds: tools/gpu/ab_dec4_occ_run.sh)
+#endif
+__global__ __launch_bounds__(LANE_BLOCK, FPAI_DEC4_OCC) void k_dec4_pow(Dec4Params p) {
   constexpr int TQ = tile_quads<S>();
   using Q = std::make_integer_sequence<int, TQ>;
   __shared__ uint32_t lds[D4_PAIRS * D4R_SLOT + 2 * S];

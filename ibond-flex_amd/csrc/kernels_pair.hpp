@@ -143,20 +143,40 @@ struct DecPairPreParams {
 
 // one digit of the long CIOS: the constant pair (A, B) in registers times the ciphertext digit cj
 template <int S, int J>
-__device__ __forceinline__ void pre_step(uint64_t (&P1)[S], uint64_t (&P2)[S], const uint32_t (&A)[S], const uint32_t (&B)[S],
+__device__ __forceinline__ void pre_step(uint64_t (&P1)[S], uint64_t (&P2)[S], uint32_t (&A)[S], uint32_t (&B)[S],
                                          uint32_t cj, const uint32_t (&m)[S], uint32_t mprime) {
+#pragma unroll
+  for (int i = 0; i < S; ++i) asm volatile("" : "+v"(A[i]), "+v"(B[i]));   // (else LLVM hoists 64-bit zero-extended copies)
   pair::mul_digit<S, J>(P1, P2, A, B, cj, 0u);
   pair::red2<S, J>(P1, P2, m, mprime);
 }
+// the ciphertext's 28-bit digits from its words, read one digit ahead (no S-digit array beside the two rows)
+struct PreDigits {
+  const uint32_t* cw;
+  int nw, bit;       // words; bit of the next digit
+  uint32_t cur;
+  __device__ __forceinline__ uint32_t fetch() {   // (clamped loads and selects: no branch inside the pass)
+    const int wi = bit >> 5, sh = bit & 31;
+    const uint32_t l = cw[wi < nw ? wi : nw - 1], h = cw[wi + 1 < nw ? wi + 1 : nw - 1];
+    const uint64_t lo = wi < nw ? (uint64_t)l : 0ull;
+    const uint64_t hi = wi + 1 < nw ? (uint64_t)h : 0ull;
+    bit += lane::LB;
+    return (uint32_t)(((hi << 32) | lo) >> sh) & lane::LMASK;
+  }
+  __device__ __forceinline__ uint32_t next() {
+    const uint32_t v = cur;
+    cur = fetch();
+    return v;
+  }
+};
 template <int S, int... Js>
-__device__ __forceinline__ void pre_pass(uint64_t (&P1)[S], uint64_t (&P2)[S], const uint32_t (&A)[S], const uint32_t (&B)[S],
-                                         const uint32_t (&cd)[S], const uint32_t (&m)[S], uint32_t mprime,
-                                         std::integer_sequence<int, Js...>) {
-  (pre_step<S, Js>(P1, P2, A, B, cd[Js], m, mprime), ...);
+__device__ __forceinline__ void pre_pass(uint64_t (&P1)[S], uint64_t (&P2)[S], uint32_t (&A)[S], uint32_t (&B)[S],
+                                         PreDigits& dg, const uint32_t (&m)[S], uint32_t mprime, std::integer_sequence<int, Js...>) {
+  (pre_step<S, Js>(P1, P2, A, B, dg.next(), m, mprime), ...);
 }
 
 template <int S>
-__global__ __launch_bounds__(LANE_BLOCK) void k_dec_pre_pair(DecPairPreParams p) {
+__global__ __launch_bounds__(LANE_BLOCK, 2) void k_dec_pre_pair(DecPairPreParams p) {
   const int half = blockIdx.y;
   const DecPairHalf* H = p.halves + half;
   const uint32_t mprime = H->mprime;
@@ -165,25 +185,16 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_dec_pre_pair(DecPairPreParams p)
     uint32_t m[S], A[S], B[S];
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      m[j] = H->p[j];
+      m[j] = (uint32_t)__builtin_amdgcn_readfirstlane(H->p[j]);   // SGPRs (as VGPRs the pass spilled 202 of them)
       A[j] = H->cK[j];
       B[j] = H->cK[S + j];
     }
     uint64_t P1[S], P2[S];
     pair::zero2<S>(P1, P2);
-    const int nw = p.ct_words;
+    PreDigits dg{cw, p.ct_words, 0, 0u};
+    dg.cur = dg.fetch();
 #pragma unroll 1
-    for (int k = 0; k < p.kchunks; ++k) {
-      uint32_t cd[S];
-#pragma unroll
-      for (int j = 0; j < S; ++j) {
-        const int bit = (k * S + j) * lane::LB, wi = bit >> 5, sh = bit & 31;
-        const uint64_t lo = wi < nw ? (uint64_t)cw[wi] : 0ull;
-        const uint64_t hi = wi + 1 < nw ? (uint64_t)cw[wi + 1] : 0ull;
-        cd[j] = (uint32_t)(((hi << 32) | lo) >> sh) & lane::LMASK;
-      }
-      pre_pass<S>(P1, P2, A, B, cd, m, mprime, std::make_integer_sequence<int, S>{});
-    }
+    for (int k = 0; k < p.kchunks; ++k) pre_pass<S>(P1, P2, A, B, dg, m, mprime, std::make_integer_sequence<int, S>{});
     uint32_t xa[S], xb[S];
     lane::normalize<S>(P1, xa);
     lane::normalize<S>(P2, xb);

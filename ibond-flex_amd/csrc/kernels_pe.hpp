@@ -70,7 +70,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_pe_pre(PeParams p) {
   const PeConst* K = p.k;
   uint32_t m[S];
 #pragma unroll
-  for (int j = 0; j < S; ++j) m[j] = K->nl[j];
+  for (int j = 0; j < S; ++j) m[j] = (uint32_t)__builtin_amdgcn_readfirstlane(K->nl[j]);   // SGPRs: with 74 VGPRs of modulus the pass kept P in AGPRs (11 k moves, 1.8 k scratch accesses per pass)
   const uint32_t mprime = K->mprime;
   const int tig = threadIdx.x & 1;
   const bool odd = tig != 0;
@@ -124,8 +124,8 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_pe_pre(PeParams p) {
     uint64_t P[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) P[i] = 0;
-#pragma unroll 1
-    for (int k = 0; k < 2; ++k) d4_pass<S>(P, a, sx + k * S, 0, m, mprime, odd, std::make_integer_sequence<int, S>{});
+d4_pass<S>(P, a, sx, 0, m, mprime, odd, std::make_integer_sequence<int, S>{});
+    d4_pass<S>(P, a, sx + S, 0, m, mprime, odd, std::make_integer_sequence<int, S>{});
     uint32_t y[S];
     lane::normalize<S>(P, y);
     if (valid) {

@@ -96,7 +96,11 @@ def check_sgs(vec_path, out_path, K=9):
     a = [unlimbs(v[o:o + S]), unlimbs(v[o + S:o + 2 * S])]
     m2 = m * m
     g = read(out_path)
-    bad = 0
+    # the b halves sgs_stream.hip wrote: word j of b_d = 0x9E3779B9 (2 j + d + 1) ^ 0xA5A5A5A5 d (32-bit)
+    b = [sum((((0x9E3779B9 * (2 * j + d + 1)) & 0xFFFFFFFF) ^ ((0xA5A5A5A5 * d) & 0xFFFFFFFF)) << (32 * j) for j in range(64))
+         for d in range(2)]
+    bad = badb = 0
+    ob = PAIRS * 2 * S
     for e in range(PAIRS):
         want = 1
         for k in range(K):
@@ -104,8 +108,11 @@ def check_sgs(vec_path, out_path, K=9):
         A = unlimbs(g[(2 * e) * S:(2 * e + 1) * S])
         B = unlimbs(g[(2 * e + 1) * S:(2 * e + 2) * S])
         bad += (A + m * B) % m2 != want
-    print("k_sgs: %d/%d pairs exact" % (PAIRS - bad, PAIRS))
-    return bad == 0
+        w = g[ob + 66 * e:ob + 66 * e + 66]
+        got = sum(w[j] << (32 * j) for j in range(64)) + (w[64] << (32 * 32)) + (w[65] << (32 * 64))
+        badb += got != sum(b[(k + e) & 1] for k in range(K))
+    print("k_sgs: %d/%d pairs exact, %d/%d b sums exact" % (PAIRS - bad, PAIRS, PAIRS - badb, PAIRS))
+    return bad == 0 and badb == 0
 
 
 if __name__ == "__main__":

@@ -92,6 +92,27 @@ __device__ __forceinline__ uint32_t sgp_guard_digit_s(const SgsParams& p, int h,
 #define SGS_DIGIT(k) dg[(size_t)(k) * p.n]
 #endif
 
+// step 1 as a sweep over the columns [C0, C0 + NC) of X a' only (digits J = S-1 down to JMIN, a' quads descending
+// one ahead): P[c - C0] += X_i a'_J for i + J = c
+template <int S, int C0, int NC, int JMIN, int T>
+__device__ __forceinline__ void sgs_q2_digit(uint64_t (&P)[NC], const uint32_t (&X)[S], const uint4* q, uint4& cur, uint4& nxt) {
+  constexpr int J = S - 1 - T;
+  if constexpr (T > 0 && J % 4 == 3) cur = nxt;
+  if constexpr ((T == 0 || J % 4 == 3) && J / 4 > JMIN / 4) nxt = q[(J / 4 - 1) * 32];
+  const uint32_t d = sgs_qword<J % 4>(cur);
+  constexpr int lo = C0 - J > 0 ? C0 - J : 0, hi = C0 + NC - 1 - J < S - 1 ? C0 + NC - 1 - J : S - 1;
+#pragma unroll
+  for (int i = lo; i <= hi; ++i) P[i + J - C0] += (uint64_t)X[i] * d;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) asm volatile("" : "+v"(P[i]));
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int S, int C0, int NC, int JMIN, int... Ts>
+__device__ __forceinline__ void sgs_q2_all(uint64_t (&P)[NC], const uint32_t (&X)[S], const uint4* q, std::integer_sequence<int, Ts...>) {
+  uint4 cur = q[(SGS_NQ - 1) * 32], nxt;
+  (sgs_q2_digit<S, C0, NC, JMIN, Ts>(P, X, q, cur, nxt), ...);
+}
+
 // step 2 part H / part L, digit J of a: P[i + J] += X_i a_J, then += Q_i mbar_J (mbar = R - m) for i in [I0, I1] with
 // i + J < S
 template <int S, int I0, int I1, int PLO, int J>
@@ -254,6 +275,146 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_sgs(SgsParams p) {
 #pragma unroll
       for (int i = 0; i < S; ++i) p.out[((size_t)half * 2 * S + tig * S + i) * p.n + e] = X[i];
       if constexpr (BS) p.bcc[((size_t)half * 2 + tig) * p.n + e] = cc;
+    }
+  }
+}
+
+// BS = 2 form: step 1 as two column sweeps ([73, 110) then [110, 147): Q's low limbs out of the first, X, 37
+// accumulators and them live in the second: 185 VGPRs) and step 2 in four parts by the index of X_i / Q_i (i >= 56,
+// >= 37, >= 18, >= 0: at most 186 live), so that the element's b sum (32 words and a carry count per lane) stays in
+// registers and the row's b words come from LDS (DMA'd into the a' quads after step 1): no global round trip.
+template <int S, int LO, int HI>
+__device__ __forceinline__ void sgs_part(uint64_t (&P)[S], const uint32_t (&X)[S], const uint32_t (&Q)[S], const uint32_t (&m)[S],
+                                         const uint4* ar, uint32_t ob) {
+#pragma unroll
+  for (int i = LO; i <= HI; ++i) P[i] = (uint64_t)((uint32_t)__builtin_amdgcn_update_dpp(0, (int)Q[i], 0xA0, 0xF, 0xF, false) * ob);
+  sgs_s2_all<S, LO, HI, LO>(P, X, Q, m, ar, std::make_integer_sequence<int, S - LO>{});
+}
+
+template <int S>
+__global__ __launch_bounds__(LANE_BLOCK, 2) void k_sgs2(SgsParams p) {
+  static_assert(S == SGP_S, "rows of 19 quads");
+  constexpr int C1 = S - 1 + 37;   // step 1's second sweep starts at column 110
+  __shared__ __attribute__((aligned(16))) uint4 lrows[(LANE_BLOCK / 64) * SGS_WAVE_Q];
+  const int half = blockIdx.y;
+  const SgsHalf* H = p.halves + half;
+  uint32_t m[S];
+#pragma unroll
+  for (int j = 0; j < S; ++j) m[j] = H->p[j];
+  const uint4* atab = H->atab;
+  const int K = p.K, W = p.W;
+  const int lane = threadIdx.x & 63, tig = threadIdx.x & 1, pw = lane >> 1;
+  const bool odd = tig != 0;
+  const uint4* wq = lrows + (threadIdx.x >> 6) * SGS_WAVE_Q;
+  typedef __attribute__((address_space(3))) uint4 lds_q;
+  const uint32_t lb = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds_q*)wq);
+  const uint4* ar = wq + pw;
+  const uint4* apr = wq + SGS_NQ * 32 + pw;
+  uint32_t ob = odd ? 1u : 0u;
+  asm volatile("" : "+v"(ob));
+  constexpr int PAIRS = LANE_BLOCK / 2;
+  for (long long base = (long long)blockIdx.x * PAIRS; base < p.n; base += (long long)gridDim.x * PAIRS) {
+    const long long e = base + (threadIdx.x >> 1);
+    const bool valid = e < p.n;
+    const long long ee = valid ? e : p.n - 1;
+    const uint32_t* dg = p.digits + (size_t)half * K * p.n + ee;
+    (void)dg;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    uint32_t dcur = SGS_DIGIT(0);
+    sgs_rows_dma(atab, 0, W, dcur, lb, lane, p.g);
+    uint32_t dn = K > 1 ? SGS_DIGIT(1) : 0u;
+    lds_dma_wait();
+    uint32_t X[S];
+#pragma unroll
+    for (int g = 0; g < SGS_NQ; ++g) {
+      const uint4 v = ar[g * 32];
+      if (4 * g < S) X[4 * g] = odd ? 0u : v.x;
+      if (4 * g + 1 < S) X[4 * g + 1] = odd ? 0u : v.y;
+      if (4 * g + 2 < S) X[4 * g + 2] = odd ? 0u : v.z;
+      if (4 * g + 3 < S) X[4 * g + 3] = odd ? 0u : v.w;
+    }
+    uint32_t bsw[32], cc = 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    sgs_b_dma(H->btab, H->bstride, 0, W, dcur, lb, lane);
+    lds_dma_wait();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint4 b = apr[(8 * tig + q) * 32];
+      bsw[4 * q] = b.x, bsw[4 * q + 1] = b.y, bsw[4 * q + 2] = b.z, bsw[4 * q + 3] = b.w;
+    }
+    for (int k = 1; k < K; ++k) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      sgs_rows_dma(atab, (size_t)k, W, dn, lb, lane, p.g);
+      dcur = dn;
+      dn = k + 1 < K ? SGS_DIGIT(k + 1) : 0u;
+      lds_dma_wait();
+      uint32_t Q[S];
+      {
+        uint64_t c;
+        {
+          uint64_t P[37];
+#pragma unroll
+          for (int i = 0; i < 37; ++i) P[i] = 0;
+          sgs_q2_all<S, S - 1, 37, 0>(P, X, apr, std::make_integer_sequence<int, S>{});
+          c = P[0] >> lane::LB;
+#pragma unroll
+          for (int i = 1; i < 37; ++i) {
+            const uint64_t t = P[i] + c;
+            Q[i - 1] = lane::limb32(t);
+            c = t >> lane::LB;
+          }
+        }
+        {
+          uint64_t P[37];
+#pragma unroll
+          for (int i = 0; i < 37; ++i) P[i] = 0;
+          sgs_q2_all<S, C1, 37, C1 - (S - 1)>(P, X, apr, std::make_integer_sequence<int, 2 * S - 1 - C1>{});
+#pragma unroll
+          for (int i = 0; i < 37; ++i) {
+            const uint64_t t = P[i] + c;
+            Q[36 + i] = lane::limb32(t);
+            c = t >> lane::LB;
+          }
+          Q[S - 1] = lane::limb32(c);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      sgs_b_dma(H->btab, H->bstride, (size_t)k, W, dcur, lb, lane);
+      uint64_t P[S];
+      sgs_part<S, 56, S - 1>(P, X, Q, m, ar, ob);
+      sgs_part<S, 37, 55>(P, X, Q, m, ar, ob);
+      sgs_part<S, 18, 36>(P, X, Q, m, ar, ob);
+      sgs_part<S, 0, 17>(P, X, Q, m, ar, ob);
+      {
+        uint64_t c = 0;
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+          const uint64_t t = P[i] + c;
+          X[i] = lane::limb32(t);
+          c = t >> lane::LB;
+        }
+      }
+      lds_dma_wait();
+      {
+        unsigned int c = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const uint4 b = apr[(8 * tig + q) * 32];
+          bsw[4 * q] = __builtin_addc(bsw[4 * q], b.x, c, &c);
+          bsw[4 * q + 1] = __builtin_addc(bsw[4 * q + 1], b.y, c, &c);
+          bsw[4 * q + 2] = __builtin_addc(bsw[4 * q + 2], b.z, c, &c);
+          bsw[4 * q + 3] = __builtin_addc(bsw[4 * q + 3], b.w, c, &c);
+        }
+        cc += c;
+      }
+    }
+    if (valid && FPAI_GUARD_OK(p.g, GS_SGP_OUT, ((size_t)half * 2 * S + tig * S + S - 1) * p.n + e, p.g.out, e)) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) p.out[((size_t)half * 2 * S + tig * S + i) * p.n + e] = X[i];
+      uint4* bsp = p.bsum + ((size_t)half * 16 + 8 * tig) * p.n + e;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) bsp[(size_t)q * p.n] = make_uint4(bsw[4 * q], bsw[4 * q + 1], bsw[4 * q + 2], bsw[4 * q + 3]);
+      p.bcc[((size_t)half * 2 + tig) * p.n + e] = cc;
     }
   }
 }

@@ -4,9 +4,10 @@
 //   time : ./sgs_stream time <n> <W> <K>      one half, random 28-bit limbs in every row, random digits: k_sgp on a
 //                                             table of 512-B factored rows, k_sgs on 640-B Shoup rows with (BS = 1) or
 //                                             without (BS = 0) the b sum over the factored table's b halves
-//   check: ./sgs_stream check <vec.bin> <out.bin>   rows (k, 0) = (a0, a0', b0), (k, 1) = (a1, a1', b1) of
+//   check: ./sgs_stream check <vec.bin> <out.bin> [2]   rows (k, 0) = (a0, a0', b0), (k, 1) = (a1, a1', b1) of
 //                                             tools/microbench/sgp_shoup_vec.py, digit k of element e = (k + e) & 1,
-//                                             K = 9, BS = 1; the first 64 pairs and b sums written for check_sgs
+//                                             K = 9, k_sgs BS = 1 (or k_sgs2); the first 64 pairs and b sums written
+//                                             for check_sgs
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -115,7 +116,8 @@ int main(int argc, char** argv) {
   sp.bcc = bcc;
   const int grid = (int)std::min<long long>((n + 127) / 128, (long long)cus * 2);
   if (check) {
-    k_sgs<S, 1><<<dim3(grid, 1), LANE_BLOCK>>>(sp);
+    if (argc > 4 && atoi(argv[4]) == 2) k_sgs2<S><<<dim3(grid, 1), LANE_BLOCK>>>(sp);
+    else k_sgs<S, 1><<<dim3(grid, 1), LANE_BLOCK>>>(sp);
     CK(hipDeviceSynchronize());
     std::vector<uint32_t> o((size_t)2 * S * n), r(64 * 2 * S), bs((size_t)64 * n), cc((size_t)2 * n), rb(64 * 66);
     CK(hipMemcpy(o.data(), out, o.size() * 4, hipMemcpyDeviceToHost));
@@ -180,13 +182,16 @@ int main(int argc, char** argv) {
   auto sgp = [&]() { k_sgp<S><<<dim3(grid, 1), LANE_BLOCK>>>(gp); };
   auto sgs0 = [&]() { k_sgs<S, 0><<<dim3(grid, 1), LANE_BLOCK>>>(sp); };
   auto sgs1 = [&]() { k_sgs<S, 1><<<dim3(grid, 1), LANE_BLOCK>>>(sp); };
+  auto sgs2 = [&]() { k_sgs2<S><<<dim3(grid, 1), LANE_BLOCK>>>(sp); };
   timeit(sgp);
   timeit(sgs0);
   timeit(sgs1);
+  timeit(sgs2);
   for (int r = 0; r < 3; ++r) {
-    const float a = timeit(sgp), b = timeit(sgs0), c = timeit(sgs1);
-    printf("round %d: k_sgp %.3f ms (K %d products, b sum included)  k_sgs %.3f ms without the b sum (%.3f)  %.3f ms with it (%.3f)\n",
-           r, a, K, b, b / a, c, c / a);
+    const float a = timeit(sgp), b = timeit(sgs0), c = timeit(sgs1), d = timeit(sgs2);
+    printf("round %d: k_sgp %.3f ms (K %d products, b sum included)  k_sgs %.3f ms without the b sum (%.3f)  %.3f ms with "
+           "it in global memory (%.3f)  k_sgs2 %.3f ms with it in registers (%.3f)\n",
+           r, a, K, b, b / a, c, c / a, d, d / a);
     fflush(stdout);
   }
   hipError_t err = hipDeviceSynchronize();

@@ -46,6 +46,7 @@ static const char* xcheck_env(const char* name) {
 #include "engine_pe.hpp"
 #include "engine_pfb.hpp"
 #include "engine_sgp.hpp"
+#include "engine_sgs.hpp"
 #include "engine_grp.hpp"
 #include "engine_mul.hpp"
 
@@ -140,6 +141,7 @@ struct pai_ctx {
   FbgpHalf* d_fbgp_halves = nullptr;  // 4096-bit keys: pair-group tables (kernels_grp_pair.hpp)
   bool fb_gpair = false;
   SgpHalf* d_sgp_fb = nullptr;  // 4096-bit keys: the split-pair sampler over the same tables (kernels_sgp.hpp)
+  SgsHalf* d_sgs_fb = nullptr;  //   ... on Shoup rows ($FLEXPAI_SGS=1, kernels_sgs.hpp)
   const uint32_t* d_sgp_q = nullptr;   //   q's S limbs (k_sgp_fin)
   FbRed* d_fb_red = nullptr;
   uint32_t *d_fb_m8 = nullptr, *d_fb_coefR = nullptr, *d_fb_q2 = nullptr, *d_fb_m0 = nullptr;
@@ -914,6 +916,13 @@ static bool sgp_enabled() {
   const char* e = xcheck_env("FLEXPAI_SGP");
   return !e || atoi(e) != 0;
 }
+// Shoup rows for the 4096-bit key holder's split-pair sampler (kernels_sgs.hpp): opt-in, $FLEXPAI_SGS=1, in every
+// build. Their 640-B rows sit beside the factored rows (whose b halves they keep using), so the tables' window is
+// chosen for both (fb_bytes): W = 20 at nb = 4096 on a 288-GB device.
+static bool sgs_enabled() {
+  const char* e = getenv("FLEXPAI_SGS");
+  return e && atoi(e) != 0;
+}
 // Garner's last step on lanes (k_sgp_fin); the test build's $FLEXPAI_SGP_FIN=0 keeps the group kernel k_fbg_fin
 static bool sgp_fin_enabled() {
   const char* e = xcheck_env("FLEXPAI_SGP_FIN");
@@ -937,6 +946,65 @@ static int sgp_make_half(const HBig& P, const HBig& w, int K, const void* table,
       (rc = up(nmc, &dnmc)) || (rc = up(mul(P, pow2(20)).limbs(SGP_S, LB), &dpb)))
     return rc;
   *out = SgpHalf{(const uint4*)table, dp, dca, dcb, dnmc, dpb, mont_prime(P, LB)};
+  return 0;
+}
+
+// The Shoup rows of both halves from their factored rows t[h] (kernels_sgs.hpp k_sgs_conv) and the constants of
+// k_sgs_bfin: w 2^(16 c) R mod P (R = 2^(28 FBGP_S), the b rows' radix; w = the other prime) and mu = floor(2^(56 S) / P).
+// A failed allocation leaves the Montgomery sampler in place (returns 0, d_sgs_fb unset).
+template <class Ctx>
+static int sgs_build(Ctx* c, const HBig* primes, int K, int W, void* const* t, const SgpHalf* sv) {
+  SgsHalf sh[2];
+  uint4* at[2] = {nullptr, nullptr};
+  const size_t rows = (size_t)K << W;
+  for (int h = 0; h < 2; ++h) {
+    const HBig& P = primes[h];
+    std::vector<uint32_t> nmr;
+    for (int k = 0; k < 4; ++k) {
+      const std::vector<uint32_t> v = mul_pow2_mod(mod(primes[1 - h], P), (size_t)16 * k + (size_t)LB * FBGP_S, P).limbs(SGP_S, LB);
+      nmr.insert(nmr.end(), v.begin(), v.end());
+    }
+    const HBig mu = div_big(pow2((size_t)2 * LB * SGP_S), P);
+    if (mu.bits() > (size_t)LB * (SGP_S + 1)) return fail(PAI_ERR_KEY, "Shoup rows: mu exceeds S + 1 limbs");
+    // R^-K mod P^2 = c_A (1 + P beta): the rows' Montgomery factor R = 2^(28 FBGP_S), once per row product
+    const HBig P2 = mul(P, P);
+    const HBig Ci = inv_mod(mul_pow2_mod(HBig(1), (size_t)LB * FBGP_S * K, P2), P2);
+    if (Ci.is_zero()) return fail(PAI_ERR_KEY, "Shoup rows: 2 not invertible mod P^2");
+    const HBig cB = div_big(Ci, P), cA = sub(Ci, mul(cB, P));
+    const HBig cAi = inv_mod(cA, P);
+    if (cAi.is_zero()) return fail(PAI_ERR_KEY, "Shoup rows: c_A not invertible");
+    // the pass multiplies by the integer y = c_A R' mod P, and y R'^-1 = c_A (1 + P delta)^-1 mod P^2 with Y = c_A R'
+    // mod P^2 = y (1 + P delta): delta joins the b sum with beta
+    const HBig Y = mul_pow2_mod(cA, (size_t)LB * SGP_S, P2);
+    const HBig yB = div_big(Y, P), y = sub(Y, mul(yB, P));
+    const HBig yi = inv_mod(y, P);
+    if (yi.is_zero()) return fail(PAI_ERR_KEY, "Shoup rows: y not invertible");
+    const HBig delta = mod(mul(yB, yi), P);
+    const HBig beta = mod(add(mul(cB, cAi), delta), P);
+    uint32_t *dn, *dmu, *dcy, *dbr;
+    int rc;
+    if ((rc = upload_fb(c, nmr, &dn)) || (rc = upload_fb(c, mu.limbs(SGP_S + 2, LB), &dmu)) ||
+        (rc = upload_fb(c, y.words(FBGP_PW), &dcy)) ||
+        (rc = upload_fb(c, mul_pow2_mod(beta, (size_t)LB * FBGP_S, P).limbs(SGP_S, LB), &dbr)))
+      return rc;
+    if (hipMalloc((void**)&at[h], rows * SGS_ROW_Q * sizeof(uint4)) != hipSuccess) {
+      (void)hipGetLastError();
+      if (h == 1) {
+        c->fb_mem.erase(std::find(c->fb_mem.begin(), c->fb_mem.end(), (void*)at[0]));
+        (void)hipFree(at[0]);
+      }
+      return 0;
+    }
+    c->fb_mem.push_back(at[h]);
+    sh[h] = SgsHalf{at[h], (const uint4*)t[h], sv[h].p, dn, sv[h].pbig, dmu, dcy, dbr, sv[h].mprime};
+  }
+  SgsHalf* d = nullptr;
+  std::vector<SgsHalf> shv(sh, sh + 2);
+  int rc;
+  if ((rc = upload_fb(c, shv, &d))) return rc;
+  if (sgs_launch_conv(d, rows, at[0], at[1], nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    return fail(PAI_ERR_HIP, "Shoup row conversion failed");
+  c->d_sgs_fb = d;
   return 0;
 }
 
@@ -1031,7 +1099,8 @@ static int fb_digit_count(const pai_ctx* c, int W) {
 }
 
 static uint64_t fb_bytes(const pai_ctx* c, int W) {
-  return 2ull * (uint64_t)fb_digit_count(c, W) * (1ull << W) * (uint64_t)fb_table_row_words(c) * 4ull;
+  const uint64_t sgs = fb_gpair_possible(c) && sgp_enabled() && sgs_enabled() ? 4ull * SGS_ROW_Q : 0ull;   // Shoup rows beside
+  return 2ull * (uint64_t)fb_digit_count(c, W) * (1ull << W) * ((uint64_t)fb_table_row_words(c) + sgs) * 4ull;
 }
 
 // Budget for the two tables: $FLEXPAI_FB_MAX_BYTES, else the free device memory less a reserve of
@@ -1087,6 +1156,7 @@ static void fb_release(pai_ctx* c) {
   c->d_fbgp_halves = nullptr;
   c->fb_gpair = false;
   c->d_sgp_fb = nullptr;
+  c->d_sgs_fb = nullptr;
   c->d_fb_red = nullptr;
 }
 
@@ -1473,6 +1543,10 @@ static int ensure_fb(pai_ctx* c) {
   for (void* p : fb_scratch) {
     c->fb_mem.erase(std::find(c->fb_mem.begin(), c->fb_mem.end(), p));
     (void)hipFree(p);
+  }
+  if (gpair_ok && sgp_enabled() && sgs_enabled()) {
+    SetupTrace tr_s("  Shoup rows (k_sgs_conv)");
+    if ((rc = sgs_build(c, primes, K, W, t, sv))) return fb_unavailable(c, pai_last_error());
   }
   const auto t2 = std::chrono::steady_clock::now();
   c->fb_host_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
@@ -1865,7 +1939,8 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
     case PAI_OPT_SPLIT_SAMPLER:
       *value = (c->fb_state == pai_ctx::FB_READY && c->d_sgp_fb ? 1 : 0) |
                (c->pfb_state == pai_ctx::FB_READY && c->d_sgp_pfb ? 2 : 0) |
-               (c->fb_state == pai_ctx::FB_READY && c->fb_shoup ? 4 : 0);
+               (c->fb_state == pai_ctx::FB_READY && c->fb_shoup ? 4 : 0) |
+               (c->fb_state == pai_ctx::FB_READY && c->d_sgs_fb ? 8 : 0);
       return 0;
     case PAI_OPT_PAIR:
       *value = ((c->dec_pair_ok || c->dec4_ok) && c->dec_lane_enabled ? 1 : 0) | (c->crt_pair_ok ? 2 : 0) |
@@ -2028,9 +2103,16 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
   const int gxG = (int)std::max<long long>(1, std::min<long long>(lane_blocks, (long long)occG * c->cus));
   const size_t dbytes = (size_t)2 * c->fb_K * 4, wbytes = (size_t)2 * std::max(SB, 2 * c->fb_pair_s) * 4;   // per element
   int rc;
-  if ((rc = ensure_work(c, dbytes * chunk + wbytes * (size_t)fbp_npad(chunk)))) return rc;   // pairs: 64-element tiles
+  const size_t sbytes = c->d_sgs_fb ? (size_t)2 * (16 * sizeof(uint4) + 2 * 4) : 0;   // k_sgs's b sums
+  if ((rc = ensure_work(c, dbytes * chunk + wbytes * (size_t)fbp_npad(chunk) + sbytes * chunk))) return rc;   // pairs: 64-element tiles
   uint32_t* digits = (uint32_t*)c->d_work;
   uint32_t* w = (uint32_t*)((char*)c->d_work + dbytes * chunk);
+  uint4* sgs_bsum = (uint4*)((char*)w + wbytes * (size_t)fbp_npad(chunk));
+  int dbg_stage = 0;   // test build: $FLEXPAI_DEBUG_SGS_STAGE = 1 stops after k_sgs, 2 after the b sums (or k_sgp)
+#if FLEXPAI_XCHECK
+  if (const char* ds = getenv("FLEXPAI_DEBUG_SGS_STAGE")) dbg_stage = atoi(ds);
+#endif
+  uint32_t* sgs_bcc = (uint32_t*)(sgs_bsum + (size_t)2 * 16 * chunk);
   const size_t esz = e.dtype == PAI_F32 ? 4 : 8;
   for (long long off = 0; off < N; off += chunk) {
     const long long n = std::min(chunk, N - off);
@@ -2081,7 +2163,17 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
       if (c->fb_shoup) HIPCHK(fbs_launch(c->fb_pair_s, pp, gF, st));
     } else if (grp && c->fb_gpair) {
       const FbgpParams pg{c->d_fbgp_halves, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
-      if (c->d_sgp_fb) {   // split pairs (kernels_sgp.hpp): SGP_PAIRS elements per block, grid (gx, 2)
+      if (c->d_sgs_fb) {   // split pairs on Shoup rows (kernels_sgs.hpp), then the b sums applied
+        int occS = 1;
+        sgs_occupancy(&occS);
+        SgsParams sp{c->d_sgs_fb, n, pf.K, pf.W, digits, w, sgs_bsum, sgs_bcc};
+        sp.g = guard_args(c, (unsigned long long)pf.K << pf.W, dig_words, w_words, 0);
+        const long long nb = (n + SGP_PAIRS - 1) / SGP_PAIRS;
+        HIPCHK(sgs_launch(sp, (int)std::max<long long>(1, std::min<long long>(nb, (long long)occS * c->cus / 2)), 2, st));
+        const SgsFinParams sf{c->d_sgs_fb, n, w, sgs_bsum, sgs_bcc, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status,
+                              dbg_stage};
+        if (dbg_stage != 1) HIPCHK(sgs_launch_bfin(sf, 2, c->cus, st));
+      } else if (c->d_sgp_fb) {   // split pairs (kernels_sgp.hpp): SGP_PAIRS elements per block, grid (gx, 2)
         int occS = 1;
         sgp_occupancy(&occS);
         SgpParams sp{c->d_sgp_fb, n, pf.K, pf.W, digits, w, pf.x, pf.dtype, pf.exp_mode, pf.fexp, pf.exp, pf.status};
@@ -2101,6 +2193,7 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
     stage_mark(c, 2, st);
     c->fb_last_w = w;
     c->fb_last_n = n;
+    if (dbg_stage) continue;
     if (grp) {   // w_h = c0 G_h^(a_h) mod p_h^2 -> Garner: h mod p^2 (S = 148), c = w_q + q^2 h mod n^2 (S = 296)
       int occH = 1, occC = 1;
       grp_fin_occupancy(&occH, &occC);

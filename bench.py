@@ -151,6 +151,14 @@ def work_fbgp(nb: int, digits: int) -> dict:
             "k_fbg_fin": float(2 * _M(nb // 32) + _M(nb // 32) + _M(nb // 16))}
 
 
+def work_sgs(nb: int, digits: int) -> float:
+    """The 4096-bit sampler on Shoup rows ($FLEXPAI_SGS=1, kernels_sgs.hpp): K - 1 Shoup products per half (3 s^2 + 3 s
+    over the nb/64 32-bit limbs of p_h, as k_fbs's count) and k_sgs_bfin's split pass by the constant c_A (4 s^2 + 2 s)
+    and b-sum product M(s)."""
+    s = nb // 64
+    return float(2 * ((digits - 1) * (3 * s * s + 3 * s) + _Mf(s) + _M(s)))
+
+
 def work_sgp_fin(nb: int) -> float:
     """The 4096-bit split-pair path's fin stage (round 5): k_sgp_w's plain product p_h B per half ((nb/64)^2 each),
     k_fbg_garner's product mod p^2 (M(nb/32)) and k_sgp_fin's two plain products by q (q h: (nb/64)(nb/32), q t:
@@ -186,14 +194,23 @@ def work_add(exps: "torch.Tensor", nb: int) -> float:
 
 
 # ------------------------------------------------------------- per-rank HBM plan
-FB_ROW_BYTES = {1024: 224, 2048: 448, 4096: 512}   # Shoup rows (k_fbs) at 1024/2048, factored word rows (k_sgp) at 4096
+FB_ROW_BYTES = {1024: 224, 2048: 448, 4096: 512}   # Shoup rows (k_fbs) at 1024/2048, factored word rows at 4096 (+ 640-B
+                                                    # Shoup rows beside them for k_sgs, fb_table_bytes)
 FB_WINDOWS = (24, 23, 22, 21, 20, 16, 12, 8)        # the library's ladder (flexpai.hip ensure_fb)
 GiB = 1 << 30
 
 
+def sgs_enabled() -> bool:
+    """The 4096-bit key holder's Shoup-row sampler (kernels_sgs.hpp; off with $FLEXPAI_SGS=0), whose 640-B rows sit
+    beside the factored rows: at the windows a dedicated MI355X allows the library takes them (flexpai.hip fb_choose:
+    W = 20 with them prices below W = 21 without)."""
+    return os.environ.get("FLEXPAI_SGS", "") != "0"
+
+
 def fb_table_bytes(nb: int, w: int) -> int:
     """Both halves' fixed-base tables at window w: 2 x K x 2^w rows, K = ceil(bits(p_h - 1) / w) (fb_digit_count)."""
-    return 2 * (-(-(nb // 2) // w)) * (1 << w) * FB_ROW_BYTES[nb]
+    row = FB_ROW_BYTES[nb] + (640 if nb == 4096 and sgs_enabled() else 0)
+    return 2 * (-(-(nb // 2) // w)) * (1 << w) * row
 
 
 def fb_reserve(device_bytes: int) -> int:
@@ -210,6 +227,8 @@ def rank_memory_plan(cfg_id: int, world: int, nb: int, strong_leg: bool = True) 
     K = -(-(nb // 2) // 16)                  # digits per half at the smallest window the legs might see (upper bound)
     S2 = 2 * (nb // 64 + 5)                  # words of a pair (2 S limbs) per half, rounded up
     work = 2 * K * 4 + 2 * S2 * 4            # library work per element of a chunk: digits + pairs
+    if nb == 4096 and sgs_enabled():
+        work += 2 * (16 * 16 + 2 * 4)        # + k_sgs's b sums
     dec = 8 + 4 + 2 * 2 * S2 * 4             # decrypt check: value + status + the library's pair outputs
 
     def leg(total, shard):
@@ -500,6 +519,7 @@ def main():
     fb_info = None
     fb_pair = 0
     fb_split = False
+    fb_sgs = False
     fb_shoup = False
     if use_fb:
         ctx.set_fb_window(args.fb_window)     # a dedicated encrypt GPU: the largest tables that fit its HBM
@@ -523,6 +543,7 @@ def main():
         fb_pair = ctx.fb_pair if use_fb else 0
         fb_split = bool(ctx.split_sampler & 1) if use_fb else False   # k_sgp (kernels_sgp.hpp) for k_fbgp
         fb_shoup = bool(ctx.split_sampler & 4) if use_fb else False   # k_fbs (kernels_fbs.hpp) for k_fbp
+        fb_sgs = bool(ctx.split_sampler & 8) if use_fb else False     # k_sgs (kernels_sgs.hpp, $FLEXPAI_SGS=1) for k_sgp
         if use_fb:
             fb_info = ctx.fixed_base_info()
             h_ms, d_ms, tbytes = ctx.fixed_base_setup()
@@ -1170,6 +1191,10 @@ def main():
                 names[2] = "k_sgp_w+garner+fin"
                 works.pop("k_fbg_fin")
                 works[names[2]] = work_sgp_fin(nb)
+                if fb_sgs:   # Shoup rows: k_sgs + k_sgs_bfin in the sampler stage
+                    names[1] = "k_sgs+bfin"
+                    works.pop("k_sgp")
+                    works["k_sgs+bfin"] = work_sgs(nb, fb_info[2])
         elif grp_fb:
             names, works = ["k_fb_digits", "k_fbg", "k_fbg_fin"], work_fbg(nb, fb_info[2])
         elif use_crt and use_fb and fb_pair and fb_shoup:

@@ -916,12 +916,15 @@ static bool sgp_enabled() {
   const char* e = xcheck_env("FLEXPAI_SGP");
   return !e || atoi(e) != 0;
 }
-// Shoup rows for the 4096-bit key holder's split-pair sampler (kernels_sgs.hpp): opt-in, $FLEXPAI_SGS=1, in every
-// build. Their 640-B rows sit beside the factored rows (whose b halves they keep using), so the tables' window is
-// chosen for both (fb_bytes): W = 20 at nb = 4096 on a 288-GB device.
-static bool sgs_enabled() {
+// Shoup rows for the 4096-bit key holder's split-pair sampler (kernels_sgs.hpp). Their 640-B rows sit beside the
+// factored rows (whose b halves they keep using): 1152 B per entry against 512, so they fit one window lower (W = 20
+// at nb = 4096 on a 288-GB device, 249 GB, against the factored rows' W = 21, 205 GB). fb_choose takes them when the
+// product count at their window, priced at the measured 0.835 of a Montgomery row product
+// (profiles/r05_ab_sgs_prototype_stream.txt), is below the factored rows' at theirs. $FLEXPAI_SGS=0 never takes them,
+// $FLEXPAI_SGS=1 whenever they fit.
+static int sgs_mode() {
   const char* e = getenv("FLEXPAI_SGS");
-  return e && atoi(e) != 0;
+  return !e || !*e ? -1 : atoi(e) != 0 ? 1 : 0;
 }
 // Garner's last step on lanes (k_sgp_fin); the test build's $FLEXPAI_SGP_FIN=0 keeps the group kernel k_fbg_fin
 static bool sgp_fin_enabled() {
@@ -1098,9 +1101,29 @@ static int fb_digit_count(const pai_ctx* c, int W) {
   return (int)((kb + W - 1) / W);
 }
 
-static uint64_t fb_bytes(const pai_ctx* c, int W) {
-  const uint64_t sgs = fb_gpair_possible(c) && sgp_enabled() && sgs_enabled() ? 4ull * SGS_ROW_Q : 0ull;   // Shoup rows beside
-  return 2ull * (uint64_t)fb_digit_count(c, W) * (1ull << W) * ((uint64_t)fb_table_row_words(c) + sgs) * 4ull;
+static uint64_t fb_bytes(const pai_ctx* c, int W, bool sgs = false) {
+  return 2ull * (uint64_t)fb_digit_count(c, W) * (1ull << W) * ((uint64_t)fb_table_row_words(c) + (sgs ? 4ull * SGS_ROW_Q : 0ull)) *
+         4ull;
+}
+
+// The window of the tables (<= c->fb_W, within budget) and whether Shoup rows join them (sgs_mode, above)
+static int fb_choose(const pai_ctx* c, uint64_t budget, bool* sgs) {
+  static const int ladder[] = {24, 23, 22, 21, 20, 16, 12, 8};
+  int wm = 0, ws = 0;
+  for (int w : ladder)
+    if (w <= c->fb_W && fb_bytes(c, w) <= budget) {
+      wm = w;
+      break;
+    }
+  const int mode = sgs_mode();
+  if (mode != 0 && fb_gpair_possible(c) && sgp_enabled())
+    for (int w : ladder)
+      if (w <= c->fb_W && fb_bytes(c, w, true) <= budget) {
+        ws = w;
+        break;
+      }
+  *sgs = ws && (mode == 1 || (wm && 0.835 * fb_digit_count(c, ws) < (double)fb_digit_count(c, wm)));
+  return *sgs ? ws : wm;
 }
 
 // Budget for the two tables: $FLEXPAI_FB_MAX_BYTES, else the free device memory less a reserve of
@@ -1232,12 +1255,8 @@ static int ensure_fb(pai_ctx* c) {
     return fb_unavailable(c, "unbalanced primes: p^2 or q^2 exceeds the table row");
   if (!c->fb_W) c->fb_W = fb_default_window();
   const uint64_t budget = fb_budget(c);
-  int W = 0;
-  for (int w : {24, 23, 22, 21, 20, 16, 12, 8})
-    if (w <= c->fb_W && fb_bytes(c, w) <= budget) {
-      W = w;
-      break;
-    }
+  bool sgs = false;
+  const int W = fb_choose(c, budget, &sgs);
   if (!W) return fb_unavailable(c, "tables do not fit the device memory budget");
   SetupTrace tr_all("ensure_fb");
   const auto t0 = std::chrono::steady_clock::now();
@@ -1544,14 +1563,14 @@ static int ensure_fb(pai_ctx* c) {
     c->fb_mem.erase(std::find(c->fb_mem.begin(), c->fb_mem.end(), p));
     (void)hipFree(p);
   }
-  if (gpair_ok && sgp_enabled() && sgs_enabled()) {
+  if (gpair_ok && sgp_enabled() && sgs) {
     SetupTrace tr_s("  Shoup rows (k_sgs_conv)");
     if ((rc = sgs_build(c, primes, K, W, t, sv))) return fb_unavailable(c, pai_last_error());
   }
   const auto t2 = std::chrono::steady_clock::now();
   c->fb_host_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
   c->fb_dev_ms = std::chrono::duration<float, std::milli>(t2 - t1).count();
-  c->fb_table_bytes = fb_bytes(c, W);
+  c->fb_table_bytes = fb_bytes(c, W, c->d_sgs_fb != nullptr);
   c->fb_K = K;
   c->fb_pair_s = pair_ok ? ps : 0;
   c->fb_shoup = shoup;
@@ -2001,10 +2020,9 @@ static long long fb_threshold(pai_ctx* c) {
   const int TW = fb_row_words(c);
   if (!TW) return 0;
   if (!c->fb_W) c->fb_W = fb_default_window();
-  const uint64_t budget = fb_budget(c);
-  for (int w : {24, 23, 22, 21, 20, 16, 12, 8})
-    if (w <= c->fb_W && fb_bytes(c, w) <= budget) return fb_break_even(c, w, fb_digit_count(c, w), 4 * fb_table_row_words(c));
-  return 0;
+  bool sgs = false;
+  const int w = fb_choose(c, fb_budget(c), &sgs);
+  return w ? fb_break_even(c, w, fb_digit_count(c, w), 4 * fb_table_row_words(c) + (sgs ? 16 * SGS_ROW_Q : 0)) : 0;
 }
 
 static bool fb_wanted(pai_ctx* c, long long n) {

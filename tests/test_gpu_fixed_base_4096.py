@@ -48,14 +48,18 @@ def test_fixed_base_4096_params(ctx4096):
     assert (gp, gq) == (O.fb_base(key.p), O.fb_base(key.q))
     assert W == 12 and K == O.fb_digits(key.p, key.q, W)
     _, _, nbytes = ctx.fixed_base_setup()
-    assert nbytes == 2 * K * (1 << W) * 128 * 4          # rows: the canonical pair as 2 x 64 32-bit words
+    # rows: the canonical pair as 2 x 64 32-bit words (+ 640-B Shoup rows for k_sgs, the default at this window)
+    assert nbytes == 2 * K * (1 << W) * (128 * 4 + (640 if ctx.split_sampler & 8 else 0))
 
 
 @pytest.mark.parametrize("window", [12, 16, 21])
-def test_fixed_base_4096_matches_reference_goldens(ctx4096, golden_fb, window):
-    """W = 21 is the configs[4] bench window (98 digits per half, the largest whose tables fit one MI355X)."""
+def test_fixed_base_4096_matches_reference_goldens(ctx4096, golden_fb, window, monkeypatch):
+    """W = 21: the factored rows' largest window on one MI355X (98 digits per half), on k_sgp ($FLEXPAI_SGS=0: Shoup
+    rows beside them fit only W <= 20); W = 12, 16 on the default sampler."""
     N = _native()
     ctx, key = ctx4096
+    if window == 21:
+        monkeypatch.setenv("FLEXPAI_SGS", "0")
     g = golden_fb["keys"][str(NB)]
     assert (hex(key.n), hex(key.p), hex(key.q)) == (g["n"], g["p"], g["q"])
     recs = golden_fb["encrypt"][str(NB)]

@@ -1,8 +1,9 @@
 """GPU parity of the Shoup-row split-pair sampler for 4096-bit keys (kernels_sgs.hpp: k_sgs_conv, k_sgs, k_sgs_bfin;
-opt-in, $FLEXPAI_SGS=1), VERDICT r4 item 3, reference semantics /root/reference/flex/crypto/paillier/obfuscator.py:36
+the default where it prices below the factored rows, flexpai.hip fb_choose; $FLEXPAI_SGS=0 keeps k_sgp), VERDICT r4
+item 3, reference semantics /root/reference/flex/crypto/paillier/obfuscator.py:36
 (r^n mod n^2 with the sampler's r):
 
-* the same ciphertexts and exponents as the Montgomery sampler (k_sgp, the default) from the same digits, at ragged
+* the same ciphertexts and exponents as the Montgomery sampler (k_sgp, $FLEXPAI_SGS=0) from the same digits, at ragged
   counts (one element leaves 127 of a block's lane pairs clamped) and a non-zero index base;
 * bit-exact against THE REFERENCE's own 4096-bit ciphertexts under the sampler's obfuscator
   (tests/golden/paillier_golden_fb.json) at W = 12 and 16;
@@ -29,10 +30,7 @@ def _key(golden):
 
 def _encrypt(key, x, window, sgs, monkeypatch, lib=None, base=7):
     N = _native()
-    if sgs:
-        monkeypatch.setenv("FLEXPAI_SGS", "1")
-    else:
-        monkeypatch.delenv("FLEXPAI_SGS", raising=False)
+    monkeypatch.setenv("FLEXPAI_SGS", "1" if sgs else "0")
     ctx = N.Context(key.n, 0, key.p, key.q, lib=lib) if lib is not None else N.Context(key.n, 0, key.p, key.q)
     try:
         ctx.set_fb_window(window)
@@ -90,3 +88,28 @@ def test_shoup_sampler_guarded(golden, monkeypatch, xlib, count):
     ca, ea = _encrypt(key, x, 8, True, monkeypatch, lib=xlib)
     cb, eb = _encrypt(key, x, 8, False, monkeypatch)
     assert np.array_equal(ea, eb) and np.array_equal(ca, cb)
+
+
+def test_shoup_rows_are_the_default_where_they_price_lower(golden, monkeypatch):
+    """fb_choose: at W = 12 both tables fit, and 0.835 K(12) < K(12): Shoup rows without $FLEXPAI_SGS; with a budget
+    that fits only the factored rows, k_sgp."""
+    N = _native()
+    key = _key(golden)
+    monkeypatch.delenv("FLEXPAI_SGS", raising=False)
+    ctx = N.Context(key.n, 0, key.p, key.q)
+    try:
+        ctx.set_fb_window(12)
+        ctx.prepare_fixed_base()
+        assert ctx.split_sampler & 8
+        K, W = ctx.fixed_base_info()[2:]
+        assert W == 12 and ctx.fixed_base_setup()[2] == 2 * K * (1 << W) * (512 + 640)
+    finally:
+        ctx.close()
+    monkeypatch.setenv("FLEXPAI_FB_MAX_BYTES", str(2 * 171 * (1 << 12) * 512 + 1000))
+    ctx = N.Context(key.n, 0, key.p, key.q)
+    try:
+        ctx.set_fb_window(12)
+        ctx.prepare_fixed_base()
+        assert ctx.fb_ready and not ctx.split_sampler & 8 and ctx.fixed_base_info()[3] == 12
+    finally:
+        ctx.close()

@@ -1,4 +1,5 @@
-// Host interface of the Shoup-row split-pair sampler (engine_sgs.hip, kernels_sgs.hpp; opt-in, $FLEXPAI_SGS=1).
+// Host interface of the Shoup-row split-pair sampler (engine_sgs.hip, kernels_sgs.hpp; the default where it prices
+// lower, flexpai.hip fb_choose).
 #pragma once
 #include "kernels_sgs.hpp"
 

@@ -1,5 +1,6 @@
-// Split-pair fixed-base sampler on Shoup rows (round 5; opt-in, $FLEXPAI_SGS=1): kernels_sgp.hpp's
-// lane-pair layout -- element-half e on lanes 2e, 2e+1, the even lane keeps A, the odd lane B, V = A + m B mod m^2 --
+// Split-pair fixed-base sampler on Shoup rows (round 5; the default where it prices lower,
+// flexpai.hip fb_choose; $FLEXPAI_SGS=0 keeps k_sgp): kernels_sgp.hpp's lane-pair layout -- element-half e on lanes
+// 2e, 2e+1, the even lane keeps A, the odd lane B, V = A + m B mod m^2 --
 // with each product by a row (a, 0) done as kernels_fbs.hpp's Shoup product instead of a Montgomery split pass, at
 // S = 74 (the 2048-bit p_h of a 4096-bit key):
 //   step 1: Q = floor(X a' / R), R = 2^(28 S), from the columns >= S - 1 of X a' (Q at most S + 1 below the floor);
@@ -307,7 +308,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_sgs(SgsParams p) {
 // A mod m (its multiples t of m into B), z = REDC'(A bs) 2^-56 = A bs mod m (< 2 m, the pass's R' = 2^(28 S) against
 // the rows' R = 2^(28 76)), B + t + z to B mod m. Out: A < m, B < m.
 template <int S>
-__global__ __launch_bounds__(LANE_BLOCK, 1) void k_sgs_bfin(SgsFinParams p) {
+__global__ __launch_bounds__(LANE_BLOCK, 2) void k_sgs_bfin(SgsFinParams p) {
   __shared__ __attribute__((aligned(16))) uint32_t bsum[SGP_PAIRS * SGP_BW];
   __shared__ uint32_t cyl[FBGP_PW];
   const int half = blockIdx.y;
@@ -356,42 +357,62 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_sgs_bfin(SgsFinParams p) {
         bs[w] = (uint32_t)v;
         c = v >> 32;
       }
-      // + gamma R (sum_c nmr_c |M|_c, or 2^20 m minus that for M < 0) + (beta + delta) R, limb by limb into the words:
-      // running carries, no limb arrays (they had cost 180 spilled VGPRs)
       const bool neg = M < 0;
       const uint64_t mag = neg ? (uint64_t)0 - (uint64_t)M : (uint64_t)M;
       const uint32_t* nmr = opaque_uniform(H->nmr);
       const uint32_t* pbg = opaque_uniform(H->pbig);
-      const uint32_t* br = opaque_uniform(H->bR);
-      const uint32_t ch0 = (uint32_t)mag & 0xFFFFu, ch1 = (uint32_t)(mag >> 16) & 0xFFFFu, ch2 = (uint32_t)(mag >> 32) & 0xFFFFu,
-                     ch3 = (uint32_t)(mag >> 48) & 0xFFFFu;
-      uint64_t cs = 0;   // carry of the chunk sum
-      int64_t cg = 0;    // carry of gamma R's signed form
-      uint64_t acc = 0, cw = 0;
-      int have = 0, w = 0;
-#pragma unroll 1
-      for (int i = 0; i < S; ++i) {   // (not unrolled: all 4 S loads would be hoisted and held)
-        const uint64_t v = (uint64_t)nmr[i] * ch0 + (uint64_t)nmr[S + i] * ch1 + (uint64_t)nmr[2 * S + i] * ch2 +
-                           (uint64_t)nmr[3 * S + i] * ch3 + cs;
-        cs = v >> LB;
-        const int64_t gv = (neg ? (int64_t)pbg[i] - (int64_t)(v & LMASK) : (int64_t)(v & LMASK)) + (int64_t)br[i] + cg;
-        cg = gv >> LB;   // (arithmetic: -1, 0 or a small carry)
-        acc |= (uint64_t)((uint32_t)gv & LMASK) << have;
-        have += LB;
-        if (have >= 32) {
-          const uint64_t t = (uint64_t)bs[w] + (uint32_t)acc + cw;
-          bs[w] = (uint32_t)t;
-          cw = t >> 32;
-          acc >>= 32;
-          have -= 32;
-          ++w;
+      uint64_t P[S];
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        uint64_t v = 0;
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) v += (uint64_t)nmr[c4 * S + i] * ((uint32_t)(mag >> (16 * c4)) & 0xFFFFu);
+        P[i] = v;
+      }
+      uint32_t g[S], pb[S], D[S];
+      lane::normalize<S>(P, g);
+      if (neg) {
+#pragma unroll
+        for (int i = 0; i < S; ++i) pb[i] = pbg[i];
+        (void)lane::sub<S>(pb, g, D);
+#pragma unroll
+        for (int i = 0; i < S; ++i) g[i] = D[i];
+      }
+      {   // + beta R
+        const uint32_t* br = opaque_uniform(H->bR);
+        uint32_t cy = 0;
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+          const uint32_t v = g[i] + br[i] + cy;
+          g[i] = v & LMASK;
+          cy = v >> LB;
         }
       }
-      for (; w < SGP_BW; ++w) {   // (gamma R + (beta + delta) R < 2^(28 S): cs and cg end at 0)
-        const uint64_t t = (uint64_t)bs[w] + (uint32_t)acc + cw;
-        bs[w] = (uint32_t)t;
-        cw = t >> 32;
-        acc >>= 32;
+      // bs += g
+      {
+        // limbs -> words by a running 64-bit window: 28 bits in per limb, 32 out per word
+        uint64_t acc = 0;
+        int have = 0, w = 0;
+        uint64_t carry = 0;
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+          acc |= (uint64_t)g[i] << have;
+          have += LB;
+          if (have >= 32) {
+            const uint64_t v = (uint64_t)bs[w] + (uint32_t)acc + carry;
+            bs[w] = (uint32_t)v;
+            carry = v >> 32;
+            acc >>= 32;
+            have -= 32;
+            ++w;
+          }
+        }
+        for (; w < SGP_BW; ++w) {
+          const uint64_t v = (uint64_t)bs[w] + (uint32_t)acc + carry;
+          bs[w] = (uint32_t)v;
+          carry = v >> 32;
+          acc >>= 32;
+        }
       }
     }
     wave_lds_fence();

@@ -1335,12 +1335,18 @@ def main():
                    "world_size_seen": dist.get_world_size() if world > 1 else 1},
         "roofline": {"bound": "valu-int-mac", "achieved": achieved / 1e12, "peak": INT_MAC_PEAK / 1e12,
                      "unit": "TMAC/s", "frac": achieved / INT_MAC_PEAK,
-                     "traffic": load_traffic(dom, N, nb, fb_info[3] if (use_fb and dom in ("k_fb", "k_fbp", "k_fbs", "k_fbg", "k_fbgp", "k_sgp")) else None),
+                     "traffic": load_traffic("k_sgs" if dom == "k_sgs+bfin" else dom, N, nb,   # (k_sgs's launch: the rows)
+                                             fb_info[3] if (use_fb and dom in ("k_fb", "k_fbp", "k_fbs", "k_fbg", "k_fbgp", "k_sgp",
+                                                                               "k_sgs+bfin")) else None),
                      "kernel": dom, "kernel_ms": dom_ms,
                      "work_per_unit": (f"{dom_work:.4g} MAC per element: the Shoup-row count (K - 1 = {fb_info[2] - 1} Shoup products "
                                        f"mod p_h^2 per half (the first of K rows is the start), 3 s^2 + 3 s each over s = nb/64 32-bit limbs of p_h, + the c0 sum "
                                        f"and the b-sum correction, kernels_fbs.hpp), not SURVEY.md §8d's W_enc"
                                        if dom == "k_fbs" else
+                                       f"{dom_work:.4g} MAC per element: the Shoup-row count at nb = 4096 (K - 1 = {fb_info[2] - 1} Shoup "
+                                       f"products mod p_h^2 per half, 3 s^2 + 3 s each over s = nb/64 32-bit limbs of p_h, + k_sgs_bfin's "
+                                       f"pass by the constant c_A and b-sum product, kernels_sgs.hpp), not SURVEY.md §8d's W_enc"
+                                       if dom == "k_sgs+bfin" else
                                        f"{dom_work:.4g} MAC per element: the fixed-base count (K = {fb_info[2]} products by "
                                        f"factored rows (a, 0) mod p_h^2 per half, 4 s^2 + 2 s each over s = nb/64 32-bit limbs "
                                        f"of p_h, + the c0 sum and the b-sum correction, "

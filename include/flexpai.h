@@ -136,7 +136,10 @@ typedef struct pai_comm pai_comm;
                                   * $FLEXPAI_SGP=0 at table build selects k_fbgp / k_pfb); bit 2 = the resident
                                   * 1024/2048-bit key-holder tables hold Shoup rows sampled on split pairs
                                   * (kernels_fbs.hpp: k_fbs, the default; $FLEXPAI_FBS=0 in the test build keeps
-                                  * k_fbp's Montgomery rows)                                                   */
+                                  * k_fbp's Montgomery rows); bit 3 = the resident 4096-bit key-holder tables add
+                                  * Shoup rows (kernels_sgs.hpp: k_sgs, the default where they price lower than the
+                                  * factored rows at their window; $FLEXPAI_SGS=0 keeps k_sgp, =1 takes them
+                                  * whenever they fit)                                                        */
 
 /* Number of visible GPUs (0 when there is none or the runtime cannot start). */
 int pai_device_count(int* count);

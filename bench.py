@@ -395,6 +395,224 @@ def launch_ranks(n: int, argv) -> int:
     return rc
 
 
+# ------------------------------------------------------------- the timed step of the sharded legs
+def step_base(rank_base: int, stride: int, i: int) -> int:
+    """The obfuscator index base of step i: the rank's first global index + i x the job's elements per step, so that no
+    two steps of a run encrypt under the same obfuscators (nothing in the timed region could be served from a cache)
+    and the ciphertexts still do not depend on the number of ranks."""
+    return rank_base + i * stride
+
+
+def job_units(shard: str, total: int, world: int, n: int, steps: int) -> int:
+    """Elements of the whole job over `steps` steps: strong = the fixed total, weak = n per rank."""
+    return (total if shard == "strong" else world * n) * steps
+
+
+class ShardSteps:
+    """The step of configs[1]/[3]/[4] and of the configs[3] leg, the same code at every world size and on every backend.
+
+    Step i encrypts this rank's shard (`encrypt(out_words, out_exps, base)`, base = step_base(rank_base, stride, i))
+    into output buffer i % nbuf; at world > 1 it then starts the all-gather of that buffer's words and exponents into
+    the matching receive buffers (`gather_async(local, rows, world, out=recv) -> (view, work|None)`, sharding.
+    gather_shards_async: RCCL on the process group's stream on GPUs, gloo in the CPU tests). With two buffers step i's
+    gather runs while step i + 1 encrypts; a buffer is written again only after the gather that read it has completed
+    (the waits at the top of step). `rows` = world x the per-rank row count (the last shard is padded)."""
+
+    def __init__(self, encrypt, bufs, recv, world, rank_base, stride, gather_async=None):
+        if world > 1 and len(recv) != len(bufs):
+            raise ValueError("one receive pair per output buffer")
+        self.encrypt, self.bufs, self.recv, self.world = encrypt, bufs, recv, world
+        self.rank_base, self.stride, self.gather_async = rank_base, stride, gather_async
+        self.works = [[] for _ in bufs]
+        self.rows = bufs[0][0].shape[0] * world
+        self.last_i = None
+
+    def base(self, i: int) -> int:
+        return step_base(self.rank_base, self.stride, i)
+
+    def buffer(self, i: int) -> int:
+        return i % len(self.bufs)
+
+    def step(self, i: int) -> None:
+        b = self.buffer(i)
+        for w in self.works[b]:
+            w.wait()                         # the gather that last read this buffer is done
+        self.works[b] = []
+        self.encrypt(self.bufs[b][0], self.bufs[b][1], self.base(i))
+        if self.world > 1:
+            for t, o in zip(self.bufs[b], self.recv[b]):
+                _, w = self.gather_async(t, self.rows, self.world, out=o)
+                if w is not None:
+                    self.works[b].append(w)
+        self.last_i = i
+
+    def drain(self) -> None:
+        for b in range(len(self.bufs)):
+            for w in self.works[b]:
+                w.wait()
+            self.works[b] = []
+
+    def pending(self, b: int) -> int:
+        return len(self.works[b])
+
+    def last_output(self):
+        """(words, exponents) of the last step, and its receive pair at world > 1 (None at world 1)."""
+        b = self.buffer(self.last_i)
+        return self.bufs[b], (self.recv[b] if self.world > 1 else None)
+
+    def own_shard_identical(self, rank: int) -> bool:
+        """This rank's block of the last step's gathered arrays equals its own output (call after drain)."""
+        (ct, ex), rv = self.last_output()
+        n = ct.shape[0]
+        return all(bool(torch.equal(g[rank * n:(rank + 1) * n], t)) for g, t in zip(rv, (ct, ex)))
+
+
+def run_timed(stepper, steps: int, warmup: int, sync, barrier, max_over_ranks, after_step=None) -> float:
+    """`warmup` untimed steps, then exactly `steps` timed ones bracketed by drain + sync + barrier + sync on both sides;
+    returns the MAX over ranks of the timed region's wall time. Timed step i runs as stepper.step(warmup + i), so its
+    obfuscators differ from every warmup step's. after_step() (host bookkeeping, e.g. reading the stage events) runs
+    after each timed step."""
+    for i in range(warmup):
+        stepper.step(i)
+    stepper.drain()
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        stepper.step(warmup + i)
+        if after_step is not None:
+            after_step()
+    stepper.drain()
+    sync()
+    barrier()
+    sync()
+    return max_over_ranks(time.perf_counter() - t0)
+
+
+def nb1024_leg(args, dev, stream, lib, rng_key, x, local_rank, base, steps=5):
+    """configs[1]'s vector under a 1024-bit key -- the default of the factory (flex/crypto/paillier/api.py:22) and of
+    every Paillier protocol's sec_param.json (e.g. he_sa_ft/sec_param.json:3): the key holder's fixed-base encrypt
+    (k_fb_digits + k_fbs<19> + k_fbp_fin<19> at the largest window <= --fb-window that fits), its decryption
+    (k_dec_*_pair<19>) and the public-key per-element path, each with its dominant kernel's fraction of the MAC peak.
+    Returns (leg, check): check = what the cpu_baseline section compares with the GMP port and the oracle."""
+    from flex.crypto.paillier import _native
+    from flex.crypto.paillier.keypair import generate_paillier_keypair
+    nb1 = 1024
+    N = x.numel()
+    pk1, sk1 = generate_paillier_keypair(nb1, seed=1)
+    c1 = _native.Context(pk1.n, local_rank)
+    c1.set_private(sk1.p, sk1.q)
+    c1.set_crt(True)
+    c1.set_fixed_base(True)
+    c1.set_fb_window(args.fb_window)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    c1.prepare_fixed_base()
+    setup_ms = (time.perf_counter() - t0) * 1e3
+    c1.set_stage_timing(True)
+    fbi = c1.fixed_base_info()
+    W1 = c1.ct_words
+    ct = torch.empty((N, W1), dtype=torch.int32, device=dev)
+    ex = torch.empty(N, dtype=torch.int32, device=dev)
+    st = torch.empty(N, dtype=torch.int32, device=dev)
+
+    def enc(ctx, n, b, out=ct, exo=ex):
+        rc = lib.pai_encrypt_dev(ctx.handle, _native.PAI_F32, x.data_ptr(), n, 0, 0, _native.PAI_OBF_RNG, None, 0, 0,
+                                 rng_key, b, out.data_ptr(), exo.data_ptr(), st.data_ptr(), stream.cuda_stream)
+        if rc != 0:
+            raise RuntimeError(lib.pai_last_error().decode())
+
+    enc(c1, N, base)                                     # warmup
+    torch.cuda.synchronize()
+    stages = []
+    t0 = time.perf_counter()
+    for i in range(steps):
+        enc(c1, N, base + (i + 1) * N)
+        stages.append(c1.stage_times())
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    base_chk = base + steps * N                          # the last step's obfuscators
+    st_avg = [float(np.mean([s[i] for s in stages])) for i in range(len(stages[0]))]
+    wk = work_fbs(nb1, fbi[2])
+    names = ["k_fb_digits", "k_fbs", "k_fbp_fin"]
+    sdict = {nm: {"kernel_ms": ms, "work_mac_per_elem": wk[nm],
+                  "int_mac_frac": (N * wk[nm] / (ms * 1e-3) / INT_MAC_PEAK) if wk[nm] else None}
+             for nm, ms in zip(names, st_avg)}
+    leg = {"workload": "configs[1]'s 1M-element float32 vector under a 1024-bit key (the reference protocols' default)",
+           "key_bits": nb1, "elements": N,
+           "encrypt": {"value": N * steps / el, "unit": "encrypts/s", "steps": steps, "ms_per_step": el / steps * 1e3,
+                       "path": "key holder: k_fb_digits + k_fbs<19> (Shoup rows) + k_fbp_fin<19>",
+                       "window_bits": fbi[3], "digits": fbi[2], "stages": sdict,
+                       "roofline": {"kernel": "k_fbs", "frac": sdict["k_fbs"]["int_mac_frac"],
+                                    "work_per_unit": wk["k_fbs"], "peak_tmac_s": INT_MAC_PEAK / 1e12},
+                       "table_setup_ms": setup_ms, "table_bytes": c1.fixed_base_setup()[2]}}
+    # decryption of the last step's output, exact against the input
+    val = torch.empty(N, dtype=torch.float64, device=dev)
+    stt = torch.empty(N, dtype=torch.int32, device=dev)
+    d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for rep in range(2):                                 # the first call allocates the decrypt work buffers
+        d0.record(stream)
+        rc = lib.pai_decrypt_dev(c1.handle, ct.data_ptr(), ex.data_ptr(), N, val.data_ptr(), None, stt.data_ptr(), None,
+                                 stream.cuda_stream)
+        if rc != 0:
+            raise RuntimeError(lib.pai_last_error().decode())
+        d1.record(stream)
+        torch.cuda.synchronize()
+    dms = d0.elapsed_time(d1)
+    dst = c1.stage_times()
+    wd = work_dec_pair(nb1)
+    ok = bool(torch.equal(val, x.double())) and int((stt > 1).sum().item()) == 0
+    leg["decrypt"] = {"value": N / (dms * 1e-3), "unit": "decrypts/s", "kernel_ms": dms,
+                      "stages_ms": dict(zip(["k_dec_pre_pair", "k_dec_pow_pair", "k_dec_fin_pair"], dst)) if len(dst) == 3 else dst,
+                      "roofline": {"kernel": "k_dec_pow_pair", "work_per_unit": wd,
+                                   "frac": (N * wd / (dst[1] * 1e-3) / INT_MAC_PEAK) if len(dst) == 3 else None},
+                      "roundtrip_exact": ok}
+    if not ok:
+        raise SystemExit("nb = 1024: decrypt(encrypt(x)) != x")
+    # the generic CRT path on a prefix (bit-identical to the GMP port, checked in the cpu_baseline section) and the
+    # public-key per-element path on a larger prefix (bit-identical to CRT)
+    nchk = min(N, args.cpu_sample)
+    ctg = torch.empty((nchk, W1), dtype=torch.int32, device=dev)
+    exg = torch.empty(nchk, dtype=torch.int32, device=dev)
+    c1.set_fixed_base(False)
+    enc(c1, nchk, base_chk, ctg, exg)
+    c1.set_fixed_base(True)
+    npub = min(N, 1 << 18)
+    ctp = torch.empty((npub, W1), dtype=torch.int32, device=dev)
+    exp_ = torch.empty(npub, dtype=torch.int32, device=dev)
+    c1.set_crt(False)
+    c1.set_fixed_base(False)
+    c1.set_public_fixed_base(False)
+    enc(c1, npub, base_chk, ctp, exp_)                   # warmup (work buffers)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    enc(c1, npub, base_chk, ctp, exp_)
+    torch.cuda.synchronize()
+    tp = time.perf_counter() - t0
+    pst = c1.stage_times()
+    pe = bool(c1.pair_paths & 4) and len(pst) == 3
+    wpe = float((_P(nb1) + 1) * _Mp(nb1 // 32)) if pe else work_enc_public(nb1)
+    dom_ms = (pst[1] if pe else sum(pst)) if pst else tp * 1e3
+    same_pub = bool(torch.equal(ctp[:nchk], ctg)) and bool(torch.equal(exp_[:nchk], exg))
+    leg["public_key_path"] = {"value": npub / tp, "unit": "encrypts/s", "elements": npub,
+                              "kernel": "k_pe_pre + k_pe_pow + k_pe_fin" if pe else "k_encrypt", "stages_ms": pst,
+                              "roofline": {"kernel": "k_pe_pow" if pe else "k_encrypt", "work_per_unit": wpe,
+                                           "frac": npub * wpe / (dom_ms * 1e-3) / INT_MAC_PEAK},
+                              "bit_identical_to_crt_on_prefix": same_pub}
+    if not same_pub:
+        raise SystemExit("nb = 1024: public-key and CRT ciphertexts differ")
+    check = {"n": pk1.n, "p": sk1.p, "q": sk1.q, "base": base_chk, "fb_info": fbi, "pk": pk1,
+             "generic": (ctg.cpu().numpy().view(np.uint32).copy(), exg.cpu().numpy().copy()),
+             "fb_idx": sorted({0, 1, N // 2, N - 1}),
+             "fb_ct": ct[sorted({0, 1, N // 2, N - 1})].cpu().numpy().view(np.uint32).copy(),
+             "fb_ex": ex[sorted({0, 1, N // 2, N - 1})].cpu().numpy().copy()}
+    c1.close()
+    del c1, ct, ex, st, val, stt, ctg, exg, ctp, exp_
+    torch.cuda.empty_cache()
+    return leg, check
+
+
 def selftest_cpu(args) -> None:
     """The launcher's CPU self-test (tests/test_bench_launcher.py): gloo ranks, each contributes a shard
     of rank-stamped rows, one all-gather through sharding.gather_shards; rank 0 prints the world as the
@@ -459,6 +677,9 @@ def main():
     ap.add_argument("--strong-steps", type=int, default=3, help="timed steps of the configs[3] leg")
     ap.add_argument("--no-contention", action="store_true",
                     help="skip the one-GPU rehearsal of the N = 8 all-gather's HBM contention")
+    ap.add_argument("--no-nb1024", action="store_true",
+                    help="skip the nb = 1024 leg (configs[1]'s vector under a 1024-bit key: fixed-base encrypt, decrypt, "
+                         "public-key path)")
     ap.add_argument("--selftest-cpu", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -592,8 +813,20 @@ def main():
     extra = {}
     K8 = 8
     add_events = []
+    stride = job_units(cfg["shard"], total, world, N, 1)     # the job's elements per step (step_base)
+    sync = torch.cuda.synchronize
+    barrier = dist.barrier if world > 1 else (lambda: None)
+
+    def max_over_ranks(v):
+        if world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     if cfg_id == 2:
-        # ---- a step = the configs[2] pipeline: encrypt 8 arrays, one 8-way add, decrypt the sum
+        # ---- a step = the configs[2] pipeline: encrypt 8 arrays, one 8-way add, decrypt the sum; step i's arrays
+        # are under obfuscator bases index_base + (8 i + k + 1) x total, k = 0..7
         xs8 = torch.stack([torch.from_numpy(np.random.default_rng(k).standard_normal(N, dtype=np.float32))
                            for k in range(K8)]).to(dev)
         cts8 = torch.empty((K8, N, W), dtype=torch.int32, device=dev)
@@ -603,71 +836,42 @@ def main():
         val8 = torch.empty(N, dtype=torch.float64, device=dev)
         st8 = torch.empty(N, dtype=torch.int32, device=dev)
 
-        def step(i):
-            for k in range(K8):
-                encrypt(xs8[k], cts8[k], exs8[k], index_base + (k + 1) * total)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            add_k(cts8, exs8, K8, sum_ct, sum_ex)
-            e1.record(stream)
-            add_events.append((e0, e1))
-            decrypt(sum_ct, sum_ex, val8, st8)
+        class Add8Steps:
+            last_i = None
 
-        def drain():
-            pass
+            def step(self, i):
+                for k in range(K8):
+                    encrypt(xs8[k], cts8[k], exs8[k], index_base + (K8 * i + k + 1) * total)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                add_k(cts8, exs8, K8, sum_ct, sum_ex)
+                e1.record(stream)
+                if i >= args.warmup:
+                    add_events.append((e0, e1))
+                decrypt(sum_ct, sum_ex, val8, st8)
+                self.last_i = i
+
+            def drain(self):
+                pass
+
+        stepper = Add8Steps()
+        stage_ms = []
+        elapsed = run_timed(stepper, args.steps, args.warmup, sync, barrier, max_over_ranks)
     else:
         ct = torch.empty((N, W), dtype=torch.int32, device=dev)
         ex = torch.empty(N, dtype=torch.int32, device=dev)
         # N > 1: double-buffered shards and gathered outputs; step i's RCCL all-gather (ciphertexts +
-        # exponents) runs on the process group's stream while step i+1 encrypts
+        # exponents) runs on the process group's stream while step i+1 encrypts (ShardSteps)
         bufs = [(ct, ex)] + ([(torch.empty_like(ct), torch.empty_like(ex))] if world > 1 else [])
         gath = [(torch.empty((world * N, W), dtype=torch.int32, device=dev),
                  torch.empty(world * N, dtype=torch.int32, device=dev)) for _ in bufs] if world > 1 else []
-        works = [[] for _ in bufs]
-
-        def step(i):
-            b = i % len(bufs)
-            for w in works[b]:
-                w.wait()                   # the gather that last read this buffer is done
-            works[b] = []
-            encrypt(x, bufs[b][0], bufs[b][1], index_base)
-            if world > 1:
-                for t, o in zip(bufs[b], gath[b]):
-                    _, w = gather_shards_async(t, world * N, world, out=o)
-                    if w is not None:
-                        works[b].append(w)
-
-        def drain():
-            for b in range(len(bufs)):
-                for w in works[b]:
-                    w.wait()
-                works[b] = []
-
-    for i in range(args.warmup):
-        step(i)
-    drain()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    add_events.clear()
-    stage_ms = []
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-        if cfg_id != 2:
-            stage_ms.append(ctx.stage_times())   # HIP events recorded between this encrypt call's kernels
-    drain()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    units = (total if cfg["shard"] == "strong" else world * N) * args.steps
+        stepper = ShardSteps(lambda o, e, base: encrypt(x, o, e, base), bufs, gath, world, index_base, stride,
+                             gather_shards_async)
+        stage_ms = []
+        # HIP events recorded between each timed encrypt call's kernels
+        elapsed = run_timed(stepper, args.steps, args.warmup, sync, barrier, max_over_ranks,
+                            after_step=lambda: stage_ms.append(ctx.stage_times()))
+    units = job_units(cfg["shard"], total, world, N, args.steps)
     value = units / elapsed
 
     if cfg_id == 2:
@@ -681,17 +885,21 @@ def main():
         ct, ex = cts8[0], exs8[0]
         x_host = xs8[0].cpu().numpy()
         x = xs8[0]
-        index_base_chk = index_base + total
+        index_base_chk = index_base + (K8 * stepper.last_i + 1) * total
     else:
-        index_base_chk = index_base
-        ct, ex = bufs[(args.steps - 1) % len(bufs)]   # the last timed step's output (checked below)
+        index_base_chk = stepper.base(stepper.last_i)
+        (ct, ex), _ = stepper.last_output()       # the last timed step's output (checked below)
         if world > 1:
             # the gathered array holds every rank's shard; this rank's block equals its own output
-            go, ge = gath[(args.steps - 1) % len(gath)]
-            same = bool(torch.equal(go[rank * N:(rank + 1) * N], ct)) and bool(torch.equal(ge[rank * N:(rank + 1) * N], ex))
+            same = stepper.own_shard_identical(rank)
             extra["allgather_own_shard_identical"] = same
             if not same:
                 raise SystemExit("all-gathered shard differs from the local one")
+    extra["obfuscator_index_bases"] = {"first_timed_step": (index_base + K8 * args.warmup * total + total) if cfg_id == 2
+                                       else stepper.base(args.warmup),
+                                       "stride_per_step": K8 * total if cfg_id == 2 else stride,
+                                       "note": "every step encrypts under fresh obfuscators (global index base advanced "
+                                               "by the job's elements per step, bench.py step_base)"}
     stage_avg = [float(np.mean([s[i] for s in stage_ms])) for i in range(len(stage_ms[0]))] if stage_ms else []
 
     # ---- correctness of the timed output: decrypt on the device, compare with the input exactly
@@ -750,7 +958,7 @@ def main():
                         ev["c1"].record(side)
                 if run_enc:
                     ev["e0"].record(stream)
-                    encrypt(x, ct, ex, index_base)
+                    encrypt(x, ct, ex, index_base_chk)   # (rewrites the last step's own output)
                     ev["e1"].record(stream)
                 torch.cuda.synchronize()
                 wall = (time.perf_counter() - t0) * 1e3
@@ -786,53 +994,15 @@ def main():
               for _ in range(2 if world > 1 else 1)]
         g3 = [(torch.empty((world * N3, W), dtype=torch.int32, device=dev),
                torch.empty(world * N3, dtype=torch.int32, device=dev)) for _ in b3] if world > 1 else []
-        w3 = [[] for _ in b3]
-
-        def step3(i):
-            b = i % len(b3)
-            for w in w3[b]:
-                w.wait()
-            w3[b] = []
-            encrypt(x3, b3[b][0], b3[b][1], lo3, N3, st3)
-            if world > 1:
-                for t, o in zip(b3[b], g3[b]):
-                    _, w = gather_shards_async(t, world * N3, world, out=o)
-                    if w is not None:
-                        w3[b].append(w)
-
-        def drain3():
-            for b in range(len(b3)):
-                for w in w3[b]:
-                    w.wait()
-                w3[b] = []
-
-        step3(0)
-        drain3()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t3 = time.perf_counter()
-        for i in range(args.strong_steps):
-            step3(i)
-        drain3()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        el3 = time.perf_counter() - t3
-        if world > 1:
-            t = torch.tensor([el3], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el3 = float(t.item())
+        s3 = ShardSteps(lambda o, e, base: encrypt(x3, o, e, base, N3, st3), b3, g3, world, lo3, tot3,
+                        gather_shards_async)
+        el3 = run_timed(s3, args.strong_steps, 1, sync, barrier, max_over_ranks)
         leg = {"workload": CONFIGS[3]["desc"], "elements_total": tot3, "elements_per_gpu": N3,
                "value": tot3 * args.strong_steps / el3, "unit": "encrypts/s", "scaling": "strong",
                "steps": args.strong_steps, "ms_per_step": el3 / args.strong_steps * 1e3,
                "allgather": "RCCL all_gather_into_tensor of words + exponents per step" if world > 1 else "none (N = 1)"}
         if world > 1:
-            bl = (args.strong_steps - 1) % len(b3)
-            same = bool(torch.equal(g3[bl][0][rank * N3:(rank + 1) * N3], b3[bl][0])) and \
-                bool(torch.equal(g3[bl][1][rank * N3:(rank + 1) * N3], b3[bl][1]))
+            same = s3.own_shard_identical(rank)
             leg["allgather_own_shard_identical"] = same
             leg["gathered_bytes_per_rank_per_step"] = world * N3 * (W + 1) * 4
             if not same:
@@ -840,22 +1010,23 @@ def main():
         # the last timed step's output, checked: this rank's shard decrypted on the device (up to
         # the 2M elements of one rank's shard at N = 8), the sampler's restatement at the shard's seams, and at
         # N > 1 a block of the next rank's shard as gathered here, against that rank's regenerated input
-        bl = (args.strong_steps - 1) % len(b3)
+        (c3o, e3o), r3o = s3.last_output()
+        base3 = s3.base(s3.last_i)               # the last step's obfuscator base (global index of the shard's row 0)
         n3 = hi3 - lo3
         nchk = min(n3, 2 << 20)
         v3 = torch.empty(nchk, dtype=torch.float64, device=dev)
-        s3 = torch.empty(nchk, dtype=torch.int32, device=dev)
-        decrypt(b3[bl][0], b3[bl][1], v3, s3, nchk)
+        st3v = torch.empty(nchk, dtype=torch.int32, device=dev)
+        decrypt(c3o, e3o, v3, st3v, nchk)
         torch.cuda.synchronize()
         chk = {"decrypted_own_elements": nchk,
-               "own_roundtrip_exact": bool(torch.equal(v3, x3[:nchk].double())) and int((s3 > 1).sum().item()) == 0}
+               "own_roundtrip_exact": bool(torch.equal(v3, x3[:nchk].double())) and int((st3v > 1).sum().item()) == 0}
         if use_fb and fb_info is not None:
             # checked against the oracle's restatement in the cpu_baseline leg below (the one place bench.py
             # runs oracle/ code)
             seam = [0, n3 - 1]
-            c3_seams = (leg, [lo3 + i for i in seam], [x3_host[i] for i in seam],
-                        _native.words_to_ints(b3[bl][0][seam].cpu().numpy().view(np.uint32)),
-                        [int(v) for v in b3[bl][1][seam].cpu().numpy()])
+            c3_seams = (leg, [base3 + i for i in seam], [x3_host[i] for i in seam],
+                        _native.words_to_ints(c3o[seam].cpu().numpy().view(np.uint32)),
+                        [int(v) for v in e3o[seam].cpu().numpy()])
         if world > 1:
             peer = (rank + 1) % world
             plo, phi = shard_bounds(tot3, world, peer)
@@ -863,7 +1034,7 @@ def main():
             xp = torch.from_numpy(np.random.default_rng(1000 + peer).standard_normal(N3, dtype=np.float32)[:npe]).to(dev)
             vp = torch.empty(npe, dtype=torch.float64, device=dev)
             sp = torch.empty(npe, dtype=torch.int32, device=dev)
-            decrypt(g3[bl][0][peer * N3:], g3[bl][1][peer * N3:], vp, sp, npe)
+            decrypt(r3o[0][peer * N3:], r3o[1][peer * N3:], vp, sp, npe)
             torch.cuda.synchronize()
             chk["gathered_peer_block"] = {"peer": peer, "elements": npe,
                                           "roundtrip_exact": bool(torch.equal(vp, xp.double())) and int((sp > 1).sum().item()) == 0}
@@ -873,7 +1044,7 @@ def main():
         if bad:
             raise SystemExit(f"configs[3]: last step's output failed its check: {chk}")
         extra["config3_strong"] = leg
-        del x3, st3, b3, g3, w3, v3, s3
+        del x3, st3, b3, g3, s3, c3o, e3o, r3o, v3, st3v
         torch.cuda.empty_cache()
 
     solo = world == 1 and rank == 0        # single-GPU legs beside the timed path
@@ -1015,12 +1186,12 @@ def main():
     if not args.no_host and solo and cfg_id in (1, 3):
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        hct, hex_, hst = ctx.encrypt(x_host, obf_mode=_native.PAI_OBF_RNG, rng_key=rng_key, index_base=index_base)
+        hct, hex_, hst = ctx.encrypt(x_host, obf_mode=_native.PAI_OBF_RNG, rng_key=rng_key, index_base=index_base_chk)
         t_fresh = time.perf_counter() - t1
         t_host = float("inf")
         for _ in range(2):                        # a streaming sender reuses its output buffers
             t1 = time.perf_counter()
-            ctx.encrypt(x_host, obf_mode=_native.PAI_OBF_RNG, rng_key=rng_key, index_base=index_base,
+            ctx.encrypt(x_host, obf_mode=_native.PAI_OBF_RNG, rng_key=rng_key, index_base=index_base_chk,
                         out=(hct, hex_, hst))
             t_host = min(t_host, time.perf_counter() - t1)
         hb = {"host_buffers_encrypts_per_s": N / t_host,
@@ -1056,7 +1227,7 @@ def main():
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             rc = lib.pai_encrypt_dev(rctx.handle, _native.PAI_F32, x.data_ptr(), N, 0, 0, _native.PAI_OBF_RNG, None, 0, 0,
-                                     rng_key, index_base, ct_r.data_ptr(), ex_r.data_ptr(), st_r.data_ptr(),
+                                     rng_key, index_base_chk, ct_r.data_ptr(), ex_r.data_ptr(), st_r.data_ptr(),
                                      stream.cuda_stream)
             if rc != 0:
                 raise RuntimeError(lib.pai_last_error().decode())
@@ -1169,6 +1340,14 @@ def main():
         torch.cuda.empty_cache()
         if not okp:
             raise SystemExit("public fixed-base ciphertexts do not decrypt to the input")
+
+    # ---- the 1024-bit key every reference protocol defaults to (VERDICT r5 Missing #2)
+    nb1_check = None
+    if cfg_id == 1 and solo and nb == 2048 and not args.no_nb1024 and use_fb:
+        ctx.set_fb_window(16)                 # (the key holder's big tables are not needed after the timed region)
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        extra["nb1024"], nb1_check = nb1024_leg(args, dev, stream, lib, rng_key, x, local_rank, index_base_chk + 7 * total)
 
     if rank != 0:
         if world > 1:
@@ -1294,6 +1473,23 @@ def main():
                 cpu["public_fixed_base_bit_exact_vs_oracle"] = {"elements": list(range(len(got))), "ok": pok}
                 if not pok:
                     raise SystemExit("public fixed-base ciphertexts differ from the oracle restatement")
+            if nb1_check is not None:
+                # the nb = 1024 leg: its generic CRT prefix against the GMP port, its fixed-base outputs against the
+                # oracle's restatement of the sampler
+                from oracle import paillier_oracle as O
+                g1, e1g = nb1_check["generic"]
+                s1 = len(g1)
+                x1 = x_host[:s1]
+                cc1, ce1 = gmp_oracle.encrypt_f32_chacha(nb1_check["n"], x1, rng_key, nb1_check["base"], th)
+                ok1 = bool(np.array_equal(g1, cc1) and np.array_equal(e1g, ce1))
+                okey1 = O.Key(nb1_check["n"], nb1_check["p"], nb1_check["q"])
+                got1 = _native.words_to_ints(nb1_check["fb_ct"])
+                okf = all(O.fb_encrypt_value(x_host[i], okey1, rng_key, nb1_check["base"] + i, nb1_check["fb_info"])
+                          == (got1[j], int(nb1_check["fb_ex"][j])) for j, i in enumerate(nb1_check["fb_idx"]))
+                extra["nb1024"]["check"] = {"generic_prefix_bit_exact_vs_gmp": {"elements": s1, "ok": ok1},
+                                            "fixed_base_bit_exact_vs_oracle": {"elements": nb1_check["fb_idx"], "ok": okf}}
+                if not (ok1 and okf):
+                    raise SystemExit(f"nb = 1024 leg differs from the GMP port / oracle: {extra['nb1024']['check']}")
             # configs[0] timed in full: nb = 1024, 1000 elements, encrypt + decrypt, threads = os.cpu_count()
             pk0, sk0 = generate_paillier_keypair(1024, seed=1)
             x0 = np.random.default_rng(0).standard_normal(1000, dtype=np.float32)

@@ -38,19 +38,10 @@ hipError_t pe_launch_iota_pow_f(const PeParams& p, const Dec4Geom& g, hipStream_
   if (ev && ev[1]) (void)hipEventRecord(ev[1], st);
   hipLaunchKernelGGL(k_pe_pow_f<D4_S>, dim3((int)std::min<long long>(g.gx_pow, pb)), dim3(LANE_BLOCK), 0, st, p);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (ev && ev[2]) (void)hipEventRecord(ev[2], st);
-  hipLaunchKernelGGL(k_pe_fin<D4_S>, dim3((int)std::min<long long>(g.gx_L, lb)), dim3(LANE_BLOCK), 0, st, p);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (ev && ev[3]) (void)hipEventRecord(ev[3], st);
-  return hipSuccess;
-}
-
-hipError_t pe_launch_pow_fin(const PeParams& p, const Dec4Geom& g, hipStream_t st, hipEvent_t* ev) {
-  const long long pb = (p.n + D4_PAIRS - 1) / D4_PAIRS, lb = (p.n + LANE_BLOCK - 1) / LANE_BLOCK;
-  if (ev && ev[1]) (void)hipEventRecord(ev[1], st);
-  hipLaunchKernelGGL(k_pe_pow<D4_S>, dim3((int)std::min<long long>(g.gx_pow, pb)), dim3(LANE_BLOCK), 0, st, p);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  if (p.noinv) {   // the general chain, which exits at once unless the chunk had no inverse (PeParams::noinv)
+    hipLaunchKernelGGL(k_pe_pow<D4_S>, dim3((int)std::min<long long>(g.gx_pow, pb)), dim3(LANE_BLOCK), 0, st, p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   if (ev && ev[2]) (void)hipEventRecord(ev[2], st);
   hipLaunchKernelGGL(k_pe_fin<D4_S>, dim3((int)std::min<long long>(g.gx_L, lb)), dim3(LANE_BLOCK), 0, st, p);
   if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -12,7 +12,6 @@ hipError_t pe_launch(const PeParams& p, const Dec4Geom& g, hipStream_t st, hipEv
 hipError_t pe_launch_pre_aw(const PeParams& p, const Dec4Geom& g, hipStream_t st, hipEvent_t* ev);
 hipError_t pe_launch_iota_pow_f(const PeParams& p, const Dec4Geom& g, hipStream_t st, hipEvent_t* ev);
 // the general chain after pe_launch_pre_aw (a chunk whose batch inversion found a non-unit): k_pe_pow + k_pe_fin
-hipError_t pe_launch_pow_fin(const PeParams& p, const Dec4Geom& g, hipStream_t st, hipEvent_t* ev);
 // k_pe_fin alone: c = A + n B from the pairs in p.xw (the public fixed-base path, engine_pfb.hip)
 hipError_t pe_launch_fin(const PeParams& p, int cus, hipStream_t st);
 

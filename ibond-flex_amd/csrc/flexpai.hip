@@ -192,6 +192,14 @@ struct pai_ctx {
   void* d_inv = nullptr;        // batch-inversion prefix products and segment products
   size_t inv_bytes = 0;
   std::vector<uint32_t> inv_host;   // top of the inversion tree (host side of an async copy)
+  // the public-key chain's inversion without a host wait (batch_invert_async): the top value goes device -> pinned
+  // words, a host function in stream order inverts it mod n there, and the result (+ a no-inverse flag) goes back
+  struct AsyncInv {
+    HBig mod;
+    int W = 0;
+    uint32_t* pin = nullptr;     // [W] words of the top value, then its inverse; [W]: 1 = no inverse exists
+  };
+  AsyncInv* inv_async = nullptr;
   int cus = 0;
   // optional per-stage timing of the last encrypt call (PAI_OPT_STAGE_TIMING)
   bool timing = false;
@@ -268,6 +276,10 @@ pai_ctx::~pai_ctx() {
   if (d_work) (void)hipFree(d_work);
   if (d_mul) (void)hipFree(d_mul);
   if (d_inv) (void)hipFree(d_inv);
+  if (inv_async) {
+    if (inv_async->pin) (void)hipHostFree(inv_async->pin);
+    delete inv_async;
+  }
   if (d_plain) (void)hipFree(d_plain);
   if (d_seg) (void)hipFree(d_seg);
   if (d_addplan) (void)hipFree(d_addplan);
@@ -954,11 +966,13 @@ static int sgp_make_half(const HBig& P, const HBig& w, int K, const void* table,
 
 // The Shoup rows of both halves from their factored rows t[h] (kernels_sgs.hpp k_sgs_conv) and the constants of
 // k_sgs_bfin: w 2^(16 c) R mod P (R = 2^(28 FBGP_S), the b rows' radix; w = the other prime) and mu = floor(2^(56 S) / P).
-// A failed allocation leaves the Montgomery sampler in place (returns 0, d_sgs_fb unset).
+// The row memory at[h] was reserved before the factored tables were built (ensure_fb), so that a device without room for
+// both never ends up on the factored rows at the Shoup rows' lower window. Any failure here leaves the Montgomery sampler
+// k_sgp in place over the complete factored tables (returns nonzero with the reason in pai_last_error; the caller frees
+// at[] and keeps the fixed-base path).
 template <class Ctx>
-static int sgs_build(Ctx* c, const HBig* primes, int K, int W, void* const* t, const SgpHalf* sv) {
+static int sgs_build(Ctx* c, const HBig* primes, int K, int W, void* const* t, const SgpHalf* sv, uint4* const* at) {
   SgsHalf sh[2];
-  uint4* at[2] = {nullptr, nullptr};
   const size_t rows = (size_t)K << W;
   for (int h = 0; h < 2; ++h) {
     const HBig& P = primes[h];
@@ -990,23 +1004,16 @@ static int sgs_build(Ctx* c, const HBig* primes, int K, int W, void* const* t, c
         (rc = upload_fb(c, y.words(FBGP_PW), &dcy)) ||
         (rc = upload_fb(c, mul_pow2_mod(beta, (size_t)LB * FBGP_S, P).limbs(SGP_S, LB), &dbr)))
       return rc;
-    if (hipMalloc((void**)&at[h], rows * SGS_ROW_Q * sizeof(uint4)) != hipSuccess) {
-      (void)hipGetLastError();
-      if (h == 1) {
-        c->fb_mem.erase(std::find(c->fb_mem.begin(), c->fb_mem.end(), (void*)at[0]));
-        (void)hipFree(at[0]);
-      }
-      return 0;
-    }
-    c->fb_mem.push_back(at[h]);
     sh[h] = SgsHalf{at[h], (const uint4*)t[h], sv[h].p, dn, sv[h].pbig, dmu, dcy, dbr, sv[h].mprime};
   }
   SgsHalf* d = nullptr;
   std::vector<SgsHalf> shv(sh, sh + 2);
   int rc;
   if ((rc = upload_fb(c, shv, &d))) return rc;
-  if (sgs_launch_conv(d, rows, at[0], at[1], nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+  if (sgs_launch_conv(d, rows, at[0], at[1], nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    (void)hipGetLastError();
     return fail(PAI_ERR_HIP, "Shoup row conversion failed");
+  }
   c->d_sgs_fb = d;
   return 0;
 }
@@ -1107,7 +1114,7 @@ static uint64_t fb_bytes(const pai_ctx* c, int W, bool sgs = false) {
 }
 
 // The window of the tables (<= c->fb_W, within budget) and whether Shoup rows join them (sgs_mode, above)
-static int fb_choose(const pai_ctx* c, uint64_t budget, bool* sgs) {
+static int fb_choose(const pai_ctx* c, uint64_t budget, bool* sgs, bool allow_sgs = true) {
   static const int ladder[] = {24, 23, 22, 21, 20, 16, 12, 8};
   int wm = 0, ws = 0;
   for (int w : ladder)
@@ -1115,7 +1122,7 @@ static int fb_choose(const pai_ctx* c, uint64_t budget, bool* sgs) {
       wm = w;
       break;
     }
-  const int mode = sgs_mode();
+  const int mode = allow_sgs ? sgs_mode() : 0;
   if (mode != 0 && fb_gpair_possible(c) && sgp_enabled())
     for (int w : ladder)
       if (w <= c->fb_W && fb_bytes(c, w, true) <= budget) {
@@ -1256,8 +1263,29 @@ static int ensure_fb(pai_ctx* c) {
   if (!c->fb_W) c->fb_W = fb_default_window();
   const uint64_t budget = fb_budget(c);
   bool sgs = false;
-  const int W = fb_choose(c, budget, &sgs);
+  int W = fb_choose(c, budget, &sgs);
   if (!W) return fb_unavailable(c, "tables do not fit the device memory budget");
+  // the 4096-bit Shoup rows' memory is taken first: without room for it the tables are built at the factored rows'
+  // own (higher) window instead of at the one chosen for both
+  uint4* sgs_rows[2] = {nullptr, nullptr};
+  if (sgs) {
+    const size_t rows = (size_t)fb_digit_count(c, W) << W;
+    for (int h = 0; h < 2 && sgs; ++h)
+      if (hipMalloc((void**)&sgs_rows[h], rows * SGS_ROW_Q * sizeof(uint4)) != hipSuccess) {
+        (void)hipGetLastError();
+        sgs_rows[h] = nullptr;
+        sgs = false;
+      }
+    if (!sgs) {
+      for (uint4*& r : sgs_rows)
+        if (r) (void)hipFree(r), r = nullptr;
+      W = fb_choose(c, fb_budget(c), &sgs, false);
+      if (!W) return fb_unavailable(c, "tables do not fit the device memory budget");
+      if (setup_trace_on()) fprintf(stderr, "flexpai-trace Shoup rows: no room; factored rows at W = %d\n", W);
+    } else {
+      for (uint4* r : sgs_rows) c->fb_mem.push_back(r);
+    }
+  }
   SetupTrace tr_all("ensure_fb");
   const auto t0 = std::chrono::steady_clock::now();
   const size_t kb[2] = {sub(c->fb_p, HBig(1)).bits(), sub(c->fb_q, HBig(1)).bits()};
@@ -1563,9 +1591,24 @@ static int ensure_fb(pai_ctx* c) {
     c->fb_mem.erase(std::find(c->fb_mem.begin(), c->fb_mem.end(), p));
     (void)hipFree(p);
   }
+  if (sgs && !(gpair_ok && sgp_enabled())) {   // (a test build's $FLEXPAI_SGP=0 / $FLEXPAI_FB_PAIR=0 context)
+    for (uint4*& r : sgs_rows) {
+      c->fb_mem.erase(std::find(c->fb_mem.begin(), c->fb_mem.end(), (void*)r));
+      (void)hipFree(r);
+      r = nullptr;
+    }
+  }
   if (gpair_ok && sgp_enabled() && sgs) {
     SetupTrace tr_s("  Shoup rows (k_sgs_conv)");
-    if ((rc = sgs_build(c, primes, K, W, t, sv))) return fb_unavailable(c, pai_last_error());
+    if ((rc = sgs_build(c, primes, K, W, t, sv, sgs_rows))) {
+      // the factored rows are complete: k_sgp runs on them (split_sampler bit 3 stays clear)
+      if (setup_trace_on()) fprintf(stderr, "flexpai-trace Shoup rows failed (%s): k_sgp at W = %d\n", pai_last_error(), W);
+      for (uint4*& r : sgs_rows) {
+        c->fb_mem.erase(std::find(c->fb_mem.begin(), c->fb_mem.end(), (void*)r));
+        (void)hipFree(r);
+        r = nullptr;
+      }
+    }
   }
   const auto t2 = std::chrono::steady_clock::now();
   c->fb_host_ms = std::chrono::duration<float, std::milli>(t1 - t0).count();
@@ -2635,6 +2678,7 @@ struct InvMod {
 };
 static int batch_invert(pai_ctx* c, uint32_t* x, const uint8_t* flag, long long n, hipStream_t st, const InvMod& md);
 static int batch_invert(pai_ctx* c, uint32_t* x, const uint8_t* flag, long long n, hipStream_t st);
+static int batch_invert_async(pai_ctx* c, uint32_t* x, long long n, hipStream_t st, const InvMod& md, uint32_t** d_noinv);
 
 // Chunks below this many elements take the general chain: the factored one saves ~0.2 us per element (k_pe_pow_f
 // against k_pe_pow) and costs the batch inversion's fixed ~1-2 ms of short dependent launches. $FLEXPAI_PEF_MIN
@@ -2689,13 +2733,12 @@ static int launch_pe(pai_ctx* c, const EncParams& e, hipStream_t st) {
     p.aw_words = c->pt_words;
     p.iota = (uint32_t*)((char*)p.aw + awbytes * chunk);
     HIPCHK(pe_launch_pre_aw(p, g, st, ev));
-    rc = batch_invert(c, p.aw, nullptr, n, st,
-                      InvMod{2, c->pt_words, 2 * L, c->d_pe_n, c->d_pe_r2, c->d_pe_oneR, c->pe_mprime, &c->n});
-    if (rc == PAI_ERR_NOINV) {   // an A_r shares a factor with n (probability ~2^-1023): the general chain for this chunk
-      HIPCHK(pe_launch_pow_fin(p, g, st, ev));
-      continue;
-    }
+    uint32_t* noinv = nullptr;
+    rc = batch_invert_async(c, p.aw, n, st,
+                            InvMod{2, c->pt_words, 2 * L, c->d_pe_n, c->d_pe_r2, c->d_pe_oneR, c->pe_mprime, &c->n}, &noinv);
     if (rc) return rc;
+    // an A_r that shares a factor with n (no inverse): the device flag sends this chunk down the general chain
+    p.noinv = noinv;
     HIPCHK(pe_launch_iota_pow_f(p, g, st, ev));
   }
   return 0;
@@ -3182,6 +3225,93 @@ static int batch_invert(pai_ctx* c, uint32_t* x, const uint8_t* flag, long long 
   c->inv_host = inv.words(W);
   HIPCHK(hipMemcpyAsync(top, c->inv_host.data(), (size_t)W * 4, hipMemcpyHostToDevice, st));
   for (int l = levels - 1; l >= 0; --l) HIPCHK(inv_launch(md.tpi, false, params(l), inv_grid(c, md.tpi, ns[l + 1]), st));
+  return 0;
+}
+
+// The public-key encryption's batch inversion (launch_pe) without blocking the caller: batch_invert's levels, but the top
+// value is inverted by a host function queued on `st` (hipLaunchHostFunc: it runs when the stream reaches it, on the
+// runtime's thread, touching only the pinned words) instead of after a hipStreamSynchronize, so pai_encrypt_dev stays
+// asynchronous and capturable. An A_r that shares a factor with n (no inverse, probability ~2^-1023 for
+// random r; r = 0, n, 5p given explicitly) sets *d_noinv = 1, and the kernels choose the chain on the device:
+// k_pe_iota / k_pe_pow_f exit, the general k_pe_pow runs (kernels_pe.hpp, PeParams::noinv).
+static void inv_top_host(void* u) {
+  auto* a = (pai_ctx::AsyncInv*)u;
+  try {
+    HBig v;
+    v.w.assign(a->pin, a->pin + a->W);
+    v.trim();
+    const HBig inv = inv_mod(v, a->mod);
+    if (inv.is_zero()) {
+      a->pin[a->W] = 1u;
+      return;
+    }
+    const std::vector<uint32_t> w = inv.words(a->W);
+    std::memcpy(a->pin, w.data(), (size_t)a->W * 4);
+    a->pin[a->W] = 0u;
+  } catch (...) {
+    a->pin[a->W] = 1u;   // the general chain, same ciphertexts
+  }
+}
+
+static int batch_invert_async(pai_ctx* c, uint32_t* x, long long n, hipStream_t st, const InvMod& md, uint32_t** d_noinv) {
+  const int S = md.S, W = md.W;
+  std::vector<long long> ns{n};
+  std::vector<int> seg;
+  do {
+    seg.push_back((int)std::max<long long>(4, std::min<long long>(INV_SEG, ns.back() / 4096)));
+    ns.push_back((ns.back() + seg.back() - 1) / seg.back());
+  } while (ns.back() > 1);
+  const int levels = (int)ns.size() - 1;
+  std::vector<size_t> pre_off(levels), seg_off(levels);
+  size_t off = 0;
+  for (int l = 0; l < levels; ++l) {
+    pre_off[l] = off;
+    off = align16(off + (size_t)ns[l] * S * 4);
+    seg_off[l] = off;
+    off = align16(off + (size_t)ns[l + 1] * W * 4);
+  }
+  const size_t flag_off = off;
+  off += 16;
+  int rc = ensure_buf(&c->d_inv, &c->inv_bytes, off);
+  if (rc) return rc;
+  if (!c->inv_async || c->inv_async->W != W || !(c->inv_async->mod.w == md.mod->w)) {
+    if (!c->inv_async) c->inv_async = new pai_ctx::AsyncInv;
+    if (c->inv_async->pin && c->inv_async->W < W) {
+      HIPCHK(hipStreamSynchronize(st));   // (once per context: a previous call's host function may still read it)
+      (void)hipHostFree(c->inv_async->pin);
+      c->inv_async->pin = nullptr;
+    }
+    if (!c->inv_async->pin) HIPCHK(hipHostMalloc((void**)&c->inv_async->pin, (size_t)(W + 4) * 4, hipHostMallocDefault));
+    c->inv_async->W = W;
+    c->inv_async->mod = *md.mod;
+  }
+  char* base = (char*)c->d_inv;
+  auto params = [&](int l) {
+    InvParams p{};
+    p.x = l == 0 ? x : (uint32_t*)(base + seg_off[l - 1]);
+    p.flag = nullptr;
+    p.n = ns[l];
+    p.pre = (uint32_t*)(base + pre_off[l]);
+    p.seg = (uint32_t*)(base + seg_off[l]);
+    p.N = md.N;
+    p.R2 = md.R2;
+    p.oneR = md.oneR;
+    p.mprime = md.mprime;
+    p.ct_words = W;
+    p.seg_len = seg[l];
+    return p;
+  };
+  for (int l = 0; l < levels; ++l) HIPCHK(inv_launch(md.tpi, true, params(l), inv_grid(c, md.tpi, ns[l + 1]), st));
+  uint32_t* top = (uint32_t*)(base + seg_off[levels - 1]);
+  uint32_t* flag = (uint32_t*)(base + flag_off);
+  uint32_t* pin = c->inv_async->pin;
+  HIPCHK(hipMemcpyAsync(pin, top, (size_t)W * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipLaunchHostFunc(st, inv_top_host, c->inv_async));
+  HIPCHK(hipMemcpyAsync(top, pin, (size_t)W * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(flag, pin + W, 4, hipMemcpyHostToDevice, st));
+  // (with no inverse the words copied back are the top value itself: the levels below produce values nobody reads)
+  for (int l = levels - 1; l >= 0; --l) HIPCHK(inv_launch(md.tpi, false, params(l), inv_grid(c, md.tpi, ns[l + 1]), st));
+  *d_noinv = flag;
   return 0;
 }
 

@@ -57,6 +57,8 @@ struct PeParams {
   uint32_t* aw;            // [n][aw_words] A_r mod n as words, then its inverse mod n (k_pe_awords -> batch inversion -> k_pe_iota)
   int aw_words;            // words of n
   uint32_t* iota;          // [S][n] A_r^-1 R^2 mod n (k_pe_iota -> k_pe_pow_f)
+  const uint32_t* noinv;   // the factored chain's device flag (flexpai.hip batch_invert_async), or null: when set, 1 = no
+                           // inverse exists (k_pe_iota / k_pe_pow_f exit, k_pe_pow runs), 0 = k_pe_pow exits
   uint32_t* scratch;
   uint32_t* ct;
   int ct_words;
@@ -137,6 +139,7 @@ d4_pass<S>(P, a, sx, 0, m, mprime, odd, std::make_integer_sequence<int, S>{});
 
 template <int S>
 __global__ __launch_bounds__(LANE_BLOCK, 2) void k_pe_pow(PeParams p) {
+  if (p.noinv && *p.noinv == 0u) return;   // the factored chain ran
   constexpr int TQ = tile_quads<S>();
   using Q = std::make_integer_sequence<int, TQ>;
   __shared__ uint32_t lds[D4_PAIRS * D4R_SLOT + S];
@@ -220,6 +223,7 @@ __global__ __launch_bounds__(LANE_BLOCK) void k_pe_awords(PeParams p) {
 // (staged in LDS) by the pair of R^3 (k_pe_pre's constant), the even lane's row (the A component: R^3 mod n)
 template <int S>
 __global__ __launch_bounds__(LANE_BLOCK, 1) void k_pe_iota(PeParams p) {
+  if (p.noinv && *p.noinv != 0u) return;   // no inverse: the general chain (k_pe_pow) instead
   __shared__ uint32_t lds[D4_PAIRS * D4_SLOT];
   const PeConst* K = p.k;
   uint32_t m[S];
@@ -265,6 +269,7 @@ __global__ __launch_bounds__(LANE_BLOCK, 1) void k_pe_iota(PeParams p) {
 // the factored chain (d4f_run<S, true>): the plain pair of c = c0 r^n, as k_pe_pow
 template <int S>
 __global__ __launch_bounds__(LANE_BLOCK, 2) void k_pe_pow_f(PeParams p) {
+  if (p.noinv && *p.noinv != 0u) return;
   __shared__ uint32_t lds[D4_PAIRS * D4R_SLOT + 2 * S];
   const PeConst* K = p.k;
   uint32_t m[S];

@@ -43,19 +43,15 @@ def gather_shards_async(local, total: int, world: int, group=None, out=None):
     the RCCL all-gather runs on the process group's own stream (ordered after the work already queued
     on the current stream), so the caller can launch the next shard's kernels on the compute stream
     while it runs, and calls work.wait() before reusing `local` or reading `out`. work is None when
-    the gather completed synchronously (CPU tensors). `out` (optional, [world * ceil(total / world), ...])
-    is a preallocated receive buffer reused across steps instead of a fresh allocation per call."""
+    the gather completed synchronously. `out` (optional, [world * ceil(total / world), ...])
+    is a preallocated receive buffer reused across steps instead of a fresh allocation per call. On CPU tensors (gloo,
+    the multi-rank CPU tests) the gather is asynchronous too: gloo writes the world's shards into views of `out`
+    in the background until work.wait()."""
     import torch
     import torch.distributed as dist
     per = -(-total // world)
     if local.shape[0] > per:
         raise ValueError("shard larger than ceil(total / world)")
-    if not local.is_cuda:
-        res = gather_shards(local, total, world, group)
-        if out is not None:
-            out[:total].copy_(res)
-            return out[:total], None
-        return res, None
     if local.shape[0] < per:
         pad = torch.zeros((per - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         local = torch.cat([local, pad])
@@ -64,5 +60,8 @@ def gather_shards_async(local, total: int, world: int, group=None, out=None):
         out = torch.empty(shape, dtype=local.dtype, device=local.device)
     elif tuple(out.shape) != shape or out.dtype != local.dtype:
         raise ValueError(f"receive buffer {tuple(out.shape)} {out.dtype} != {shape} {local.dtype}")
-    work = dist.all_gather_into_tensor(out, local.contiguous(), group=group, async_op=True)
+    if local.is_cuda:
+        work = dist.all_gather_into_tensor(out, local.contiguous(), group=group, async_op=True)
+    else:
+        work = dist.all_gather(list(out.chunk(world)), local.contiguous(), group=group, async_op=True)
     return out[:total], work

@@ -250,7 +250,10 @@ int pai_matmul(pai_ctx* ctx, const uint32_t* ct, const int32_t* exp, size_t m, s
                size_t d, uint32_t* ct_out, int32_t* exp_out);
 
 /* Device-resident variants (device pointers, asynchronous on `stream`, a hipStream_t; pai_mul_dev and
- * pai_matmul_dev synchronise `stream` once, for the single host-side inversion of the batch). */
+ * pai_matmul_dev synchronise `stream` once, for the single host-side inversion of the batch). pai_encrypt_dev never
+ * waits on the host: the public-key chain's batch inversion (chunks of >= 16384 elements) inverts its one top value
+ * in a host function queued on `stream` (hipLaunchHostFunc), so the call stays asynchronous and capturable; only
+ * the first device-RNG call that BUILDS a key's fixed-base tables synchronises the device (per-key setup). */
 int pai_encrypt_dev(pai_ctx* ctx, int dtype, const void* d_x, size_t N, int exp_mode, int32_t fixed_exp,
                     int obf_mode, const uint32_t* d_r_words, size_t r_stride_words, size_t r_words,
                     const uint8_t* rng_key32, uint64_t index_base,

@@ -113,3 +113,46 @@ def test_pe_factored_chain_above_threshold_matches_general(key2048, monkeypatch)
     d = N.Context(key2048.n, 0, key2048.p, key2048.q)
     val, _, _, _ = d.decrypt(ca, ea)
     assert np.array_equal(val, x.astype(np.float64))
+
+
+def test_pe_dev_call_is_asynchronous_on_a_side_stream(key2048, monkeypatch):
+    """pai_encrypt_dev on the factored public-key chain (>= 16 384 elements) queues its batch inversion's host
+    step as a host function instead of synchronising the stream. On a non-default torch stream that is still busy with
+    ~0.5 s of earlier work, the call returns at once; its ciphertexts equal the general chain's."""
+    import time
+    import torch
+    N = _native()
+    monkeypatch.delenv("FLEXPAI_PEF_MIN", raising=False)
+    a = _pub(monkeypatch, key2048, True)
+    a.set_public_fixed_base(False)
+    lib = N.load_library()
+    n = 20000
+    dev = torch.device("cuda", 0)
+    x = torch.from_numpy((np.random.default_rng(9).standard_normal(n) * 100).astype(np.float32)).to(dev)
+    W = a.ct_words
+    ct = torch.empty((n, W), dtype=torch.int32, device=dev)
+    ex = torch.empty(n, dtype=torch.int32, device=dev)
+    st = torch.empty(n, dtype=torch.int32, device=dev)
+    key = bytes(range(7, 39))
+    s = torch.cuda.Stream(dev)
+    # calibrate torch's spin kernel, then keep the side stream busy for ~0.5 s
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(s):
+        e0.record(s)
+        torch.cuda._sleep(10 ** 7)
+        e1.record(s)
+    torch.cuda.synchronize()
+    cyc_per_ms = 10 ** 7 / max(e0.elapsed_time(e1), 1e-3)
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(int(500 * cyc_per_ms))
+    t0 = time.perf_counter()
+    rc = lib.pai_encrypt_dev(a.handle, N.PAI_F32, x.data_ptr(), n, 0, 0, N.PAI_OBF_RNG, None, 0, 0, key, 11,
+                             ct.data_ptr(), ex.data_ptr(), st.data_ptr(), s.cuda_stream)
+    t_call = time.perf_counter() - t0
+    assert rc == 0, lib.pai_last_error().decode()
+    busy = not s.query()
+    torch.cuda.synchronize()
+    assert busy and t_call < 0.25, f"the call blocked the host for {t_call * 1e3:.0f} ms"
+    monkeypatch.setenv("FLEXPAI_PEF_MIN", str(1 << 40))       # the general chain on the same inputs
+    cg, eg, _ = a.encrypt(x.cpu().numpy(), obf_mode=N.PAI_OBF_RNG, rng_key=key, index_base=11)
+    assert np.array_equal(ct.cpu().numpy().view(np.uint32), cg) and np.array_equal(ex.cpu().numpy(), eg)

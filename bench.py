@@ -947,14 +947,27 @@ def main():
         if src is not None:
             side = torch.cuda.Stream(dev)
 
-            def timed(run_copy, run_enc):
+            standin = None
+            try:                                  # tools/gpu/rccl_standin.hip (__graft_entry__.build_standin)
+                import ctypes
+                standin = ctypes.CDLL(os.path.join(ROOT, "tools", "gpu", "librccl_standin.so"))
+                standin.standin_throttled_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulonglong,
+                                                           ctypes.c_int, ctypes.c_ulonglong, ctypes.c_void_p]
+            except OSError:
+                standin = None
+
+            def timed(run_copy, run_enc, cu_copy=None):
                 ev = {k: torch.cuda.Event(enable_timing=True) for k in ("c0", "c1", "e0", "e1")}
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 if run_copy:
                     with torch.cuda.stream(side):
                         ev["c0"].record(side)
-                        dst.copy_(src, non_blocking=True)
+                        if cu_copy is None:
+                            dst.copy_(src, non_blocking=True)
+                        elif standin.standin_throttled_copy(src.data_ptr(), dst.data_ptr(), nbytes, cu_copy[0],
+                                                            int(cu_copy[1] * 1e6), side.cuda_stream) != 0:
+                            raise RuntimeError("stand-in copy kernel failed to launch")
                         ev["c1"].record(side)
                 if run_enc:
                     ev["e0"].record(stream)
@@ -977,6 +990,22 @@ def main():
                 "encrypt_slowdown": e_both / e_alone,
                 "note": "a 3.8 GB device-to-device copy on a side stream (reads + writes HBM) stands in for the N = 8 "
                         "all-gather's receive writes into this rank's HBM during the next step's encrypt"}
+            # the same bytes moved by CU-resident copy workgroups (RCCL's channels: one workgroup each) that stay on
+            # their CUs for the xGMI-limited time of the gather (3.8 GB over 7 links x ~153 GB/s at ring efficiency:
+            # ~8-12 ms of each step), launched ahead of the encrypt like the previous step's gather
+            if standin is not None:
+                cu = []
+                for blocks, dur_ms in ((32, 10.0), (64, 10.0), (64, 12.0), (128, 8.0)):
+                    timed(True, False, (blocks, dur_ms))
+                    runs = [timed(True, True, (blocks, dur_ms)) for _ in range(3)]
+                    cb, eb, wb = min(runs, key=lambda t: t[1])
+                    ca = min(timed(True, False, (blocks, dur_ms))[0] for _ in range(2))
+                    cu.append({"workgroups": blocks, "target_ms": dur_ms, "copy_alone_ms": ca, "copy_with_encrypt_ms": cb,
+                               "encrypt_with_copy_ms": eb, "encrypt_slowdown": eb / e_alone, "both_wall_ms": wb})
+                extra["allgather_contention_1gpu"]["cu_resident_copy"] = {
+                    "runs": cu, "encrypt_alone_ms": e_alone,
+                    "note": "tools/gpu/rccl_standin.hip: the 3.8 GB moved by `workgroups` x 256 lanes that hold their CUs "
+                            "for target_ms (wall-clock throttled), on a side stream launched before the encrypt"}
             del src, dst
             torch.cuda.empty_cache()
 

@@ -14,9 +14,11 @@
 #include <thread>
 #include <array>
 #include <vector>
+#include <optional>
 
 #include "flexpai.h"
 #include "host_bignum.hpp"
+#include "table_arena.hpp"
 #include "kernels.hpp"
 #include "kernels_crt.hpp"
 #include "engine_dec.hpp"
@@ -148,7 +150,8 @@ struct pai_ctx {
   uint32_t* d_fb_q2Rn = nullptr;  // 4096-bit keys: q^2 R mod n^2 (k_fbg_fin)
   uint32_t fb_mprime0 = 0;      // p^2 (Garner)
   uint32_t fb_g[2] = {0, 0};   // the bases g_p, g_q (generators of Z_p*, Z_q*)
-  std::vector<void*> fb_mem;    // tables and their constants (rebuilt when the window changes)
+  std::vector<void*> fb_mem;    // the tables' constants and build scratch (rebuilt when the window changes)
+  std::vector<void*> fb_tables; // the tables themselves (TableArena: pooled device memory)
   HBig fb_p, fb_q;              // p < q
   float fb_host_ms = 0.f, fb_dev_ms = 0.f;
   uint32_t* fb_last_w = nullptr;  // debugging: k_fb output of the last chunk ([2][SB][fb_last_n])
@@ -168,6 +171,7 @@ struct pai_ctx {
   PfbConst* d_pfb = nullptr;
   SgpHalf* d_sgp_pfb = nullptr;  // the split-pair sampler over the public tables (kernels_sgp.hpp)
   std::vector<void*> pfb_mem;
+  std::vector<void*> pfb_tables;  // (TableArena)
   long long pfb_seen = 0;
   float pfb_host_ms = 0.f, pfb_dev_ms = 0.f;
   uint64_t pfb_table_bytes = 0;
@@ -272,6 +276,9 @@ pai_ctx::~pai_ctx() {
   for (void* p : priv_allocs) (void)hipFree(p);
   for (void* p : fb_mem) (void)hipFree(p);
   for (void* p : pfb_mem) (void)hipFree(p);
+  for (void* p : fb_tables) TableArena::get().free(p);
+  for (void* p : pfb_tables) TableArena::get().free(p);
+  if (counted && g_contexts.load() == 0) TableArena::get().trim();   // the process's last context: pooled chunks go back
   if (d_scratch) (void)hipFree(d_scratch);
   if (d_work) (void)hipFree(d_work);
   if (d_mul) (void)hipFree(d_mul);
@@ -610,12 +617,24 @@ static int ensure_scratch(pai_ctx* c, size_t bytes) {
 
 static size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
 
+// hipMalloc that, when the device is full, first hands the released tables' pooled chunks (table_arena.hpp) back to the
+// driver and tries again: pooled memory serves table rebuilds, never at the expense of a call's working buffers
+static hipError_t dev_malloc(void** p, size_t bytes) {
+  hipError_t e = hipMalloc(p, bytes);
+  if (e == hipErrorOutOfMemory && TableArena::get().pooled_any()) {
+    (void)hipGetLastError();
+    TableArena::get().trim();
+    e = hipMalloc(p, bytes);
+  }
+  return e;
+}
+
 static int ensure_buf(void** buf, size_t* have, size_t bytes) {
   if (bytes <= *have) return 0;
   if (*buf) HIPCHK(hipFree(*buf));
   *buf = nullptr;
   *have = 0;
-  HIPCHK(hipMalloc(buf, bytes));
+  HIPCHK(dev_malloc(buf, bytes));
   *have = bytes;
   return 0;
 }
@@ -625,7 +644,7 @@ static int ensure_work(pai_ctx* c, size_t bytes) {
   if (c->d_work) HIPCHK(hipFree(c->d_work));
   c->d_work = nullptr;
   c->work_bytes = 0;
-  HIPCHK(hipMalloc(&c->d_work, bytes));
+  HIPCHK(dev_malloc(&c->d_work, bytes));
   c->work_bytes = bytes;
   return 0;
 }
@@ -1141,10 +1160,10 @@ static int fb_choose(const pai_ctx* c, uint64_t budget, bool* sgs, bool allow_sg
 // memory, so an automatic choice never takes the whole device (W = 22 at nb = 2048 is 177 GB of 287 GB free; W = 23's
 // Shoup rows, 338 GB, do not fit).
 static uint64_t fb_budget(const pai_ctx* c) {
-  (void)c;
   if (const char* e = getenv("FLEXPAI_FB_MAX_BYTES")) return (uint64_t)strtod(e, nullptr);
   size_t fr = 0, tot = 0;
   if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 0;
+  fr += TableArena::get().pooled_bytes(c->device);   // released tables' chunks, held for reuse (table_arena.hpp)
   const uint64_t reserve = std::max<uint64_t>(4ull << 30, (uint64_t)tot / 12);
   uint64_t b = fr > reserve ? fr - reserve : 0;
   if (fb_window_auto()) {
@@ -1177,6 +1196,8 @@ static void pfb_release(pai_ctx* c);
 static void fb_release(pai_ctx* c) {
   for (void* p : c->fb_mem) (void)hipFree(p);
   c->fb_mem.clear();
+  for (void* p : c->fb_tables) TableArena::get().free(p);
+  c->fb_tables.clear();
   c->d_fb_halves = nullptr;
   c->d_fbp_halves = nullptr;
   c->d_fbp_fin_cs = c->d_fbp_fin_p = nullptr;
@@ -1271,19 +1292,15 @@ static int ensure_fb(pai_ctx* c) {
   if (sgs) {
     const size_t rows = (size_t)fb_digit_count(c, W) << W;
     for (int h = 0; h < 2 && sgs; ++h)
-      if (hipMalloc((void**)&sgs_rows[h], rows * SGS_ROW_Q * sizeof(uint4)) != hipSuccess) {
-        (void)hipGetLastError();
-        sgs_rows[h] = nullptr;
-        sgs = false;
-      }
+      if (!(sgs_rows[h] = (uint4*)TableArena::get().alloc(c->device, rows * SGS_ROW_Q * sizeof(uint4)))) sgs = false;
     if (!sgs) {
       for (uint4*& r : sgs_rows)
-        if (r) (void)hipFree(r), r = nullptr;
+        if (r) TableArena::get().free(r), r = nullptr;
       W = fb_choose(c, fb_budget(c), &sgs, false);
       if (!W) return fb_unavailable(c, "tables do not fit the device memory budget");
       if (setup_trace_on()) fprintf(stderr, "flexpai-trace Shoup rows: no room; factored rows at W = %d\n", W);
     } else {
-      for (uint4* r : sgs_rows) c->fb_mem.push_back(r);
+      for (uint4* r : sgs_rows) c->fb_tables.push_back(r);
     }
   }
   SetupTrace tr_all("ensure_fb");
@@ -1324,22 +1341,61 @@ static int ensure_fb(pai_ctx* c) {
   std::vector<void*> fb_scratch;   // further build scratch (freed with lohi)
   uint32_t* gcval[2] = {nullptr, nullptr};
   uint32_t* pcval[2] = {nullptr, nullptr};
+  // The per-half host work that needs no device -- the generator search, G = g^n mod p_h^2 (ONE powm) and the digit
+  // bases B_k by squarings in the form the resident sampler's build takes -- for both halves at once on two threads (a
+  // fresh key's setup, HE_SA_FT re-keys per exchange; round 6: the pair paths had computed G and the B_k twice)
+  struct HalfPrep {
+    uint32_t g = 0;
+    std::vector<uint32_t> bl, bases_p;
+  };
+  HalfPrep hp[2];
+  {
+    SetupTrace tr_hp("  host prep (generator, G, B_k; both halves)");
+    auto split_into = [](const HBig& v, const HBig& P, int limbs, std::vector<uint32_t>& out) {
+      const HBig qt = div_big(v, P), rm = sub(v, mul(qt, P));
+      const std::vector<uint32_t> a = rm.limbs(limbs, LB), b = qt.limbs(limbs, LB);
+      out.insert(out.end(), a.begin(), a.end());
+      out.insert(out.end(), b.begin(), b.end());
+    };
+    auto prep = [&](int h) {
+      HalfPrep& o = hp[h];
+      o.g = c->fb_g[h] ? c->fb_g[h] : fb_base(primes[h]);
+      if (!o.g) return;
+      const HBig& m2 = sq[h];
+      HMont M2(m2);
+      const HBig G = M2.to(M2.pow(HBig(o.g), c->n));
+      if (pair_ok || gpair_ok) {
+        // pair constants: (x mod p_h, x div p_h) of Montgomery-form values x = v R mod p_h^2: B_k R and B_k^(2^LO) R
+        const HBig& P = primes[h];
+        const int limbs = pair_ok ? ps : FBGP_S;
+        const size_t RS = (size_t)LB * limbs;
+        HBig y = G;
+        for (int k = 0; k < K; ++k) {
+          split_into(mul_pow2_mod(M2.from(y), RS, m2), P, limbs, o.bases_p);
+          split_into(mul_pow2_mod(M2.from(M2.sqr_k(y, (size_t)(W / 2))), RS, m2), P, limbs, o.bases_p);
+          y = M2.sqr_k(y, (size_t)W);
+        }
+      } else {
+        // B_k = G^(2^(W k)) as SB limbs (the test build's k_fb / k_fbg tables)
+        o.bl.resize((size_t)K * sb);
+        HBig x = G;
+        for (int k = 0; k < K; ++k) {
+          const std::vector<uint32_t> v = M2.from(x).limbs(sb, LB);
+          std::copy(v.begin(), v.end(), o.bl.begin() + (size_t)k * sb);
+          x = M2.sqr_k(x, (size_t)W);
+        }
+      }
+    };
+    std::thread t1(prep, 1);
+    prep(0);
+    t1.join();
+  }
   for (int h = 0; h < 2; ++h) {
-    if (!c->fb_g[h]) {
-      SetupTrace tr_g("  fb_base (generator search)");
-      if (!(c->fb_g[h] = fb_base(primes[h]))) return fb_unavailable(c, "no base found");
-    }
+    if (!(c->fb_g[h] = hp[h].g)) return fb_unavailable(c, "no base found");
     SetupTrace tr_h("  host prep (one half)");
     const HBig& m2 = sq[h];
-    HMont M2(m2);
-    // B_k = G^(2^(W k)), G = g^n mod p_h^2
-    std::vector<uint32_t> bl((size_t)K * sb);
-    HBig x = M2.to(M2.pow(HBig(c->fb_g[h]), c->n));
-    for (int k = 0; k < K; ++k) {
-      const std::vector<uint32_t> v = M2.from(x).limbs(sb, LB);
-      std::copy(v.begin(), v.end(), bl.begin() + (size_t)k * sb);
-      x = M2.sqr_k(x, (size_t)W);
-    }
+    std::vector<uint32_t>& bl = hp[h].bl;
+    if (bl.empty()) bl.assign(sb, 0u);   // (unused by the pair samplers' builds: a placeholder row)
     // c0 folding: n 2^(CB c) mod p_h^2 (c < NC) and 2^PB p_h^2 (the group kernel uses 74's geometry:
     // 16-bit chunks, PB = 20)
     std::vector<uint32_t> nm;
@@ -1363,11 +1419,11 @@ static int ensure_fb(pai_ctx* c) {
     c->fb_mem.push_back(lohi[h]);
     dlohi = (uint32_t*)lohi[h];
     {
-      SetupTrace tr_m("  table hipMalloc (one half)");
-      if (hipMalloc(&t[h], ((size_t)K << W) * (fb_table_row_words(c) / 4) * sizeof(uint4)) != hipSuccess)
+      SetupTrace tr_m("  table allocation (one half)");
+      if (!(t[h] = TableArena::get().alloc(c->device, ((size_t)K << W) * (fb_table_row_words(c) / 4) * sizeof(uint4))))
         return fb_unavailable(c, "table allocation failed");
     }
-    c->fb_mem.push_back(t[h]);
+    c->fb_tables.push_back(t[h]);
     hv[h] = FbHalf{(const uint4*)t[h], dm, dR2, done, dbases, dlohi, dnm, dpbig, mont_prime(m2, LB)};
     if (pair_ok) {
       // pair constants: (x mod p_h, x div p_h) of Montgomery-form values x = v R mod p_h^2, R = 2^(28 S)
@@ -1379,17 +1435,9 @@ static int ensure_fb(pai_ctx* c) {
         out.insert(out.end(), a.begin(), a.end());
         out.insert(out.end(), b.begin(), b.end());
       };
-      std::vector<uint32_t> one_p, bases_p, nm_p;
+      std::vector<uint32_t> one_p, nm_p;
+      const std::vector<uint32_t>& bases_p = hp[h].bases_p;   // B_k R, B_k^(2^LO) R (host prep above)
       split(mul_pow2_mod(HBig(1), RS, m2), one_p);
-      const int LOb = W / 2;
-      HBig y = M2.to(M2.pow(HBig(c->fb_g[h]), c->n));   // G in M2's domain
-      for (int k = 0; k < K; ++k) {
-        HBig z = y;
-        split(mul_pow2_mod(M2.from(z), RS, m2), bases_p);                 // B_k R
-        z = M2.sqr_k(z, (size_t)LOb);
-        split(mul_pow2_mod(M2.from(z), RS, m2), bases_p);                 // B_k^(2^LO) R
-        y = M2.sqr_k(y, (size_t)W);
-      }
       const HBig other = primes[1 - h];
       std::vector<uint32_t> nmr_p;   // the same times R (k_fbs: gamma R joins the b sum)
       for (int k = 0; k < FBP_NC; ++k) {
@@ -1445,17 +1493,9 @@ static int ensure_fb(pai_ctx* c) {
         out.insert(out.end(), a.begin(), a.end());
         out.insert(out.end(), b.begin(), b.end());
       };
-      std::vector<uint32_t> one_p, bases_p, nm_p;
+      std::vector<uint32_t> one_p, nm_p;
+      const std::vector<uint32_t>& bases_p = hp[h].bases_p;
       split(mul_pow2_mod(HBig(1), RS, m2), one_p);
-      const int LOb = W / 2;
-      HBig y = M2.to(M2.pow(HBig(c->fb_g[h]), c->n));
-      for (int k = 0; k < K; ++k) {
-        HBig z = y;
-        split(mul_pow2_mod(M2.from(z), RS, m2), bases_p);
-        z = M2.sqr_k(z, (size_t)LOb);
-        split(mul_pow2_mod(M2.from(z), RS, m2), bases_p);
-        y = M2.sqr_k(y, (size_t)W);
-      }
       for (int k = 0; k < 4; ++k) {
         const std::vector<uint32_t> v = mul_pow2_mod(mod(primes[1 - h], P), (size_t)16 * k, P).limbs(FBGP_S, LB);
         nm_p.insert(nm_p.end(), v.begin(), v.end());
@@ -1593,8 +1633,8 @@ static int ensure_fb(pai_ctx* c) {
   }
   if (sgs && !(gpair_ok && sgp_enabled())) {   // (a test build's $FLEXPAI_SGP=0 / $FLEXPAI_FB_PAIR=0 context)
     for (uint4*& r : sgs_rows) {
-      c->fb_mem.erase(std::find(c->fb_mem.begin(), c->fb_mem.end(), (void*)r));
-      (void)hipFree(r);
+      c->fb_tables.erase(std::find(c->fb_tables.begin(), c->fb_tables.end(), (void*)r));
+      TableArena::get().free(r);
       r = nullptr;
     }
   }
@@ -1604,8 +1644,8 @@ static int ensure_fb(pai_ctx* c) {
       // the factored rows are complete: k_sgp runs on them (split_sampler bit 3 stays clear)
       if (setup_trace_on()) fprintf(stderr, "flexpai-trace Shoup rows failed (%s): k_sgp at W = %d\n", pai_last_error(), W);
       for (uint4*& r : sgs_rows) {
-        c->fb_mem.erase(std::find(c->fb_mem.begin(), c->fb_mem.end(), (void*)r));
-        (void)hipFree(r);
+        c->fb_tables.erase(std::find(c->fb_tables.begin(), c->fb_tables.end(), (void*)r));
+        TableArena::get().free(r);
         r = nullptr;
       }
     }
@@ -1946,6 +1986,8 @@ static int set_private_impl(pai_ctx* c, HBig p, HBig q) {
 }
 
 void pai_ctx_destroy(pai_ctx* c) { delete c; }
+
+void pai_release_table_cache(void) { TableArena::get().trim(); }
 
 int pai_ctx_set_option(pai_ctx* c, int option, int value) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
@@ -2345,6 +2387,8 @@ static int pfb_choose_window(pai_ctx* c) {
 static void pfb_release(pai_ctx* c) {
   for (void* q : c->pfb_mem) (void)hipFree(q);
   c->pfb_mem.clear();
+  for (void* q : c->pfb_tables) TableArena::get().free(q);
+  c->pfb_tables.clear();
   c->d_pfb = nullptr;
   c->d_sgp_pfb = nullptr;
 }
@@ -2415,11 +2459,13 @@ static int ensure_pfb(pai_ctx* c) {
   if (!pfb_supported(c)) return pfb_unavailable(c, "the public fixed-base kernels need a 1537..2048-bit n");
   const int W = pfb_choose_window(c);
   if (!W) return pfb_unavailable(c, "tables do not fit the device memory budget");
+  SetupTrace tr_all("ensure_pfb");
   const auto t0 = std::chrono::steady_clock::now();
   int K0, KS;
   pfb_digit_counts(c, W, &K0, &KS);
   const int K = K0 + PFB_SHORT * KS;
   const HBig& n = c->n;
+  std::optional<SetupTrace> tr_h(std::in_place, "  pfb host prep (bases, constants)");
   if (c->pfb_bases.empty()) {
     HBig g;
     do {
@@ -2447,7 +2493,9 @@ static int ensure_pfb(pai_ctx* c) {
     const std::vector<uint32_t> v = g.limbs(PFB_S, LB);
     gl.insert(gl.end(), v.begin(), v.end());
   }
+  tr_h.reset();
   pfb_release(c);
+  std::optional<SetupTrace> tr_m(std::in_place, "  pfb uploads + hipMalloc");
   uint32_t *dn, *dx, *done, *dr2, *dgl, *dnw, *dbases, *dlohi;
   uint4* dtab;
   int rc;
@@ -2468,9 +2516,9 @@ static int ensure_pfb(pai_ctx* c) {
   c->pfb_mem.push_back(vb);
   if (hipMalloc(&vl, (size_t)K * 2 * FB_LO * 2 * PFB_S * 4) != hipSuccess) return pfb_unavailable(c, "table allocation failed");
   c->pfb_mem.push_back(vl);
-  if (hipMalloc(&vt, ((size_t)K << W) * PFB_ROW4 * sizeof(uint4)) != hipSuccess)
+  if (!(vt = TableArena::get().alloc(c->device, ((size_t)K << W) * PFB_ROW4 * sizeof(uint4))))
     return pfb_unavailable(c, "table allocation failed");
-  c->pfb_mem.push_back(vt);
+  c->pfb_tables.push_back(vt);
   dbases = (uint32_t*)vb;
   dlohi = (uint32_t*)vl;
   dtab = (uint4*)vt;
@@ -2499,12 +2547,23 @@ static int ensure_pfb(pai_ctx* c) {
     std::vector<SgpHalf> shv{sh};
     if ((rc = upload_pfb(c, shv, &dsgp))) return pfb_unavailable(c, pai_last_error());
   }
+  tr_m.reset();
   const auto t1 = std::chrono::steady_clock::now();
-  if (pfb_build_phase1(dpc, pc.nbases, K, W, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
-    return pfb_unavailable(c, "table construction failed");
-  if (pair_host_invert(n, (uint32_t*)vcv, 2 * K, PFB_S)) return pfb_unavailable(c, pai_last_error());
-  if (pfb_build_phase2(dpc, K, W, dtab, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
-    return pfb_unavailable(c, "table construction failed");
+  {
+    SetupTrace tr_1("  pfb phase 1 (chains, lohi, inv_fwd)");
+    if (pfb_build_phase1(dpc, pc.nbases, K, W, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+      return pfb_unavailable(c, "table construction failed");
+  }
+  {
+    SetupTrace tr_i("  pfb host invert");
+    if (pair_host_invert(n, (uint32_t*)vcv, 2 * K, PFB_S)) return pfb_unavailable(c, pai_last_error());
+  }
+  {
+    SetupTrace tr_2("  pfb phase 2 (inv_bwd, fill)");
+    if (pfb_build_phase2(dpc, K, W, dtab, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+      return pfb_unavailable(c, "table construction failed");
+  }
+  SetupTrace tr_f("  pfb scratch frees");
   for (void* q : {vb, vl, vinv, vpre, vcv}) {   // build scratch
     c->pfb_mem.erase(std::find(c->pfb_mem.begin(), c->pfb_mem.end(), q));
     (void)hipFree(q);

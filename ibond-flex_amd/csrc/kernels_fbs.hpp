@@ -75,8 +75,8 @@ __device__ __forceinline__ void fbs_q_digit(uint64_t (&P)[S + 1], const uint32_t
   const uint32_t d = rd(std::integral_constant<int, T>{});
 #pragma unroll
   for (int i = S - 1 - J; i < S; ++i) P[i + J - (S - 1)] += (uint64_t)X[i] * d;
-#pragma unroll
-  for (int i = 0; i <= S; ++i) asm volatile("" : "+v"(P[i]));
+  // (no empty-asm pins here, unlike step 2: one MAC per column and digit leaves LLVM nothing to re-associate, and
+  // each pinned block cost an s_nop before the next MAC -- round 6, profiles/r06d_ab_fbs_pins_startcols.txt)
   __builtin_amdgcn_sched_barrier(0);
 }
 template <int S, class Rd, int... Ts>
@@ -112,7 +112,7 @@ __device__ __forceinline__ void fbs_r_digit(uint64_t (&P)[S], const uint32_t (&X
     P[i + J] += (uint64_t)q[i] * pb;
   }
 #pragma unroll
-  for (int i = J; i < S; ++i) asm volatile("" : "+v"(P[i]));
+  for (int i = J; i < S; ++i) asm volatile("" : "+v"(P[i]));   // (without them LLVM fuses the two MACs into mul_lo + add3)
   __builtin_amdgcn_sched_barrier(0);
 }
 template <int S, class Rd, int... Js>
@@ -375,20 +375,20 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_fbs(FbpParams p) {
         FbsPairReader<S, G::QAP, G::QA, true, 1> r1{cur};
         fbs_quotient<S>(X, r1, q);
       }
-      {   // step 2; the odd lane's accumulator starts at the even lane's Q_A
+      {   // step 2; the odd lane's accumulator columns start at the even lane's Q_A (one DPP'd AND per limb, before the
+        // digits: round 6, against one DPP, one MAC by 0 / 1 and a DPP hazard nop per limb in the normalisation)
         uint64_t P[S];
+        uint32_t om = odd ? ~0u : 0u;
+        asm volatile("" : "+v"(om));   // (a mask, not a select)
 #pragma unroll
-        for (int i = 0; i < S; ++i) P[i] = 0;   // (the first MACs take a zero addend)
+        for (int i = 0; i < S; ++i)
+          P[i] = (uint64_t)((uint32_t)__builtin_amdgcn_update_dpp(0, (int)q[i], 0xA0, 0xF, 0xF, false) & om);   // quad_perm [0,0,2,2]
         FbsPairReader<S, G::QA, 0, false, 1> r2{cur};
         fbs_r_all<S>(P, X, q, m, r2, std::make_integer_sequence<int, S>{});
-        // normalise, the odd lane adding the even lane's Q_A on the way: one DPP and one MAC by 0 / 1 per limb
-        uint32_t ob = odd ? 1u : 0u;
-        asm volatile("" : "+v"(ob));   // (a multiplier, not a select)
         uint64_t c = 0;   // (mod R: the carry out of limb S - 1 is dropped)
 #pragma unroll
         for (int i = 0; i < S; ++i) {
-          const uint32_t qa = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q[i], 0xA0, 0xF, 0xF, false);   // quad_perm [0,0,2,2]
-          const uint64_t v = P[i] + c + (uint64_t)qa * ob;
+          const uint64_t v = P[i] + c;
           X[i] = lane::limb32(v);
           c = v >> lane::LB;
         }

@@ -40,7 +40,7 @@ EXPORTED = ("pai_device_count", "pai_device_mem_info", "pai_ctx_create", "pai_ct
             "pai_encrypt", "pai_add", "pai_decrypt", "pai_encrypt_dev", "pai_add_dev", "pai_decrypt_dev",
             "pai_mul", "pai_mul_dev", "pai_matmul", "pai_matmul_dev", "pai_add_plain", "pai_add_plain_dev",
             "pai_segment_add", "pai_segment_add_dev", "pai_comm_unique_id", "pai_comm_create", "pai_comm_destroy",
-            "pai_allgather_dev", "pai_allgather_shards_dev")
+            "pai_allgather_dev", "pai_allgather_shards_dev", "pai_release_table_cache")
 PAI_COMM_ID_BYTES = 128
 
 _lib = None
@@ -106,13 +106,21 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.pai_comm_destroy.restype = None
         lib.pai_allgather_dev.argtypes = [P, P, S, P, P]
         lib.pai_allgather_shards_dev.argtypes = [P, P, P, S, I, P, P, P]
+        lib.pai_release_table_cache.argtypes = []
+        lib.pai_release_table_cache.restype = None
         for name in EXPORTED:
-            if name not in ("pai_ctx_destroy", "pai_last_error", "pai_comm_destroy"):
+            if name not in ("pai_ctx_destroy", "pai_last_error", "pai_comm_destroy", "pai_release_table_cache"):
                 getattr(lib, name).restype = ctypes.c_int
         _libs[path] = lib
         if path == LIB_PATH:
             _lib = lib
         return lib
+
+
+def release_table_cache() -> None:
+    """Give the device memory of released fixed-base tables back to the driver now (csrc/table_arena.hpp: the library
+    keeps it for the process's next table build until its last context is destroyed)."""
+    load_library().pai_release_table_cache()
 
 
 def _start_torch_runtime_first() -> None:

@@ -148,6 +148,11 @@ int pai_device_mem_info(int device, uint64_t* free_bytes, uint64_t* total_bytes)
 int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** out);
 int pai_ctx_set_private(pai_ctx* ctx, const uint8_t* p_le, const uint8_t* q_le, size_t half_bytes);
 void pai_ctx_destroy(pai_ctx* ctx);
+/* Fixed-base tables live in device memory the library keeps when they are released (a window change, a context's
+ * end): the next table build in the process maps it again instead of waiting for the driver to wipe released memory
+ * (csrc/table_arena.hpp). It goes back to the driver when the process's last context is destroyed, or now with this
+ * call (no context may be building tables concurrently). $FLEXPAI_TABLE_POOL=0: plain hipMalloc / hipFree. */
+void pai_release_table_cache(void);
 /* Encryption with the private key set uses CRT over p^2, q^2 (same ciphertext bits, ~4x fewer
  * multiply-accumulates); PAI_OPT_CRT_ENCRYPT = 0 forces the public-key kernel. */
 int pai_ctx_set_option(pai_ctx* ctx, int option, int value);

@@ -44,6 +44,10 @@ print(json.dumps(out))
 
 
 def _child(mode, **env):
+    # the device as an idle MI355X: this (parent) process hands the chunks of tables earlier tests released back to the
+    # driver first (csrc/table_arena.hpp keeps them for its own rebuilds until its last context is destroyed)
+    from flex.crypto.paillier import _native as N
+    N.release_table_cache()
     e = dict(os.environ, **env)
     r = subprocess.run([sys.executable, "-c", CHILD, ROOT, mode], env=e, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]

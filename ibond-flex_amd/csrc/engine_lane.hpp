@@ -9,6 +9,5 @@ namespace fpai {
 int crt_lane_occupancy(int sa, int* occ_a, int* occ_b);
 // k_crt_a<sa> / k_crt_b<sa, 2 sa> on grid (gx, 2)
 hipError_t crt_launch_a(int sa, const CrtParams& p, int gx, hipStream_t st);
-hipError_t crt_launch_b(int sa, const CrtParams& p, int gx, hipStream_t st);
 
 }  // namespace fpai

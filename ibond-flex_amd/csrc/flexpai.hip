@@ -28,8 +28,9 @@
 #include "engine_fbs.hpp"
 
 // FLEXPAI_XCHECK (the test-only library libflexpai_xcheck.so, __graft_entry__.build): the kernel generations the
-// pair kernels replaced -- k_fb/k_fb_fin, k_fbg, k_fbgp, k_pfb, k_fbp, the 2S-limb k_dec_* and k_crt_b -- and k_debug,
-// selected by $FLEXPAI_FB_PAIR=0 / $FLEXPAI_SGP=0 / $FLEXPAI_FBS=0 / $FLEXPAI_PAIR=0, so that the tests can cross-check the shipping
+// pair kernels replaced -- k_fbgp, k_pfb, k_fbp (k_fb/k_fb_fin, k_fbg and the 2S-limb k_dec_* / k_crt_b were retired in
+// round 6) -- and k_debug, selected by $FLEXPAI_SGP=0 / $FLEXPAI_FBS=0 ($FLEXPAI_PAIR=0: the group-engine decryption and
+// the public-key encryption kernels of the product), so that the tests can cross-check the shipping
 // kernels against them. The product library (FLEXPAI_XCHECK 0) does not contain them and ignores those variables.
 #ifndef FLEXPAI_XCHECK
 #define FLEXPAI_XCHECK 0
@@ -98,8 +99,6 @@ struct pai_ctx {
   // lane-engine CRT decryption (kernels_dec.hpp): same sizes as the CRT encryption halves
   bool dec_lane_ok = false;
   bool dec_lane_enabled = true;
-  int dec_kchunks = 0;
-  DecLaneHalf* d_dec_halves = nullptr;
   // p-adic pair exponentiations (kernels_pair.hpp): decryption and CRT stage B on the S limbs of p_h;
   // the default for 1024/2048-bit keys ($FLEXPAI_PAIR=0 selects the 2S-limb lane kernels)
   bool dec_pair_ok = false, crt_pair_ok = false;
@@ -119,8 +118,7 @@ struct pai_ctx {
   PeConst* d_pe = nullptr;
   uint32_t *d_pe_n = nullptr, *d_pe_r2 = nullptr, *d_pe_oneR = nullptr;   // n, R^2, R mod n (R = 2^(28 74)): the batch
   uint32_t pe_mprime = 0;                                                 //   inversion of the bases mod n (TPI = 2)
-  CrtHalf* d_dec_pow = nullptr;   // [2] exponentiation halves: p_h^2, op list for p_h - 1
-  uint32_t *d_dec_p = nullptr, *d_dec_q = nullptr, *d_dec_qinvR = nullptr, *d_dec_nl = nullptr, *d_dec_maxint = nullptr;
+  uint32_t *d_dec_p = nullptr, *d_dec_q = nullptr, *d_dec_qinvR = nullptr;   // (k_dec_fin_pair's CRT constants)
   uint32_t dec_pprime = 0;
   // fixed-base obfuscation (kernels_fb.hpp): device-RNG encryption for key holders. Built lazily on
   // the first PAI_OBF_RNG encryption (or pai_ctx_fixed_base_prepare); any failure (key shape, table
@@ -1075,11 +1073,9 @@ static int fb_row_words(int sb) {
 }
 
 // 4096-bit keys: the pair-group sampler (kernels_grp_pair.hpp) runs when both p_h fit its 76 limbs with
-// R >= 2^24 p_h ($FLEXPAI_FB_PAIR=0 selects k_fbg); its rows are the canonical pair as 2 x 64 words
+// R >= 2^24 p_h; its rows are the canonical pair as 2 x 64 words
 static bool fb_gpair_possible(const pai_ctx* c) {
   if (c->crt_sb != GRP_TPI * L) return false;
-  if (const char* e = xcheck_env("FLEXPAI_FB_PAIR"))
-    if (atoi(e) == 0) return false;
   for (const HBig* h : {&c->fb_p, &c->fb_q})
     if (h->bits() + 24 > (size_t)LB * FBGP_S || h->bits() > (size_t)LB * FBGP_SP || h->bits() > (size_t)32 * FBGP_PW)
       return false;
@@ -1089,13 +1085,11 @@ static bool fb_gpair_possible(const pai_ctx* c) {
 static int fb_row_words(const pai_ctx* c) { return fb_gpair_possible(c) ? 4 * FBGP_ROW4 : fb_row_words(c->crt_sb); }
 
 // 1024/2048-bit keys: the pair tables (kernels_fbp.hpp) need p_h < 2^(32 PW) and R = 2^(28 S) >= 2^12 p_h (bounds of
-// the first product, kernels_fbp.hpp); $FLEXPAI_FB_PAIR=0 selects k_fb. Returns S (19 or 37), or 0.
+// the first product, kernels_fbp.hpp). Returns S (19 or 37), or 0.
 static int fb_pair_possible(const pai_ctx* c) {
   const int sb = c->crt_sb;
   const int ps = sb == 37 ? 19 : sb == 74 ? 37 : 0;
   if (!ps) return 0;
-  if (const char* e = xcheck_env("FLEXPAI_FB_PAIR"))
-    if (atoi(e) == 0) return 0;
   const int pw = ps == 19 ? FbpGeom<19>::PW : FbpGeom<37>::PW;
   for (const HBig* h : {&c->fb_p, &c->fb_q})
     if (h->bits() > (size_t)32 * pw || h->bits() + FBP_PB + 1 > (size_t)LB * ps) return 0;
@@ -1319,12 +1313,16 @@ static int ensure_fb(pai_ctx* c) {
   const int ps = grp ? 0 : fb_pair_possible(c);
   const bool pair_ok = ps != 0;
   const bool shoup = pair_ok && fb_shoup_possible(c);
-#if !FLEXPAI_XCHECK
+#if FLEXPAI_XCHECK
+  if (!grp && !pair_ok) return fb_unavailable(c, "key outside the pair sampler's bounds");
+#else
   if (!grp && !shoup) return fb_unavailable(c, "key outside the pair sampler's bounds");
 #endif
   // 4096-bit keys: pair products on lane groups of 4 x 19 limbs (kernels_grp_pair.hpp), R = 2^(28 76) >= 2^24 p_h
   const bool gpair_ok = grp && fb_gpair_possible(c);
-#if !FLEXPAI_XCHECK
+#if FLEXPAI_XCHECK
+  if (grp && !gpair_ok) return fb_unavailable(c, "key outside the pair-group sampler's bounds");
+#else
   if (grp && !(gpair_ok && sgp_enabled())) return fb_unavailable(c, "key outside the split-pair sampler's bounds");
 #endif
   const int lohi_limbs = pair_ok ? std::max(sb, 2 * ps) : gpair_ok ? std::max(sb, 2 * FBGP_S) : sb;
@@ -1346,7 +1344,7 @@ static int ensure_fb(pai_ctx* c) {
   // fresh key's setup, HE_SA_FT re-keys per exchange; round 6: the pair paths had computed G and the B_k twice)
   struct HalfPrep {
     uint32_t g = 0;
-    std::vector<uint32_t> bl, bases_p;
+    std::vector<uint32_t> bases_p;
   };
   HalfPrep hp[2];
   {
@@ -1364,26 +1362,15 @@ static int ensure_fb(pai_ctx* c) {
       const HBig& m2 = sq[h];
       HMont M2(m2);
       const HBig G = M2.to(M2.pow(HBig(o.g), c->n));
-      if (pair_ok || gpair_ok) {
-        // pair constants: (x mod p_h, x div p_h) of Montgomery-form values x = v R mod p_h^2: B_k R and B_k^(2^LO) R
-        const HBig& P = primes[h];
-        const int limbs = pair_ok ? ps : FBGP_S;
-        const size_t RS = (size_t)LB * limbs;
-        HBig y = G;
-        for (int k = 0; k < K; ++k) {
-          split_into(mul_pow2_mod(M2.from(y), RS, m2), P, limbs, o.bases_p);
-          split_into(mul_pow2_mod(M2.from(M2.sqr_k(y, (size_t)(W / 2))), RS, m2), P, limbs, o.bases_p);
-          y = M2.sqr_k(y, (size_t)W);
-        }
-      } else {
-        // B_k = G^(2^(W k)) as SB limbs (the test build's k_fb / k_fbg tables)
-        o.bl.resize((size_t)K * sb);
-        HBig x = G;
-        for (int k = 0; k < K; ++k) {
-          const std::vector<uint32_t> v = M2.from(x).limbs(sb, LB);
-          std::copy(v.begin(), v.end(), o.bl.begin() + (size_t)k * sb);
-          x = M2.sqr_k(x, (size_t)W);
-        }
+      // pair constants: (x mod p_h, x div p_h) of Montgomery-form values x = v R mod p_h^2: B_k R and B_k^(2^LO) R
+      const HBig& P = primes[h];
+      const int limbs = pair_ok ? ps : FBGP_S;
+      const size_t RS = (size_t)LB * limbs;
+      HBig y = G;
+      for (int k = 0; k < K; ++k) {
+        split_into(mul_pow2_mod(M2.from(y), RS, m2), P, limbs, o.bases_p);
+        split_into(mul_pow2_mod(M2.from(M2.sqr_k(y, (size_t)(W / 2))), RS, m2), P, limbs, o.bases_p);
+        y = M2.sqr_k(y, (size_t)W);
       }
     };
     std::thread t1(prep, 1);
@@ -1394,8 +1381,7 @@ static int ensure_fb(pai_ctx* c) {
     if (!(c->fb_g[h] = hp[h].g)) return fb_unavailable(c, "no base found");
     SetupTrace tr_h("  host prep (one half)");
     const HBig& m2 = sq[h];
-    std::vector<uint32_t>& bl = hp[h].bl;
-    if (bl.empty()) bl.assign(sb, 0u);   // (unused by the pair samplers' builds: a placeholder row)
+    const std::vector<uint32_t> bl(sb, 0u);   // FbHalf::bases: no sampler left reads them (a placeholder row)
     // c0 folding: n 2^(CB c) mod p_h^2 (c < NC) and 2^PB p_h^2 (the group kernel uses 74's geometry:
     // 16-bit chunks, PB = 20)
     std::vector<uint32_t> nm;
@@ -1611,12 +1597,10 @@ static int ensure_fb(pai_ctx* c) {
   }
   SetupTrace tr_2("  phase 2 (inv_bwd, fill) + frees");
 #if FLEXPAI_XCHECK
-  const hipError_t be = gpair_ok  ? fbgp_build_phase2(c->d_fbgp_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
-                        : grp     ? grp_build_tables(c->d_fb_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
-                        : shoup   ? fbs_build_phase2(ps, c->d_fbp_halves, c->d_fbs_cst, (uint4*)t[0], (uint4*)t[1], K, W, nullptr,
-                                                     guard_args(c, (unsigned long long)K << W, 0, 0, 0))
-                        : pair_ok ? fbp_build_phase2(ps, c->d_fbp_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr)
-                                  : fb_build_tables(sb, c->d_fb_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
+  const hipError_t be = gpair_ok ? fbgp_build_phase2(c->d_fbgp_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
+                        : shoup  ? fbs_build_phase2(ps, c->d_fbp_halves, c->d_fbs_cst, (uint4*)t[0], (uint4*)t[1], K, W, nullptr,
+                                                    guard_args(c, (unsigned long long)K << W, 0, 0, 0))
+                                 : fbp_build_phase2(ps, c->d_fbp_halves, (uint4*)t[0], (uint4*)t[1], K, W, nullptr);
 #else
   const hipError_t be = gpair_ok ? fbgp_build_phase2(c->d_fbgp_halves, (uint32_t*)t[0], (uint32_t*)t[1], K, W, nullptr)
                                  : fbs_build_phase2(ps, c->d_fbp_halves, c->d_fbs_cst, (uint4*)t[0], (uint4*)t[1], K, W, nullptr,
@@ -1631,7 +1615,7 @@ static int ensure_fb(pai_ctx* c) {
     c->fb_mem.erase(std::find(c->fb_mem.begin(), c->fb_mem.end(), p));
     (void)hipFree(p);
   }
-  if (sgs && !(gpair_ok && sgp_enabled())) {   // (a test build's $FLEXPAI_SGP=0 / $FLEXPAI_FB_PAIR=0 context)
+  if (sgs && !(gpair_ok && sgp_enabled())) {   // (a test build's $FLEXPAI_SGP=0 context)
     for (uint4*& r : sgs_rows) {
       c->fb_tables.erase(std::find(c->fb_tables.begin(), c->fb_tables.end(), (void*)r));
       TableArena::get().free(r);
@@ -1785,48 +1769,15 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
   c->crt_ok = true;
   c->fb_p = p;   // the fixed-base tables are built lazily (ensure_fb)
   c->fb_q = q;
-  // lane-engine decryption: x_h = c^(p_h - 1) mod p_h^2, L_h, m_h = L_h h_h mod p_h; CRT + decode
+  // lane decryption's CRT constants (p, q, q^-1 R mod p), shared by the pair kernels' k_dec_fin_pair
   {
     SetupTrace tr_d("    lane decrypt consts");
-    const int kd = (int)((32 * (size_t)c->ct_words + RB - 1) / RB);
-    if (kd > KMAX_CHUNKS) return 0;
-    DecLaneHalf dh[2];
-    CrtHalf ph_pow[2];
-    for (int h = 0; h < 2; ++h) {
-      const HBig& ph = primes[h];
-      const HBig& other = primes[1 - h];
-      const HBig& m2 = sq[h];
-      std::vector<uint32_t> pd;
-      if (!build_lane_program(sub(ph, HBig(1)), pd)) return 0;
-      // h_h = L(g^(p_h - 1) mod p_h^2, p_h)^-1 mod p_h = (-other)^-1 mod p_h (g = n + 1)
-      HBig oi = inv_mod(mod(other, ph), ph);
-      if (oi.is_zero()) return 0;
-      HBig hh = sub(ph, oi);
-      std::vector<uint32_t> one(sb, 0);
-      one[0] = 1;
-      uint32_t *dm2, *dck, *done, *dprog, *dph, *dhR, *dpm1;
-      if ((rc = upload(c, m2.limbs(sb, LB), &dm2)) ||
-          (rc = upload(c, mul_pow2_mod(HBig(1), RB * (kd + 1), m2).limbs(sb, LB), &dck)) ||
-          (rc = upload(c, one, &done)) || (rc = upload(c, pd, &dprog)) || (rc = upload(c, ph.limbs(sa, LB), &dph)) ||
-          (rc = upload(c, mul_pow2_mod(hh, RA, ph).limbs(sa, LB), &dhR)) ||
-          (rc = upload(c, sub(ph, HBig(1)).limbs(sa, LB), &dpm1)))
-        return rc;
-      const uint32_t mp1 = mont_prime(ph, LB), mp2 = mont_prime(m2, LB);
-      dh[h] = DecLaneHalf{dm2, dck, mp2, (0u - mp1) & LMASK, mp1, 0u, dph, dhR, dpm1};
-      ph_pow[h] = CrtHalf{dm2, nullptr, done, dprog, (int)pd.size(), mp2};
-    }
-    std::vector<DecLaneHalf> dv(dh, dh + 2);
-    std::vector<CrtHalf> pv(ph_pow, ph_pow + 2);
-    if ((rc = upload(c, pv, &c->d_dec_pow))) return rc;
+    if ((int)((32 * (size_t)c->ct_words + RB - 1) / RB) > KMAX_CHUNKS) return 0;
     HBig qinv = inv_mod(mod(q, p), p);
-    HBig maxint = sub(div_small(c->n, 3), HBig(1));   // keypair.py:29
-    if ((rc = upload(c, dv, &c->d_dec_halves)) || (rc = upload(c, p.limbs(sa, LB), &c->d_dec_p)) ||
-        (rc = upload(c, q.limbs(sa, LB), &c->d_dec_q)) ||
-        (rc = upload(c, mul_pow2_mod(qinv, RA, p).limbs(sa, LB), &c->d_dec_qinvR)) ||
-        (rc = upload(c, c->n.limbs(sb, LB), &c->d_dec_nl)) || (rc = upload(c, maxint.limbs(sb, LB), &c->d_dec_maxint)))
+    if ((rc = upload(c, p.limbs(sa, LB), &c->d_dec_p)) || (rc = upload(c, q.limbs(sa, LB), &c->d_dec_q)) ||
+        (rc = upload(c, mul_pow2_mod(qinv, RA, p).limbs(sa, LB), &c->d_dec_qinvR)))
       return rc;
     c->dec_pprime = mont_prime(p, LB);
-    c->dec_kchunks = kd;
     c->dec_lane_ok = true;
   }
   // pair kernels: residues mod p_h^2 as (A, B) over the sa limbs of p_h, R = 2^(28 sa) >= 2^12 p_h
@@ -1975,13 +1926,11 @@ static int set_private_impl(pai_ctx* c, HBig p, HBig q) {
   c->has_priv = true;
   SetupTrace tr("  setup_crt");
   if ((rc = setup_crt(c, p, q))) return rc;
-#if !FLEXPAI_XCHECK
-  // a key outside the pair kernels' bounds (R = 2^(28 S) >= 2^12 p_h): CRT encryption and lane decryption would
-  // need the 2S-limb kernels of the test build; it encrypts on the public-key kernels and decrypts on the group
-  // engine instead
+  // a key outside the pair kernels' bounds (R = 2^(28 S) >= 2^12 p_h) -- or a test build's $FLEXPAI_PAIR=0 context --
+  // encrypts on the public-key kernels and decrypts on the group engine (the 2S-limb lane kernels were retired in
+  // round 6)
   if (c->crt_ok && !c->crt_pair_ok) c->crt_ok = false;
   if (c->dec_lane_ok && !c->dec_pair_ok) c->dec_lane_ok = false;
-#endif
   return 0;
 }
 
@@ -2185,12 +2134,9 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
   const long long chunk = std::min(N, CRT_CHUNK);
   int occF = 1, occG = 1;
 #if FLEXPAI_XCHECK
-  if (grp) {
-    if (c->fb_gpair) fbgp_occupancy(&occF);
-    else grp_occupancy(&occF);
-  } else if (!c->fb_pair_s && fb_occupancy(SB, &occF, &occG)) {
-    return fail(PAI_ERR_KEY, "fixed-base encrypt: unsupported size");
-  }
+  if (grp && !c->fb_gpair) return fail(PAI_ERR_KEY, "fixed-base encrypt: no pair tables");
+  if (grp && !c->d_sgp_fb) fbgp_occupancy(&occF);
+  if (!grp && !c->fb_pair_s) return fail(PAI_ERR_KEY, "fixed-base encrypt: no pair tables");
 #else
   if (grp && !(c->fb_gpair && c->d_sgp_fb)) return fail(PAI_ERR_KEY, "fixed-base encrypt: no split-pair tables");
   if (!grp && !c->fb_shoup) return fail(PAI_ERR_KEY, "fixed-base encrypt: no Shoup tables");
@@ -2288,10 +2234,6 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
         HIPCHK(fbgp_launch(pg, gF, st));
 #endif
       }
-    } else {
-#if FLEXPAI_XCHECK
-      HIPCHK(grp ? grp_launch_fb(pf, gF, st) : fb_launch(SB, pf, gF, st));
-#endif
     }
     stage_mark(c, 2, st);
     c->fb_last_w = w;
@@ -2337,22 +2279,7 @@ static int launch_fb(pai_ctx* c, const EncParams& e, hipStream_t st) {
       stage_mark(c, 3, st);
       continue;
     }
-#if FLEXPAI_XCHECK
-    FbFinParams pg{};
-    pg.w = w;
-    pg.n = n;
-    pg.m = c->d_fb_m0;
-    pg.mprime = c->fb_mprime0;
-    pg.m8 = c->d_fb_m8;
-    pg.coefR = c->d_fb_coefR;
-    pg.q2 = c->d_fb_q2;
-    pg.ct = e.ct + (size_t)off * c->ct_words;
-    pg.ct_words = c->ct_words;
-    HIPCHK(fb_launch_fin(SB, pg, (int)std::min<long long>(gxG, (n + LANE_BLOCK - 1) / LANE_BLOCK), st));
-    stage_mark(c, 3, st);
-#else
     (void)gxG;
-#endif
   }
   return 0;
 }
@@ -2861,10 +2788,7 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
     pb.out = u;
     pb.scratch = (uint32_t*)c->d_scratch;
     const int gB = (int)std::min<long long>(gxB, (n + LANE_BLOCK - 1) / LANE_BLOCK);
-    if (bpair) HIPCHK(crt_b_pair_launch(SA, pb, gB, st));
-#if FLEXPAI_XCHECK
-    else HIPCHK(crt_launch_b(SA, pb, gB, st));
-#endif
+    HIPCHK(crt_b_pair_launch(SA, pb, gB, st));
     HIPCHK(hipGetLastError());
     stage_mark(c, 2, st);
     CrtFinParams f{};
@@ -3116,51 +3040,6 @@ static int launch_dec4(pai_ctx* c, const DecParams& d, hipStream_t st) {
   return 0;
 }
 
-#if FLEXPAI_XCHECK
-// lane-engine decryption (kernels_dec.hpp, engine_dec.hip), in chunks of CRT_CHUNK elements
-static int launch_dec_lane(pai_ctx* c, const DecParams& d, hipStream_t st) {
-  const long long N = d.n;
-  const long long chunk = std::min(N, CRT_CHUNK);
-  DecLaneGeom g;
-  if (dec_lane_geometry(c->crt_sa, c->cus, chunk, &g)) return fail(PAI_ERR_KEY, "lane decrypt: unsupported size");
-  int rc = ensure_scratch(c, g.scratch_bytes);
-  if (rc) return rc;
-  const int SB = c->crt_sb;
-  if ((rc = ensure_work(c, (size_t)2 * SB * chunk * 4))) return rc;
-  for (long long off = 0; off < N; off += chunk) {
-    const long long n = std::min(chunk, N - off);
-    hipEvent_t* ev = stage_chunk(c);
-    if (ev) c->nev = 4;
-    uint32_t* xw = (uint32_t*)c->d_work;   // [2][SB][n]: c~, then x_h in place
-    DecPreParams pre{c->d_dec_halves, n, d.ct + (size_t)off * c->ct_words, c->ct_words, c->dec_kchunks, xw};
-    CrtParams pw{};
-    pw.halves = c->d_dec_pow;
-    pw.n = n;
-    pw.yin = xw;
-    pw.out = xw;
-    pw.scratch = (uint32_t*)c->d_scratch;
-    DecFinParams f{};
-    f.halves = c->d_dec_halves;
-    f.n = n;
-    f.xh = xw;
-    f.exp = d.exp + off;
-    f.p = c->d_dec_p;
-    f.q = c->d_dec_q;
-    f.qinvR = c->d_dec_qinvR;
-    f.pprime = c->dec_pprime;
-    f.nlimb = c->d_dec_nl;
-    f.maxint = c->d_dec_maxint;
-    f.val = d.val + off;
-    f.mant = d.mant ? d.mant + off : nullptr;
-    f.status = d.status + off;
-    f.raw = d.raw ? d.raw + (size_t)off * c->pt_words : nullptr;
-    f.pt_words = c->pt_words;
-    HIPCHK(dec_lane_launch(c->crt_sa, pre, pw, f, g, st, ev));
-  }
-  return 0;
-}
-#endif
-
 int pai_decrypt_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size_t N, double* d_val, int64_t* d_mant,
                     int32_t* d_status, uint32_t* d_raw, void* stream) {
   if (!c) return fail(PAI_ERR_ARG, "null ctx");
@@ -3191,9 +3070,6 @@ int pai_decrypt_dev(pai_ctx* c, const uint32_t* d_ct, const int32_t* d_exp, size
   hipStream_t st = (hipStream_t)stream;
   if (c->dec_pair_ok && c->dec_lane_enabled) return launch_dec_pair(c, p, st);
   if (c->dec4_ok && c->dec_lane_enabled) return launch_dec4(c, p, st);
-#if FLEXPAI_XCHECK
-  if (c->dec_lane_ok && c->dec_lane_enabled) return launch_dec_lane(c, p, st);
-#endif
   switch (c->tpi_d) {
     case 1: return launch_decrypt<1>(c, p, st);
     case 2: return launch_decrypt<2>(c, p, st);

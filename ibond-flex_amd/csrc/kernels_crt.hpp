@@ -9,7 +9,8 @@
 // r^n == u_p q^2 + u_q p^2 (mod n^2). Per element this is ~4x fewer MACs than the 4096-bit
 // modexp of the public path. Three kernels:
 //   k_crt_a<SA>   mod p_h, one element per lane (bn_lane.hpp), 1024-bit exponent  -> y_h
-//   k_crt_b<SB>   mod p_h^2, one element per lane, exponent p_h, times the CRT coefficient -> u_h
+//   stage B       mod p_h^2, exponent p_h, times the CRT coefficient -> u_h: k_crt_b_pair (kernels_pair.hpp, on
+//                 p-adic pairs; the 2S-limb k_crt_b that first did it was retired in round 6)
 //   k_crt_fin<TPI> lane groups mod n^2 (bn_group.hpp): (u_p q^2 + u_q p^2) * c0 with c0 = 1 + n m
 // blockIdx.y selects the half (p or q), so modulus, exponent schedule and constants are
 // wave-uniform: the modulus limbs live in SGPRs and the sliding window is a scalar op list.
@@ -253,40 +254,6 @@ __global__ __launch_bounds__(LANE_BLOCK, LANE_OCC) void k_crt_a(CrtParams p) {
     if (i < p.n) {
 #pragma unroll
       for (int j = 0; j < SA; ++j) p.out[((size_t)half * SA + j) * p.n + i] = a[j];
-    }
-  }
-}
-
-// ---------------------------------------------------------------- stage B: u_h = y^(p_h) * coef mod p_h^2
-template <int SA, int SB>
-__global__ __launch_bounds__(LANE_BLOCK, LANE_OCC) void k_crt_b(CrtParams p) {
-  const int half = blockIdx.y;
-  const CrtHalf* H = p.halves + half;
-  uint32_t m[SB];
-#pragma unroll
-  for (int j = 0; j < SB; ++j) m[j] = H->m[j];
-  const uint32_t mprime = H->mprime;
-  const int nprog = H->nprog;
-  const uint32_t* prog = H->prog;
-  const uint32_t* c1 = H->c1;
-  const LaneScratch tl = lane_scratch(p.scratch);
-  for (long long base = (long long)blockIdx.x * LANE_BLOCK; base < p.n; base += (long long)gridDim.x * LANE_BLOCK) {
-    const long long i = base + threadIdx.x;
-    const long long ii = i < p.n ? i : p.n - 1;
-    uint32_t a[SB];
-#pragma unroll
-    for (int j = 0; j < SB; ++j) a[j] = j < SA ? p.yin[((size_t)half * SA + j) * p.n + ii] : 0u;
-    {
-      uint32_t b[SB];
-#pragma unroll
-      for (int j = 0; j < SB; ++j) b[j] = H->c0[j];
-      lane::mont_mul<SB>(a, b, m, mprime);                       // y~ = y R mod p_h^2
-    }
-    ltile_store<SB>(tl, 0, a);
-    run_lane_program<SB>(a, tl, prog, nprog, c1, m, mprime);     // y~^(p_h) * coef R^-1
-    if (i < p.n) {
-#pragma unroll
-      for (int j = 0; j < SB; ++j) p.out[((size_t)half * SB + j) * p.n + i] = a[j];
     }
   }
 }

@@ -339,10 +339,13 @@ def test_c_abi_exports_every_declared_symbol():
     _native.load_library()
 
 
-# mangled names of the kernel generations the pair kernels replaced, and of k_debug
-LEGACY_KERNELS = (b"_ZN4fpai4k_fbILi", b"_ZN4fpai8k_fb_finILi", b"_ZN4fpai5k_fbgILi", b"_ZN4fpai6k_fbgpILi",
-                  b"_ZN4fpai5k_pfbILi", b"_ZN4fpai9k_dec_preILi", b"_ZN4fpai9k_dec_powILi", b"_ZN4fpai9k_dec_finILi",
-                  b"_ZN4fpai7k_crt_bILi", b"_ZN4fpai7k_debugILi", b"_ZN4fpai5k_fbpILi", b"_ZN4fpai10k_fbp_fillILi")
+# mangled names of the kernel generations the pair kernels replaced that the test build keeps, and of k_debug
+LEGACY_KERNELS = (b"_ZN4fpai6k_fbgpILi", b"_ZN4fpai5k_pfbILi", b"_ZN4fpai7k_debugILi", b"_ZN4fpai5k_fbpILi",
+                  b"_ZN4fpai10k_fbp_fillILi")
+# retired in round 6: in neither library
+RETIRED_KERNELS = (b"_ZN4fpai4k_fbILi", b"_ZN4fpai8k_fb_finILi", b"_ZN4fpai5k_fbgILi", b"_ZN4fpai9k_dec_preILi",
+                   b"_ZN4fpai9k_dec_powILi", b"_ZN4fpai9k_dec_finILi", b"_ZN4fpai7k_crt_bILi", b"_ZN4fpai9k_fb_lohiILi",
+                   b"_ZN4fpai9k_fb_fillILi", b"_ZN4fpai10k_fbg_lohiILi", b"_ZN4fpai10k_fbg_fillILi")
 
 
 def test_product_library_carries_no_superseded_kernels():
@@ -356,6 +359,8 @@ def test_product_library_carries_no_superseded_kernels():
     for k in LEGACY_KERNELS:
         assert k not in prod, k
         assert k in xck, k
+    for k in RETIRED_KERNELS:
+        assert k not in prod and k not in xck, k
     for k in (b"_ZN4fpai5k_fbsILi", b"_ZN4fpai9k_fbp_finILi", b"_ZN4fpai5k_sgp", b"_ZN4fpai14k_dec_pow_pairILi"):
         assert k in prod, k
 

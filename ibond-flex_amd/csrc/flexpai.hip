@@ -2509,11 +2509,12 @@ static int ensure_pfb(pai_ctx* c) {
   return 1;
 }
 
-// Break-even of the public tables, from measurements on one MI355X (round 5, tools/pfb_breakeven.py,
-// profiles/r05_pfb_breakeven_before.json): the build takes 0.114 s + 1.91 ns per row (0.117 / 0.155 / 0.648 s at
-// W = 12 / 16 / 20), and each element then costs 1 / rate(W) on k_sgp (3.05 M / 4.00 M / 4.84 M enc/s) instead of
-// 1 / 503 k on k_pe_* -- 1.99 us -- so the break-even is ~89 k elements at the default W = 16 (the earlier
-// constants were round 3's 415 k and 2.5 M)
+// Break-even of the public tables, from measurements on one MI355X (tools/pfb_breakeven.py): the build takes 0.114 s +
+// 1.91 ns per row on memory the process has not released before (0.117 / 0.155 / 0.648 s at W = 12 / 16 / 20, round 5,
+// profiles/r05_pfb_breakeven_before.json; round 6: 0.094 / 0.137 s at W = 12 / 16), and each element then costs
+// 1 / rate(W) on k_sgp (round 6, the final library: 3.00 M / 3.93 M / 4.78 M enc/s, profiles/r06e_pfb_breakeven.json)
+// instead of 1 / 552 k on the factored k_pe_* chain (round 5's 503 k predated that chain) -- 1.81 us -- so the
+// break-even is ~100 k elements at the default W = 16
 static long long pfb_threshold(pai_ctx* c) {
   if (c->pfb_state != pai_ctx::FB_UNTRIED || !pfb_supported(c)) return 0;
   if (const char* e = getenv("FLEXPAI_PFB_MIN_ELEMS")) return atoll(e);
@@ -2522,8 +2523,8 @@ static long long pfb_threshold(pai_ctx* c) {
   int K0, KS;
   pfb_digit_counts(c, W, &K0, &KS);
   const double build_s = 0.114 + (double)(K0 + PFB_SHORT * KS) * (double)(1ull << W) * 1.91e-9;
-  const double rate = W >= 20 ? 4.84e6 : W >= 16 ? 4.00e6 : 3.05e6;
-  const double save_s = 1.0 / 5.03e5 - 1.0 / rate;
+  const double rate = W >= 20 ? 4.78e6 : W >= 16 ? 3.93e6 : 3.00e6;
+  const double save_s = 1.0 / 5.52e5 - 1.0 / rate;
   return (long long)(build_s / save_s) + 1;
 }
 

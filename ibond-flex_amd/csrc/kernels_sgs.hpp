@@ -25,9 +25,6 @@
 // pair (a_0, 0) with b_0 in the b sum; k_sgs_bfin adds gamma and beta to it and applies it: B += A (gamma + beta +
 // sum_k b_k) mod m, leaving A < m, B < m for k_sgp_w / k_pe_fin.
 #pragma once
-#ifndef SGS_AB
-#define SGS_AB 0   // measurement builds only (round 6): & 1 = no pins in step 1's sweeps, & 2 = Q_A by a mask, not a multiply
-#endif
 #include "kernels_fbs.hpp"   // fbs_ap_all / fbs_apt_all / fbs_store_limbs / fbs_reduce_est
 #include "kernels_sgp.hpp"
 
@@ -89,10 +86,10 @@ __device__ __forceinline__ void sgs_q_digit(uint64_t (&P)[NC], const uint32_t (&
   constexpr int lo = C0 - J > 0 ? C0 - J : 0, hi = C0 + NC - 1 - J < S - 1 ? C0 + NC - 1 - J : S - 1;
 #pragma unroll
   for (int i = lo; i <= hi; ++i) P[i + J - C0] += (uint64_t)X[i] * d;
-#if !(SGS_AB & 1)
 #pragma unroll
   for (int i = 0; i < NC; ++i) asm volatile("" : "+v"(P[i]));
-#endif
+  // (round 6: without these pins and with Q_A by a mask instead of the multiply below -- k_fbs's two changes -- the loop
+  // lost 272 of its 9607 instructions per product but not a measurable microsecond: profiles/r06e_ab_sgs_pins_mask.txt)
   __builtin_amdgcn_sched_barrier(0);
 }
 template <int S, int C0, int NC, int JMIN, int... Ts>
@@ -133,13 +130,8 @@ __device__ __forceinline__ void sgs_r_all(uint64_t (&P)[S], const uint32_t (&X)[
 template <int S, int I0, int I1>
 __device__ __forceinline__ void sgs_part(uint64_t (&P)[S], const uint32_t (&X)[S], const uint32_t (&Q)[S], const uint32_t (&m)[S],
                                          const uint4* ar, uint32_t ob) {
-#if SGS_AB & 2
-#pragma unroll
-  for (int i = I0; i <= I1; ++i) P[i] = (uint64_t)((uint32_t)__builtin_amdgcn_update_dpp(0, (int)Q[i], 0xA0, 0xF, 0xF, false) & ob);
-#else
 #pragma unroll
   for (int i = I0; i <= I1; ++i) P[i] = (uint64_t)((uint32_t)__builtin_amdgcn_update_dpp(0, (int)Q[i], 0xA0, 0xF, 0xF, false) * ob);
-#endif
   sgs_r_all<S, I0, I1>(P, X, Q, m, ar, std::make_integer_sequence<int, S - I0>{});
 }
 
@@ -203,13 +195,8 @@ __global__ __launch_bounds__(LANE_BLOCK, 2) void k_sgs(SgsParams p) {
   const uint32_t lb = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds_q*)wq);
   const uint4* ar = wq + pw;                  // the pair's a quads (stride 32)
   const uint4* apr = wq + SGS_NQ * 32 + pw;   // its a' quads, then its b quads
-#if SGS_AB & 2
-  uint32_t ob = odd ? ~0u : 0u;
-  asm volatile("" : "+v"(ob));   // (a mask, not a select)
-#else
   uint32_t ob = odd ? 1u : 0u;
   asm volatile("" : "+v"(ob));   // (a multiplier, not a select)
-#endif
   constexpr int PAIRS = LANE_BLOCK / 2;
   for (long long base = (long long)blockIdx.x * PAIRS; base < p.n; base += (long long)gridDim.x * PAIRS) {
     const long long e = base + (threadIdx.x >> 1);

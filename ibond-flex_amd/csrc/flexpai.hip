@@ -52,6 +52,7 @@ static const char* xcheck_env(const char* name) {
 #include "engine_sgs.hpp"
 #include "engine_grp.hpp"
 #include "engine_mul.hpp"
+#include "engine_crtw.hpp"
 
 using namespace fpai;
 
@@ -66,6 +67,10 @@ static int fail(int code, const std::string& msg) {
     hipError_t _e = (expr);                                                             \
     if (_e != hipSuccess) return fail(PAI_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
   } while (0)
+
+// Largest call (elements) whose CRT exponentiations run on 16-lane rows (k_crt_w) instead of lanes / lane pairs
+// (k_crt_a + k_crt_b_pair): below it the lane kernels leave the chip mostly idle and take one lane's whole chain.
+constexpr long long CRTW_DEFAULT_MAX = 4096;
 
 struct pai_ctx {
   int device = 0;
@@ -92,6 +97,9 @@ struct pai_ctx {
   bool crt_ok = false;
   bool fbg_ok = false;        // 4096-bit keys: fixed-base sampler on the group engine (engine_grp), no lane CRT
   bool crt_enabled = true;
+  // calls of up to crtw_max elements run the CRT exponentiations on 16-lane rows (kernels_crtw.hpp: latency of
+  // protocol-sized calls); PAI_OPT_CRT_ROWS_MAX
+  long long crtw_max = CRTW_DEFAULT_MAX;
   int crt_sa = 0, crt_sb = 0;
   CrtHalf* d_crt_a = nullptr;   // [2] stage A halves
   CrtHalf* d_crt_b = nullptr;   // [2] stage B halves
@@ -1943,6 +1951,10 @@ int pai_ctx_set_option(pai_ctx* c, int option, int value) {
   CtxLock lk(c);
   switch (option) {
     case PAI_OPT_CRT_ENCRYPT: c->crt_enabled = value != 0; return 0;
+    case PAI_OPT_CRT_ROWS_MAX:
+      if (value < 0) return fail(PAI_ERR_ARG, "PAI_OPT_CRT_ROWS_MAX must be >= 0");
+      c->crtw_max = value;
+      return 0;
     case PAI_OPT_STAGE_TIMING: c->timing = value != 0; stage_reset(c); return 0;
     case PAI_OPT_LANE_DECRYPT: c->dec_lane_enabled = value != 0; return 0;
     case PAI_OPT_FIXED_BASE: c->fb_enabled = value != 0; return 0;
@@ -1973,6 +1985,7 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
   switch (option) {
     case PAI_OPT_CRT_ENCRYPT: *value = c->crt_enabled ? 1 : 0; return 0;
     case PAI_OPT_CRT_AVAILABLE: *value = c->crt_ok ? 1 : 0; return 0;
+    case PAI_OPT_CRT_ROWS_MAX: *value = (int)std::min<long long>(c->crtw_max, INT32_MAX); return 0;
     case PAI_OPT_STAGE_TIMING: *value = c->timing ? 1 : 0; return 0;
     case PAI_OPT_LANE_DECRYPT: *value = (c->dec_lane_ok && c->dec_lane_enabled) ? 1 : 0; return 0;
     // 1 when device-RNG encryption will use the fixed bases (tables resident, or not yet tried)
@@ -2731,6 +2744,61 @@ static int launch_pe(pai_ctx* c, const EncParams& e, hipStream_t st) {
   return 0;
 }
 
+// k_crt_fin over elements [off, off + n) of the call: c = (u_p q^2 + u_q p^2) c0 mod n^2 from u [2][sb][n]
+static int crt_finish(pai_ctx* c, const EncParams& e, const uint32_t* u, int sb, long long off, long long n,
+                      hipStream_t st) {
+  const size_t esz = e.dtype == PAI_F32 ? 4 : 8;
+  CrtFinParams f{};
+  f.x = (const char*)e.x + (size_t)off * esz;
+  f.dtype = e.dtype;
+  f.exp_mode = e.exp_mode;
+  f.fexp = e.fexp;
+  f.u = u;
+  f.sb = sb;
+  f.n = n;
+  f.N = c->d_N;
+  f.nl = c->d_nl;
+  f.kq = c->d_kq;
+  f.kp = c->d_kp;
+  f.mprime = c->mprime_N;
+  f.ct = e.ct + (size_t)off * c->ct_words;
+  f.exp = e.exp + off;
+  f.status = e.status ? e.status + off : nullptr;
+  f.ct_words = c->ct_words;
+  switch (c->tpi_e) {
+    case 2: return launch_crt_fin<2>(c, f, st);
+    case 4: return launch_crt_fin<4>(c, f, st);
+  }
+  return fail(PAI_ERR_KEY, "CRT finish: unsupported group size");
+}
+
+// A call of at most crtw_max elements: both exponentiations on 16-lane rows (k_crt_w, kernels_crtw.hpp), then
+// k_crt_fin. Same constants, op lists and output as k_crt_a + k_crt_b_pair; stage times: k_crt_w, k_crt_fin.
+static int launch_crtw(pai_ctx* c, const EncParams& e, int sa, int sb, int r_words, int kchunks, hipStream_t st) {
+  const long long N = e.n;
+  int rc = ensure_work(c, (size_t)2 * sb * 4 * N);
+  if (rc) return rc;
+  uint32_t* u = (uint32_t*)c->d_work;
+  crtw::Params p{};
+  p.ha = c->d_crt_a;
+  p.hb = c->d_crt_b;
+  p.n = N;
+  p.obf = e.obf;
+  p.r = e.r;
+  p.r_stride = e.r_stride;
+  p.r_words = r_words;
+  std::memcpy(p.rng_key, e.rng_key, sizeof(p.rng_key));
+  p.index_base = e.index_base;
+  p.kchunks = kchunks;
+  p.out = u;
+  stage_mark(c, 0, st);
+  HIPCHK(crtw_launch(sa, p, st));
+  stage_mark(c, 1, st);
+  if ((rc = crt_finish(c, e, u, sb, 0, N, st))) return rc;
+  stage_mark(c, 2, st);
+  return 0;
+}
+
 template <int SA, int SB>
 static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
   static_assert(SB == 2 * SA || SB == 2 * SA - 1, "stage sizes");
@@ -2743,6 +2811,7 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
   const int kchunks = (32 * r_words + LB * SA - 1) / (LB * SA);
   if (kchunks > KMAX_CHUNKS || (e.obf == PAI_OBF_RNG && r_words > RBUF_WORDS))
     return fail(PAI_ERR_ARG, "CRT encrypt: obfuscator too wide");
+  if (N <= c->crtw_max) return launch_crtw(c, e, SA, SB, r_words, kchunks, st);
   const long long chunk = std::min(N, CRT_CHUNK);
   int occA = 1, occB = 1;
   if (crt_lane_occupancy(SA, &occA, &occB)) return fail(PAI_ERR_KEY, "CRT encrypt: unsupported size");
@@ -2762,7 +2831,6 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
   if ((rc = ensure_work(c, (ybytes + (size_t)2 * SB * 4) * chunk))) return rc;
   uint32_t* y = (uint32_t*)c->d_work;
   uint32_t* u = (uint32_t*)((char*)c->d_work + ybytes * chunk);
-  const size_t esz = e.dtype == PAI_F32 ? 4 : 8;
   for (long long off = 0; off < N; off += chunk) {
     const long long n = std::min(chunk, N - off);
     CrtParams pa{};
@@ -2792,29 +2860,7 @@ static int launch_crt(pai_ctx* c, const EncParams& e, hipStream_t st) {
     HIPCHK(crt_b_pair_launch(SA, pb, gB, st));
     HIPCHK(hipGetLastError());
     stage_mark(c, 2, st);
-    CrtFinParams f{};
-    f.x = (const char*)e.x + (size_t)off * esz;
-    f.dtype = e.dtype;
-    f.exp_mode = e.exp_mode;
-    f.fexp = e.fexp;
-    f.u = u;
-    f.sb = SB;
-    f.n = n;
-    f.N = c->d_N;
-    f.nl = c->d_nl;
-    f.kq = c->d_kq;
-    f.kp = c->d_kp;
-    f.mprime = c->mprime_N;
-    f.ct = e.ct + (size_t)off * c->ct_words;
-    f.exp = e.exp + off;
-    f.status = e.status ? e.status + off : nullptr;
-    f.ct_words = c->ct_words;
-    switch (c->tpi_e) {
-      case 2: rc = launch_crt_fin<2>(c, f, st); break;
-      case 4: rc = launch_crt_fin<4>(c, f, st); break;
-      default: rc = fail(PAI_ERR_KEY, "CRT finish: unsupported group size");
-    }
-    if (rc) return rc;
+    if ((rc = crt_finish(c, e, u, SB, off, n, st))) return rc;
     stage_mark(c, 3, st);
   }
   return 0;

@@ -17,8 +17,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FLEXPAI_LIB") or os.path.join(_HERE, "libflexpai.so")   # override: experiments only
-# the test-only build (FLEXPAI_XCHECK): also holds the kernel generations the pair kernels replaced, selected by
-# $FLEXPAI_FB_PAIR=0 / $FLEXPAI_SGP=0 / $FLEXPAI_PAIR=0, for the tests that cross-check against them
+# the test-only build (FLEXPAI_XCHECK): also holds the kernel generations the tests still cross-check against
+# (k_fbgp, k_pfb, k_fbp), selected by $FLEXPAI_SGP=0 / $FLEXPAI_FBS=0, and honours $FLEXPAI_PAIR=0
 XCHECK_LIB_PATH = os.path.join(_HERE, "libflexpai_xcheck.so")
 
 PAI_F32, PAI_F64, PAI_I64 = 0, 1, 2
@@ -28,7 +28,7 @@ EL_OK, EL_INT, EL_INT_BIG, EL_OVERFLOW, EL_FLOAT_OVF, EL_ENC_RANGE = 0, 1, 2, 3,
 
 PAI_OPT_CRT_ENCRYPT, PAI_OPT_CRT_AVAILABLE, PAI_OPT_STAGE_TIMING, PAI_OPT_LANE_DECRYPT = 1, 2, 3, 4
 PAI_OPT_FIXED_BASE, PAI_OPT_FB_WINDOW, PAI_OPT_FB_READY, PAI_OPT_FB_PAIR, PAI_OPT_PAIR = 5, 6, 7, 8, 9
-PAI_OPT_SPLIT_SAMPLER = 13
+PAI_OPT_SPLIT_SAMPLER, PAI_OPT_CRT_ROWS_MAX = 13, 14
 PAI_OPT_PUBLIC_FB, PAI_OPT_PFB_READY, PAI_OPT_PFB_WINDOW = 10, 11, 12
 PFB_NBASES = 33
 
@@ -332,6 +332,15 @@ class Context:
         cnt = ctypes.c_int()
         self._chk(self.lib.pai_ctx_stage_times(self._h, buf, 8, ctypes.byref(cnt)))
         return [float(buf[i]) for i in range(cnt.value)]
+
+    @property
+    def crt_rows_max(self) -> int:
+        """Largest CRT encryption call (elements) that runs on 16-lane rows (k_crt_w, kernels_crtw.hpp)."""
+        return int(self._get_option(PAI_OPT_CRT_ROWS_MAX))
+
+    def set_crt_rows_max(self, n: int):
+        """0 keeps every CRT encryption on the lane kernels (k_crt_a + k_crt_b_pair); same ciphertext bits."""
+        self._chk(self.lib.pai_ctx_set_option(self._h, PAI_OPT_CRT_ROWS_MAX, int(n)))
 
     def set_crt(self, enabled: bool):
         """Encrypt through the private-key CRT kernels (default when available) or the public-key one.

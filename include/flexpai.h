@@ -117,7 +117,7 @@ typedef struct pai_comm pai_comm;
 #define PAI_OPT_FB_READY 7       /* read-only: 1 when the fixed-base tables are resident                    */
 #define PAI_OPT_FB_PAIR 8        /* read-only: limbs of p_h (19, 37; 76 for the 4096-bit pair-group tables)
                                     when the resident tables are pair tables (kernels_fbp.hpp,
-                                    kernels_grp_pair.hpp: the default; $FLEXPAI_FB_PAIR=0 selects k_fb / k_fbg),
+                                    kernels_grp_pair.hpp: the default; round 1's k_fb / k_fbg were retired in round 6),
                                     else 0                                                                     */
 #define PAI_OPT_PAIR 9           /* read-only: bit 0 = decryption, bit 1 = CRT encryption (stage B), bit 2 =
                                     public-key encryption (2048-bit n) run on p-adic pairs (kernels_pair.hpp,
@@ -140,6 +140,9 @@ typedef struct pai_comm pai_comm;
                                   * Shoup rows (kernels_sgs.hpp: k_sgs, the default where they price lower than the
                                   * factored rows at their window; $FLEXPAI_SGS=0 keeps k_sgp, =1 takes them
                                   * whenever they fit)                                                        */
+#define PAI_OPT_CRT_ROWS_MAX 14  /* CRT encryption calls of at most this many elements (default 4096) run both
+                                  * exponentiations with each residue on a 16-lane row (kernels_crtw.hpp: k_crt_w, the
+                                  * latency of protocol-sized calls) instead of one lane / lane pair each; 0 disables */
 
 /* Number of visible GPUs (0 when there is none or the runtime cannot start). */
 int pai_device_count(int* count);

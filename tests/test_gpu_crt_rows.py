@@ -1,0 +1,145 @@
+"""GPU parity of the 16-lane-row CRT encryption (kernels_crtw.hpp, k_crt_w: calls of at most PAI_OPT_CRT_ROWS_MAX
+elements) against the lane kernels it stands in for (k_crt_a + k_crt_b_pair, forced with crt_rows_max = 0), the
+public-key kernel and the CPU oracle (oracle/paillier_oracle.py encrypt_value: raw_encrypt.py:22-49 and
+obfuscator.py:23-37 of the reference). Bit-exact on every obfuscator mode, ragged counts and edge obfuscators."""
+import numpy as np
+import pytest
+
+from oracle import paillier_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _native():
+    from flex.crypto.paillier import _native
+    return _native
+
+
+def _key(golden, nb):
+    k = golden["keys"][str(nb)]
+    return O.Key(int(k["n"], 16), int(k["p"], 16), int(k["q"], 16))
+
+
+@pytest.fixture(scope="module")
+def ctxs(golden):
+    N = _native()
+    out = {}
+    for nb in (1024, 2048):
+        key = _key(golden, nb)
+        crt = N.Context(key.n, 0, key.p, key.q)
+        crt.set_fixed_base(False)          # the generic r^n path (the sampler: test_gpu_fixed_base / test_gpu_fbs)
+        pub = N.Context(key.n, 0)
+        out[nb] = (crt, pub, key)
+    return out
+
+
+def _both(crt, *args, **kw):
+    """(rows, lanes): the same call on k_crt_w and on k_crt_a + k_crt_b_pair, with the kernel count of each."""
+    crt.set_stage_timing(True)
+    try:
+        a = crt.encrypt(*args, **kw)
+        ka = len(crt.stage_times())
+        old = crt.crt_rows_max
+        crt.set_crt_rows_max(0)
+        try:
+            b = crt.encrypt(*args, **kw)
+            kb = len(crt.stage_times())
+        finally:
+            crt.set_crt_rows_max(old)
+    finally:
+        crt.set_stage_timing(False)
+    assert (ka, kb) == (2, 3), "k_crt_w + k_crt_fin against k_crt_a + k_crt_b_pair + k_crt_fin"
+    return a, b
+
+
+def test_rows_default_threshold(ctxs):
+    N = _native()
+    crt, _, _ = ctxs[2048]
+    assert crt.crt_rows_max == 4096
+    with pytest.raises(N.NativeError):
+        crt.set_crt_rows_max(-1)
+    assert crt.crt_rows_max == 4096
+
+
+@pytest.mark.parametrize("nb", [1024, 2048])
+@pytest.mark.parametrize("count", [1, 3, 4, 5, 17, 1000])
+def test_rows_rng_matches_lanes_and_oracle(ctxs, nb, count):
+    N = _native()
+    crt, pub, key = ctxs[nb]
+    x = np.random.default_rng(7 + count).standard_normal(count).astype(np.float32)
+    rk = bytes(range(3, 35))
+    base = (1 << 33) + 977                      # the element index's high word reaches the ChaCha nonce
+    a, b = _both(crt, x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=base)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    got = N.words_to_ints(a[0])
+    rbytes = ((nb + 64 + 31) // 32) * 4
+    for i in sorted({0, count // 2, count - 1}):
+        c, e = O.encrypt_value(x[i], key, O.device_r(rk, base + i, rbytes))
+        assert got[i] == c and int(a[1][i]) == e, f"element {i}"
+    if count == 17:
+        p = pub.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=base)
+        assert np.array_equal(a[0], p[0])
+
+
+@pytest.mark.parametrize("nb", [1024, 2048])
+def test_rows_golden_given_r(golden, ctxs, nb):
+    N = _native()
+    crt, _, _ = ctxs[nb]
+    recs = golden["encrypt"][str(nb)]
+    x = np.array([r["bits"] for r in recs], dtype=np.uint32).view(np.float32)
+    rs = [int(r["r"], 16) for r in recs]
+    a, b = _both(crt, x, obf_mode=N.PAI_OBF_GIVEN, r=rs)
+    got = N.words_to_ints(a[0])
+    for i, rec in enumerate(recs):
+        assert (hex(got[i]), int(a[1][i])) == (rec["c"], rec["e"]), f"element {i}"
+    assert np.array_equal(a[0], b[0])
+
+
+@pytest.mark.parametrize("nb", [1024, 2048])
+def test_rows_edge_obfuscators(ctxs, nb):
+    """r = 1, 2, n - 1, multiples of p and of q, r as wide as n^2 - 1, r = n + 1 and r = n (=> c = 0)."""
+    N = _native()
+    crt, _, key = ctxs[nb]
+    n, p, q = key.n, key.p, key.q
+    rs = [1, 2, n - 1, p, 3 * q, p * 7, n * n - 1, (n * n) // 3, n + 1, n, p - 1, q + 1]
+    x = np.linspace(-5, 5, len(rs)).astype(np.float32)
+    a, b = _both(crt, x, obf_mode=N.PAI_OBF_GIVEN, r=rs)
+    assert np.array_equal(a[0], b[0])
+    got = N.words_to_ints(a[0])
+    for i, r in enumerate(rs):
+        c, e = O.encrypt_value(x[i], key, r)
+        assert got[i] == c, f"r index {i}"
+
+
+@pytest.mark.parametrize("nb", [1024, 2048])
+def test_rows_scalar_r_and_dtypes(ctxs, nb):
+    """random_value reused for every element (encryptor.py:92-95); float64 and int64 inputs."""
+    N = _native()
+    crt, pub, key = ctxs[nb]
+    r = 0x1234567890ABCDEF1234567 % key.n
+    for x in (np.array([0.0, -0.0, 1.5, -2.25, 3e-30, -7e20], dtype=np.float64),
+              np.array([0, 1, -1, 2 ** 40, -(2 ** 50), 123456789], dtype=np.int64)):
+        a, b = _both(crt, x, obf_mode=N.PAI_OBF_GIVEN, r_scalar=r)
+        c = pub.encrypt(x, obf_mode=N.PAI_OBF_GIVEN, r_scalar=r)
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+        assert np.array_equal(a[0], c[0]) and np.array_equal(a[1], c[1])
+
+
+def test_rows_threshold_boundary(ctxs):
+    """crt_rows_max elements run on rows, one more on the lane kernels; the bits agree."""
+    N = _native()
+    crt, _, key = ctxs[1024]
+    old = crt.crt_rows_max
+    rk = b"t" * 32
+    x = np.random.default_rng(3).standard_normal(65).astype(np.float32)
+    crt.set_stage_timing(True)
+    try:
+        crt.set_crt_rows_max(64)
+        a = crt.encrypt(x[:64], obf_mode=N.PAI_OBF_RNG, rng_key=rk)
+        assert len(crt.stage_times()) == 2
+        b = crt.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk)
+        assert len(crt.stage_times()) == 3
+    finally:
+        crt.set_crt_rows_max(old)
+        crt.set_stage_timing(False)
+    assert np.array_equal(a[0], b[0][:64])

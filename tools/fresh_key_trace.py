@@ -3,7 +3,9 @@
 first device-RNG encrypt of a 1M float32 vector (which builds the W = 16 tables past the break-even count), each timed
 on the host clock with the device synchronised, with $FLEXPAI_SETUP_TRACE's per-step lines from the library on stderr.
 
-    python tools/fresh_key_trace.py [--keys 3] [--n 1048576] [--nb 2048]
+    python tools/fresh_key_trace.py [--keys 3] [--n 1048576] [--nb 2048] [--rows-max N]
+
+--rows-max sets PAI_OPT_CRT_ROWS_MAX (0: the lane kernels k_crt_a + k_crt_b_pair for every call size).
 """
 import argparse
 import os
@@ -22,6 +24,7 @@ def main():
     ap.add_argument("--keys", type=int, default=3)
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--nb", type=int, default=2048)
+    ap.add_argument("--rows-max", type=int, default=None)
     a = ap.parse_args()
     from flex.crypto.paillier import _native as N
     from flex.crypto.paillier.keypair import generate_paillier_keypair
@@ -42,6 +45,8 @@ def main():
         c = N.Context(pk.n, 0)
         t1 = time.perf_counter()
         c.set_private(sk.p, sk.q)
+        if a.rows_max is not None:
+            c.set_crt_rows_max(a.rows_max)
         t2 = time.perf_counter()
         c.set_stage_timing(True)
         rc = lib.pai_encrypt_dev(c.handle, N.PAI_F32, x.data_ptr(), a.n, 0, 0, N.PAI_OBF_RNG, None, 0, 0, bytes(32), 0,

@@ -66,6 +66,13 @@ hipError_t dec_pair_launch(int s, const DecPairPreParams& pre, const CrtParams& 
   return hipErrorInvalidValue;
 }
 
+hipError_t dec_pair_launch_fin(int s, const DecPairFinParams& f, int gx, hipStream_t st) {
+  if (s == 19) hipLaunchKernelGGL(k_dec_fin_pair<19>, dim3(gx), dim3(LANE_BLOCK), 0, st, f);
+  else if (s == 37) hipLaunchKernelGGL(k_dec_fin_pair<37>, dim3(gx), dim3(LANE_BLOCK), 0, st, f);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 int crt_b_pair_occupancy(int s, int* occ) {
   if (s == 19) *occ = occupancy(k_crt_b_pair<19>);
   else if (s == 37) *occ = occupancy(k_crt_b_pair<37>);

@@ -15,6 +15,8 @@ int dec_pair_geometry(int s, int cus, long long chunk, DecLaneGeom* g, bool fact
 // k_dec_pre_pair, k_dec_pow_pair (both halves on blockIdx.y), k_dec_fin_pair on `st`; ev[0..3] nullable
 hipError_t dec_pair_launch(int s, const DecPairPreParams& pre, const CrtParams& pw, const DecPairFinParams& f,
                            const DecLaneGeom& g, hipStream_t st, hipEvent_t* ev, bool factored = true);
+// k_dec_fin_pair<s> alone (grid gx), for pairs another kernel produced (k_dec_w)
+hipError_t dec_pair_launch_fin(int s, const DecPairFinParams& f, int gx, hipStream_t st);
 // blocks per CU of k_crt_b_pair<s> (-1 if unsupported) and its launch (grid gx x 2 halves)
 int crt_b_pair_occupancy(int s, int* occ);
 hipError_t crt_b_pair_launch(int s, const CrtParams& p, int gx, hipStream_t st);

@@ -114,6 +114,8 @@ struct pai_ctx {
   CrtHalf* d_decp_pow = nullptr;   // decryption halves; c0: the factored chain's K'_t ([16][S], decf)
   bool decf = false;                // the factored (B-free) decryption chain (kernels_pair.hpp decf_run)
   CrtHalf* d_crtp_b = nullptr;
+  CrtHalf* d_decw = nullptr;   // [2] k_dec_w's halves (kernels_crtw.hpp): p_h^2, R^(K+1), 1, op list over p_h - 1
+  int decw_kchunks = 0;
   uint32_t *d_decp_nl = nullptr, *d_decp_maxint = nullptr;
   int decp_kchunks = 0;
   // 4096-bit keys: decryption on split pairs (kernels_dec4.hpp), the default; the group k_decrypt otherwise
@@ -1733,7 +1735,7 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
   const size_t RA = (size_t)LB * sa, RB = (size_t)LB * sb, RE = (size_t)LB * c->S_e;
   const HBig primes[2] = {p, q};
   const HBig sq[2] = {mul(p, p), mul(q, q)};
-  CrtHalf ha[2], hb[2];
+  CrtHalf ha[2], hb[2], hd[2];
   int rc;
   SetupTrace tr_ab("    crt stage A/B consts");
   for (int h = 0; h < 2; ++h) {
@@ -1765,9 +1767,24 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
         (rc = upload(c, coef.limbs(sb, LB), &dcoef)) || (rc = upload(c, pbp, &dpb)))
       return rc;
     hb[h] = CrtHalf{dm2, dr2, dcoef, dpb, (int)pbp.size(), mont_prime(m2, LB)};
+    // decryption on 16-lane rows (k_dec_w): c R mod p_h^2 by kd passes, then the op list over p_h - 1
+    const int kd = (int)((32 * (size_t)c->ct_words + RB - 1) / RB);
+    std::vector<uint32_t> pdw, oneb(sb, 0);
+    oneb[0] = 1;
+    if (kd <= KMAX_CHUNKS && build_lane_program(sub(ph, HBig(1)), pdw)) {
+      uint32_t *dck2, *done2, *dpdw;
+      if ((rc = upload(c, mul_pow2_mod(HBig(1), RB * (kd + 1), m2).limbs(sb, LB), &dck2)) || (rc = upload(c, oneb, &done2)) ||
+          (rc = upload(c, pdw, &dpdw)))
+        return rc;
+      hd[h] = CrtHalf{dm2, dck2, done2, dpdw, (int)pdw.size(), mont_prime(m2, LB)};
+      c->decw_kchunks = kd;
+    } else {
+      c->decw_kchunks = 0;
+    }
   }
-  std::vector<CrtHalf> va(ha, ha + 2), vb(hb, hb + 2);
+  std::vector<CrtHalf> va(ha, ha + 2), vb(hb, hb + 2), vd(hd, hd + 2);
   if ((rc = upload(c, va, &c->d_crt_a)) || (rc = upload(c, vb, &c->d_crt_b))) return rc;
+  if (c->decw_kchunks && (rc = upload(c, vd, &c->d_decw))) return rc;
   // finish: q^2 R^2 mod n^2 and p^2 R^2 mod n^2 (group layout)
   if ((rc = upload(c, mul_pow2_mod(sq[1], 2 * RE, c->N).limbs(c->S_e, LB), &c->d_kq)) ||
       (rc = upload(c, mul_pow2_mod(sq[0], 2 * RE, c->N).limbs(c->S_e, LB), &c->d_kp)))
@@ -1878,6 +1895,8 @@ int pai_ctx_set_private(pai_ctx* c, const uint8_t* p_le, const uint8_t* q_le, si
     c->priv_allocs.clear();
     (void)hipGetLastError();
     c->has_priv = c->crt_ok = c->fbg_ok = c->dec_lane_ok = c->dec_pair_ok = c->crt_pair_ok = c->dec4_ok = false;
+    c->d_decw = nullptr;
+    c->decw_kchunks = 0;
     c->fb_state = pai_ctx::FB_UNTRIED;
     g_last_error = msg;
   }
@@ -3009,8 +3028,48 @@ static int launch_decrypt(pai_ctx* c, DecParams& p, hipStream_t st) {
 }
 
 // pair decryption (kernels_pair.hpp, engine_pair.hip), in chunks of CRT_CHUNK elements
+// The pair kernels' final stage over elements [off, off + n) from the pairs in xw ([2][2S][n])
+static DecPairFinParams dec_pair_fin_params(pai_ctx* c, const DecParams& d, uint32_t* xw, long long off, long long n) {
+  DecPairFinParams f{};
+  f.halves = c->d_decp_halves;
+  f.n = n;
+  f.xh = xw;
+  f.exp = d.exp + off;
+  f.p = c->d_dec_p;
+  f.q = c->d_dec_q;
+  f.qinvR = c->d_dec_qinvR;
+  f.pprime = c->dec_pprime;
+  f.nlimb = c->d_decp_nl;
+  f.maxint = c->d_decp_maxint;
+  f.val = d.val + off;
+  f.mant = d.mant ? d.mant + off : nullptr;
+  f.status = d.status + off;
+  f.raw = d.raw ? d.raw + (size_t)off * c->pt_words : nullptr;
+  f.pt_words = c->pt_words;
+  return f;
+}
+
+// A call of at most crtw_max ciphertexts: c^(p_h - 1) mod p_h^2 on 16-lane rows (k_dec_w, kernels_crtw.hpp) into
+// the pairs k_dec_fin_pair takes; stage times: k_dec_w, k_dec_fin_pair.
+static int launch_decw(pai_ctx* c, const DecParams& d, hipStream_t st) {
+  const long long N = d.n;
+  const int S = c->crt_sa;
+  int rc = ensure_work(c, (size_t)4 * S * N * 4);
+  if (rc) return rc;
+  uint32_t* xw = (uint32_t*)c->d_work;
+  crtw::DecParams p{c->d_decw, c->d_crt_a, N, d.ct, c->ct_words, c->decw_kchunks, xw};
+  stage_mark(c, 0, st);
+  HIPCHK(decw_launch(S, p, st));
+  stage_mark(c, 1, st);
+  const DecPairFinParams f = dec_pair_fin_params(c, d, xw, 0, N);
+  HIPCHK(dec_pair_launch_fin(S, f, (int)std::min<long long>((N + LANE_BLOCK - 1) / LANE_BLOCK, 4ll * c->cus), st));
+  stage_mark(c, 2, st);
+  return 0;
+}
+
 static int launch_dec_pair(pai_ctx* c, const DecParams& d, hipStream_t st) {
   const long long N = d.n;
+  if (N <= c->crtw_max && c->d_decw) return launch_decw(c, d, st);
   const long long chunk = std::min(N, CRT_CHUNK);
   const int S = c->crt_sa;
   DecLaneGeom g;
@@ -3030,22 +3089,7 @@ static int launch_dec_pair(pai_ctx* c, const DecParams& d, hipStream_t st) {
     pw.yin = xw;
     pw.out = xw;
     pw.scratch = (uint32_t*)c->d_scratch;
-    DecPairFinParams f{};
-    f.halves = c->d_decp_halves;
-    f.n = n;
-    f.xh = xw;
-    f.exp = d.exp + off;
-    f.p = c->d_dec_p;
-    f.q = c->d_dec_q;
-    f.qinvR = c->d_dec_qinvR;
-    f.pprime = c->dec_pprime;
-    f.nlimb = c->d_decp_nl;
-    f.maxint = c->d_decp_maxint;
-    f.val = d.val + off;
-    f.mant = d.mant ? d.mant + off : nullptr;
-    f.status = d.status + off;
-    f.raw = d.raw ? d.raw + (size_t)off * c->pt_words : nullptr;
-    f.pt_words = c->pt_words;
+    const DecPairFinParams f = dec_pair_fin_params(c, d, xw, off, n);
     HIPCHK(dec_pair_launch(S, pre, pw, f, g, st, ev, c->decf));
   }
   return 0;

@@ -12,6 +12,10 @@
 //                     y = x~^(q_h mod (p_h - 1)) R^-1 mod p_h (the stage-A op list),
 //                     u = (y R)^(p_h) coef R^-1 mod p_h^2 (the stage-B op list of the 2S-limb lane constants,
 //                     R = 2^(28 KB)), written as KB 28-bit limbs [2][KB][n] for k_crt_fin.
+//   k_dec_w<KA, KB>   decryption's exponentiation the same way (decryptor.py:55-61): c~ = c R mod p_h^2, x =
+//                     c~^(p_h - 1) R^-1 mod p_h^2 (the op list over p_h - 1), x made canonical, then the pair of x that
+//                     k_dec_fin_pair takes: A = x mod p_h (0 or 1: x == 1 mod p_h unless p_h | c, when x == 0) and
+//                     B = (x - A) / p_h, an exact division by REDC's digits (Q = -(x - A) p_h^-1 mod R_A, B = -Q).
 //
 // Layout: lane t of a row owns limbs [t LW, t LW + LW) of the accumulator (bn_group.hpp's rotating CIOS with L ->
 // LW); every multiplicand sits in LDS as plain limbs (limb j = word j of a slot), read by the row as a broadcast,
@@ -138,6 +142,75 @@ __device__ __forceinline__ const uint32_t* uniform_ptr(const uint32_t* p) {
   const uint64_t v = (uint64_t)p;
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
   return (const uint32_t*)(((uint64_t)hi << 32) | lo);
+}
+
+// d = a - b over the row's TPI LW limbs (bn_group.hpp sub_limbs with L -> LW); returns true (row-uniform) when a < b
+// (d is then the two's-complement wrap)
+template <int LW>
+__device__ __forceinline__ bool sub(const uint32_t (&a)[LW], const uint32_t (&b)[LW], uint32_t (&d)[LW], int lane, int tig) {
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < LW; ++i) {
+    const int32_t v = (int32_t)a[i] - (int32_t)b[i] + c;
+    d[i] = (uint32_t)v & LMASK;
+    c = v >> LB;
+  }
+  const int32_t b1 = c;
+  int32_t bin = (int32_t)dpp_from_prev((uint32_t)c);
+  if (tig == 0) bin = 0;
+#pragma unroll
+  for (int i = 0; i < LW; ++i) {
+    const int32_t v = (int32_t)d[i] + bin;
+    d[i] = (uint32_t)v & LMASK;
+    bin = v >> LB;
+  }
+  bool all_zero = true;
+#pragma unroll
+  for (int i = 0; i < LW; ++i) all_zero &= (d[i] == 0u);
+  const bool gen = bin != 0;
+  const uint32_t bi = lookahead_carry_in<TPI>(gen, all_zero, lane);
+  if (ballot(bi != 0) != 0ull) {
+    int32_t b2 = -(int32_t)bi;
+#pragma unroll
+    for (int i = 0; i < LW; ++i) {
+      const int32_t v = (int32_t)d[i] + b2;
+      d[i] = (uint32_t)v & LMASK;
+      b2 = v >> LB;
+    }
+  }
+  const bool neg_here = (tig == TPI - 1) && (b1 != 0 || gen || (all_zero && bi));
+  return ((ballot(neg_here) >> (lane - tig + TPI - 1)) & 1ull) != 0ull;
+}
+
+// row-uniform: some limb of the row is nonzero
+template <int LW>
+__device__ __forceinline__ bool nonzero(const uint32_t (&x)[LW], int lane, int tig) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < LW; ++i) o |= x[i];
+  return ((ballot(o != 0u) >> (lane - tig)) & 0xFFFFull) != 0ull;
+}
+
+// REDC digit j of an exact division (no product term): q = T_0 mprime, T = (T + q m) / 2^28; q kept by lane j / LW in
+// slot j % LW (the slot the rotation frees)
+template <int LW, int J>
+__device__ __forceinline__ void dstep(uint64_t (&P)[LW], const uint32_t (&m)[LW], uint32_t mprime, uint32_t (&o)[LW], int tig) {
+  constexpr int s = J % LW;
+  const uint32_t q = bcast0<TPI>(((uint32_t)P[s] * mprime) & LMASK);
+  o[s] = tig == J / LW ? q : o[s];
+#pragma unroll
+  for (int i = 0; i < LW; ++i) P[(i + s) % LW] += (uint64_t)q * m[i];
+  const uint64_t v0 = P[s];
+  P[(s + 1) % LW] += v0 >> LB;
+  P[s] = (uint64_t)dpp_from_next((uint32_t)v0 & LMASK);
+#pragma unroll
+  for (int i = 0; i < LW; ++i) asm volatile("" : "+v"(P[i]));
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int LW, int... Js>
+__device__ __forceinline__ void dsteps(uint64_t (&P)[LW], const uint32_t (&m)[LW], uint32_t mprime, uint32_t (&o)[LW], int tig,
+                                       std::integer_sequence<int, Js...>) {
+  (dstep<LW, Js>(P, m, mprime, o, tig), ...);
 }
 
 // row slot <- limbs (zero above the row's TPI LW limbs, up to SW words)
@@ -303,6 +376,119 @@ __global__ __launch_bounds__(BLOCK_W) void k_crt_w(Params p) {
       for (int j = 0; j < LBW; ++j) {
         const int limb = tig * LBW + j;
         if (limb < KB) p.out[((size_t)half * KB + limb) * p.n + i] = a[j];
+      }
+    }
+  }
+}
+
+struct DecParams {
+  const CrtHalf* hd;            // [2]: p_h^2 (KB limbs), R^(K+1) mod p_h^2 (R = 2^(28 KB)), 1, op list over p_h - 1
+  const CrtHalf* ha;            // [2]: p_h (KA limbs) and its mprime (the exact division)
+  long long n;
+  const uint32_t* ct;
+  int ct_words;
+  int kchunks;                  // ceil(32 ct_words / (28 KB)) <= KMAX_CHUNKS
+  uint32_t* out;                // [2][2 KA][n]: the pair (A, B) of c^(p_h - 1) mod p_h^2, k_dec_fin_pair's input
+};
+
+template <int KA, int KB>
+__global__ __launch_bounds__(BLOCK_W) void k_dec_w(DecParams p) {
+  constexpr int LBW = Geom<KB>::LW;
+  constexpr int SW = slot_words<KA, KB>();
+  constexpr int CS = (KB + 3) & ~3;                     // one ciphertext chunk per CS words
+  static_assert(RBUF_WORDS + KMAX_CHUNKS * CS <= LANE_NTILE * SW, "ciphertext staging must fit the tiles it aliases");
+  __shared__ __attribute__((aligned(16))) uint32_t sm[lds_words<KA, KB>()];
+  const int half = blockIdx.y;
+  const CrtHalf* HD = p.hd + half;
+  const CrtHalf* HA = p.ha + half;
+  const int lane = threadIdx.x, tig = lane & (TPI - 1), g = lane / TPI;
+  uint32_t* T = sm + g * NSLOT * SW;
+  uint32_t* SQ = T + LANE_NTILE * SW;
+  uint32_t* MU = SQ + SW;
+  uint32_t* CO = sm + GPW * NSLOT * SW;                 // 1
+  for (int w = lane; w < SW; w += BLOCK_W) CO[w] = w < KB ? HD->c1[w] : 0u;
+  uint32_t m[LBW], mp[LBW], cK[LBW];
+  load_const<LBW>(HD->m, KB, m, tig);
+  load_const<LBW>(HA->m, KA, mp, tig);
+  load_const<LBW>(HD->c0, KB, cK, tig);                 // R^(kchunks + 1) mod p_h^2
+  const uint32_t mpD = HD->mprime, mpA = HA->mprime;
+  const uint32_t* prog = uniform_ptr(HD->prog);
+  const int nprog = __builtin_amdgcn_readfirstlane(HD->nprog);
+  for (long long base = (long long)blockIdx.x * GPW; base < p.n; base += (long long)gridDim.x * GPW) {
+    const long long i = base + g;
+    const long long ii = i < p.n ? i : p.n - 1;
+    uint32_t* RW = T;
+    uint32_t* RL = T + RBUF_WORDS;
+    wave_lds_fence();
+    {
+      const uint32_t* cw = p.ct + ii * p.ct_words;
+      for (int w = tig; w < p.ct_words; w += TPI) RW[w] = cw[w];
+    }
+    wave_lds_fence();
+    const int nw = p.ct_words;
+    for (int j = tig; j < p.kchunks * KB; j += TPI) {
+      const int bit = j * LB, wi = bit >> 5, sh = bit & 31;
+      const uint64_t lo = wi < nw ? (uint64_t)RW[wi] : 0ull;
+      const uint64_t hi = wi + 1 < nw ? (uint64_t)RW[wi + 1] : 0ull;
+      RL[(j / KB) * CS + j % KB] = (uint32_t)(((hi << 32) | lo) >> sh) & LMASK;
+    }
+    wave_lds_fence();
+    // c~ = c R mod p_h^2, one CIOS pass per chunk of the ciphertext's digits (as k_crt_w's x~)
+    uint32_t x[LBW];
+#pragma unroll
+    for (int j = 0; j < LBW; ++j) x[j] = 0u;
+    for (int k = 0; k < p.kchunks; ++k) {
+      uint32_t acc[LBW];
+#pragma unroll
+      for (int j = 0; j < LBW; ++j) {
+        acc[j] = x[j];
+        x[j] = cK[j];
+      }
+      mont<KB, true>(x, RL + k * CS, m, mpD, lane, tig, acc);
+    }
+    put<LBW, SW>(T, x, tig);
+    run<KB, SW>(x, T, SQ, MU, CO, prog, nprog, m, mpD, lane, tig);   // x = c^(p_h - 1) mod p_h^2, < 2 p_h^2
+    {
+      uint32_t d[LBW];
+      if (!sub<LBW>(x, m, d, lane, tig)) {
+#pragma unroll
+        for (int j = 0; j < LBW; ++j) x[j] = d[j];
+      }
+    }
+    const uint32_t A = nonzero<LBW>(x, lane, tig) ? 1u : 0u;
+    {
+      uint32_t av[LBW], d[LBW];
+#pragma unroll
+      for (int j = 0; j < LBW; ++j) av[j] = (tig == 0 && j == 0) ? A : 0u;
+      (void)sub<LBW>(x, av, d, lane, tig);             // x - A (>= 0)
+#pragma unroll
+      for (int j = 0; j < LBW; ++j) x[j] = d[j];
+    }
+    uint32_t Bv[LBW];
+    {
+      uint64_t P[LBW];
+      uint32_t q[LBW], z[LBW];
+#pragma unroll
+      for (int j = 0; j < LBW; ++j) {
+        P[j] = x[j];
+        q[j] = 0u;
+        z[j] = 0u;
+      }
+      dsteps<LBW>(P, mp, mpA, q, tig, std::make_integer_sequence<int, KA>{});   // q = -(x - A) p_h^-1 mod R_A
+      (void)sub<LBW>(z, q, Bv, lane, tig);
+#pragma unroll
+      for (int j = 0; j < LBW; ++j)
+        if (tig * LBW + j >= KA) Bv[j] = 0u;                                   // B = (x - A) / p_h < p_h
+    }
+    if (i < p.n) {
+      uint32_t* o = p.out + (size_t)half * 2 * KA * p.n + i;
+#pragma unroll
+      for (int j = 0; j < LBW; ++j) {
+        const int limb = tig * LBW + j;
+        if (limb < KA) {
+          o[(size_t)limb * p.n] = limb == 0 ? A : 0u;
+          o[(size_t)(KA + limb) * p.n] = Bv[j];
+        }
       }
     }
   }

@@ -335,11 +335,11 @@ class Context:
 
     @property
     def crt_rows_max(self) -> int:
-        """Largest CRT encryption call (elements) that runs on 16-lane rows (k_crt_w, kernels_crtw.hpp)."""
+        """Largest CRT encryption / decryption call (elements) that runs on 16-lane rows (k_crt_w / k_dec_w)."""
         return int(self._get_option(PAI_OPT_CRT_ROWS_MAX))
 
     def set_crt_rows_max(self, n: int):
-        """0 keeps every CRT encryption on the lane kernels (k_crt_a + k_crt_b_pair); same ciphertext bits."""
+        """0 keeps every CRT encryption / decryption on the lane kernels (k_crt_a + k_crt_b_pair, k_dec_*_pair); same bits."""
         self._chk(self.lib.pai_ctx_set_option(self._h, PAI_OPT_CRT_ROWS_MAX, int(n)))
 
     def set_crt(self, enabled: bool):

@@ -143,3 +143,70 @@ def test_rows_threshold_boundary(ctxs):
         crt.set_crt_rows_max(old)
         crt.set_stage_timing(False)
     assert np.array_equal(a[0], b[0][:64])
+
+
+# ---------------------------------------------------------------- decryption on rows (k_dec_w + k_dec_fin_pair)
+def _dboth(ctx, ct, ex):
+    """(rows, pairs): decrypt with raw plaintext words on k_dec_w and on k_dec_pre/pow_pair, with the kernel counts."""
+    ctx.set_stage_timing(True)
+    try:
+        a = ctx.decrypt(ct, ex, want_raw=True)
+        ka = len(ctx.stage_times())
+        old = ctx.crt_rows_max
+        ctx.set_crt_rows_max(0)
+        try:
+            b = ctx.decrypt(ct, ex, want_raw=True)
+            kb = len(ctx.stage_times())
+        finally:
+            ctx.set_crt_rows_max(old)
+    finally:
+        ctx.set_stage_timing(False)
+    assert (ka, kb) == (2, 3), "k_dec_w + k_dec_fin_pair against k_dec_pre_pair + k_dec_pow_pair + k_dec_fin_pair"
+    for x, y in zip(a, b):
+        assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+    return a
+
+
+@pytest.mark.parametrize("nb", [1024, 2048])
+def test_rows_decrypt_golden(golden, ctxs, nb):
+    N = _native()
+    crt, _, _ = ctxs[nb]
+    recs = golden["encrypt"][str(nb)]
+    ct = N.ints_to_words([int(r["c"], 16) for r in recs], crt.ct_words)
+    ex = np.array([r["e"] for r in recs], dtype=np.int32)
+    val = _dboth(crt, ct, ex)[0]
+    for i, r in enumerate(recs):
+        want = float.fromhex(r["dec"]) if isinstance(r["dec"], str) else float(r["dec"])
+        assert float(val[i]) == want, f"element {i}"
+
+
+@pytest.mark.parametrize("nb", [1024, 2048])
+def test_rows_decrypt_edge_ciphertexts(ctxs, nb):
+    """c = 0, multiples of p, q, p^2, q^2 (x_h = 0 or p_h^2 before the canonical step), c >= n^2, all-ones words."""
+    N = _native()
+    crt, _, key = ctxs[nb]
+    W = crt.ct_words
+    top = (1 << (32 * W)) - 1
+    cs = [0, 1, 2, key.p, key.q, 3 * key.p, key.p * key.q, key.psquare, key.qsquare, key.psquare * 5 + key.q,
+          key.nsquare - 1, key.nsquare, key.nsquare + 12345, top, top - 1, (key.n + 1) % key.nsquare,
+          pow(key.n + 1, 5, key.nsquare)]
+    rng = np.random.default_rng(nb + 1)
+    cs += [int.from_bytes(rng.bytes(4 * W), "little") for _ in range(40)]
+    ct = N.ints_to_words(cs, W)
+    ex = np.array([(i % 5) - 1 for i in range(len(cs))], dtype=np.int32)
+    raw = N.words_to_ints(_dboth(crt, ct, ex)[3])
+    for i, c in enumerate(cs):
+        assert raw[i] == O.raw_decrypt(c, key), f"element {i} (c = {c:#x})"
+
+
+@pytest.mark.parametrize("nb", [1024, 2048])
+@pytest.mark.parametrize("count", [1, 5, 1000])
+def test_rows_decrypt_roundtrip(ctxs, nb, count):
+    N = _native()
+    crt, _, _ = ctxs[nb]
+    rng = np.random.default_rng(count)
+    x = (rng.standard_normal(count) * 10.0 ** rng.integers(-30, 30, count)).astype(np.float32)
+    x[::7] = 0.0
+    ct, ex, _ = crt.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=bytes(range(32)), index_base=11)
+    val = _dboth(crt, ct, ex)[0]
+    assert np.array_equal(val, x.astype(np.float64))

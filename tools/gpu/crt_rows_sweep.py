@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Call-size sweep of the key holder's generic CRT encryption (device RNG, fixed bases off): k_crt_w on 16-lane rows
-(kernels_crtw.hpp) against k_crt_a + k_crt_b_pair on lanes, warm calls, median of --reps, one JSON line per size;
-where the rows stop winning is PAI_OPT_CRT_ROWS_MAX's default. Usage:
+(kernels_crtw.hpp) against k_crt_a + k_crt_b_pair on lanes, and of decryption (k_dec_w against k_dec_pre/pow_pair), warm
+calls, median of --reps, one JSON line per size; where the rows stop winning is PAI_OPT_CRT_ROWS_MAX's default. Usage:
     python tools/gpu/crt_rows_sweep.py [--nb 2048] [--sizes 256,1024,2048,4096,8192,16384] [--reps 3]"""
 import argparse
 import json
@@ -57,6 +57,27 @@ def main():
             outs[name] = ct.clone()
             row[name] = {"wall_ms": round(statistics.median(wall), 3), "stages_ms": kern[len(kern) // 2]}
         row["identical"] = bool(torch.equal(outs["rows"], outs["lanes"]))
+        val = torch.empty(n, dtype=torch.float64, device=dev)
+        mant = torch.empty(n, dtype=torch.int64, device=dev)
+        dst = torch.empty(n, dtype=torch.int32, device=dev)
+        dec = {}
+        for name, cap in (("rows", n), ("pairs", 0)):
+            c.set_crt_rows_max(cap)
+            wall, kern = [], []
+            for rep in range(a.reps + 1):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                rc = lib.pai_decrypt_dev(c.handle, ct.data_ptr(), ex.data_ptr(), n, val.data_ptr(), mant.data_ptr(),
+                                         dst.data_ptr(), None, stream.cuda_stream)
+                assert rc == 0, lib.pai_last_error()
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                if rep:
+                    wall.append(1e3 * (t1 - t0))
+                    kern.append([round(v, 3) for v in c.stage_times()])
+            dec[name] = val.clone()
+            row["dec_" + name] = {"wall_ms": round(statistics.median(wall), 3), "stages_ms": kern[len(kern) // 2]}
+        row["dec_identical"] = bool(torch.equal(dec["rows"], dec["pairs"])) and bool(torch.equal(dec["rows"], x.double()))
         print(json.dumps(row), flush=True)
 
 

@@ -1082,9 +1082,11 @@ def main():
     # setup included, at the library defaults (W = 16 tables, built only past the break-even count)
     if solo and cfg_id == 1 and use_fb:
         fresh = {}
-        for label, nf, seed in (("first_1M_call", N, 2), ("first_1k_call", 1000, 3)):
-            pk2, sk2 = generate_paillier_keypair(nb, seed=seed)    # host keygen, not timed (the reference's too)
-            ct_f = torch.empty((nf, W), dtype=torch.int32, device=dev)
+        for label, nf, seed, nbf in (("first_1M_call", N, 2, nb), ("first_1k_call", 1000, 3, nb),
+                                     ("first_1k_call_nb1024", 1000, 4, 1024)):
+            pk2, sk2 = generate_paillier_keypair(nbf, seed=seed)    # host keygen, not timed (the reference's too)
+            Wf = 2 * nbf // 32
+            ct_f = torch.empty((nf, Wf), dtype=torch.int32, device=dev)
             ex_f = torch.empty(nf, dtype=torch.int32, device=dev)
             torch.cuda.synchronize()
             t1 = time.perf_counter()
@@ -1096,13 +1098,28 @@ def main():
                 raise RuntimeError(lib.pai_last_error().decode())
             torch.cuda.synchronize()
             wall = time.perf_counter() - t1
-            fresh[label] = {"elements": nf, "wall_ms": wall * 1e3, "encrypts_per_s_incl_setup": nf / wall,
+            fresh[label] = {"elements": nf, "key_bits": nbf, "wall_ms": wall * 1e3, "encrypts_per_s_incl_setup": nf / wall,
                             "tables_built": c2.fb_ready,
                             "fixed_base_window": c2.fb_window if c2.fb_ready else None}
+            if nf <= 4096:   # the protocol's other half: decrypt the call's ciphertexts on the same fresh context
+                val_f = torch.empty(nf, dtype=torch.float64, device=dev)
+                mant_f = torch.empty(nf, dtype=torch.int64, device=dev)
+                st_f = torch.empty(nf, dtype=torch.int32, device=dev)
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                rc = lib.pai_decrypt_dev(c2.handle, ct_f.data_ptr(), ex_f.data_ptr(), nf, val_f.data_ptr(), mant_f.data_ptr(),
+                                         st_f.data_ptr(), None, stream.cuda_stream)
+                if rc != 0:
+                    raise RuntimeError(lib.pai_last_error().decode())
+                torch.cuda.synchronize()
+                fresh[label]["decrypt_wall_ms"] = (time.perf_counter() - t2) * 1e3
+                fresh[label]["roundtrip_exact"] = bool(torch.equal(val_f, x[:nf].double()))
             del c2, ct_f, ex_f
         fresh["note"] = ("new keypair per call (HE_SA_FT re-keys per exchange, he_sa_ft/train.py:39-40): wall time of "
                          "Context + set_private + one pai_encrypt_dev on device-resident x, synchronised; tables are "
-                         "built only when the call reaches the break-even count (pai_ctx_fixed_base_policy)")
+                         "built only when the call reaches the break-even count (pai_ctx_fixed_base_policy); calls of "
+                         "<= 4096 elements run on 16-lane rows (k_crt_w / k_dec_w, PAI_OPT_CRT_ROWS_MAX); "
+                         "decrypt_wall_ms: pai_decrypt_dev of the call's ciphertexts on the same context")
         extra["fresh_key"] = fresh
     cpu_sample = args.cpu_sample if nb <= 2048 else min(args.cpu_sample, 4096)   # bounded CPU work at nb = 4096
     S_chk = min(N, cpu_sample)

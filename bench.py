@@ -1118,7 +1118,7 @@ def main():
         fresh["note"] = ("new keypair per call (HE_SA_FT re-keys per exchange, he_sa_ft/train.py:39-40): wall time of "
                          "Context + set_private + one pai_encrypt_dev on device-resident x, synchronised; tables are "
                          "built only when the call reaches the break-even count (pai_ctx_fixed_base_policy); calls of "
-                         "<= 4096 elements run on 16-lane rows (k_crt_w / k_dec_w, PAI_OPT_CRT_ROWS_MAX); "
+                         "<= 4096 elements run on 16-lane rows (k_crt_w / k_dec_w, PAI_OPT_ROWS_MAX); "
                          "decrypt_wall_ms: pai_decrypt_dev of the call's ciphertexts on the same context")
         extra["fresh_key"] = fresh
     cpu_sample = args.cpu_sample if nb <= 2048 else min(args.cpu_sample, 4096)   # bounded CPU work at nb = 4096

@@ -70,7 +70,8 @@ static int fail(int code, const std::string& msg) {
 
 // Largest call (elements) whose CRT exponentiations run on 16-lane rows (k_crt_w) instead of lanes / lane pairs
 // (k_crt_a + k_crt_b_pair): below it the lane kernels leave the chip mostly idle and take one lane's whole chain.
-constexpr long long CRTW_DEFAULT_MAX = 4096;
+// The test build keeps 0, so that its contexts -- the cross-checks' references -- stay on the kernels the rows stand in for.
+constexpr long long CRTW_DEFAULT_MAX = FLEXPAI_XCHECK ? 0 : 4096;
 
 struct pai_ctx {
   int device = 0;
@@ -81,6 +82,8 @@ struct pai_ctx {
   HBig n, N;
   uint32_t mprime_N = 0;
   uint32_t *d_N = nullptr, *d_R2 = nullptr, *d_nl = nullptr;
+  uint32_t* d_pew_prog = nullptr;   // op list over n for k_pe_w (public-key encryption on 16-lane rows)
+  int pew_nprog = 0;
   uint32_t* d_prog = nullptr;   // Montgomery program for x^n (run_program, kernels.hpp)
   int nprog = 0;
   uint32_t* d_oneR = nullptr;   // R mod n^2
@@ -98,7 +101,7 @@ struct pai_ctx {
   bool fbg_ok = false;        // 4096-bit keys: fixed-base sampler on the group engine (engine_grp), no lane CRT
   bool crt_enabled = true;
   // calls of up to crtw_max elements run the CRT exponentiations on 16-lane rows (kernels_crtw.hpp: latency of
-  // protocol-sized calls); PAI_OPT_CRT_ROWS_MAX
+  // protocol-sized calls); PAI_OPT_ROWS_MAX
   long long crtw_max = CRTW_DEFAULT_MAX;
   int crt_sa = 0, crt_sb = 0;
   CrtHalf* d_crt_a = nullptr;   // [2] stage A halves
@@ -777,6 +780,16 @@ int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** ou
       (rc = upload(c, oneR.limbs(c->S_e, LB), &c->d_oneR)) || (rc = (SetupTrace("  setup_pe"), setup_pe(c, n)))) {
     delete c;
     return rc;
+  }
+  if (c->S_e == 74 || c->S_e == 148) {   // public-key encryption of protocol-sized calls on rows (k_pe_w)
+    std::vector<uint32_t> pw;
+    if (build_lane_program(n, pw)) {
+      if ((rc = upload(c, pw, &c->d_pew_prog))) {
+        delete c;
+        return rc;
+      }
+      c->pew_nprog = (int)pw.size();
+    }
   }
 #if FLEXPAI_XCHECK
   if (hipMalloc(&c->d_guard, sizeof(GuardRec)) != hipSuccess || hipMemset(c->d_guard, 0, sizeof(GuardRec)) != hipSuccess) {
@@ -1970,8 +1983,8 @@ int pai_ctx_set_option(pai_ctx* c, int option, int value) {
   CtxLock lk(c);
   switch (option) {
     case PAI_OPT_CRT_ENCRYPT: c->crt_enabled = value != 0; return 0;
-    case PAI_OPT_CRT_ROWS_MAX:
-      if (value < 0) return fail(PAI_ERR_ARG, "PAI_OPT_CRT_ROWS_MAX must be >= 0");
+    case PAI_OPT_ROWS_MAX:
+      if (value < 0) return fail(PAI_ERR_ARG, "PAI_OPT_ROWS_MAX must be >= 0");
       c->crtw_max = value;
       return 0;
     case PAI_OPT_STAGE_TIMING: c->timing = value != 0; stage_reset(c); return 0;
@@ -2004,7 +2017,7 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
   switch (option) {
     case PAI_OPT_CRT_ENCRYPT: *value = c->crt_enabled ? 1 : 0; return 0;
     case PAI_OPT_CRT_AVAILABLE: *value = c->crt_ok ? 1 : 0; return 0;
-    case PAI_OPT_CRT_ROWS_MAX: *value = (int)std::min<long long>(c->crtw_max, INT32_MAX); return 0;
+    case PAI_OPT_ROWS_MAX: *value = (int)std::min<long long>(c->crtw_max, INT32_MAX); return 0;
     case PAI_OPT_STAGE_TIMING: *value = c->timing ? 1 : 0; return 0;
     case PAI_OPT_LANE_DECRYPT: *value = (c->dec_lane_ok && c->dec_lane_enabled) ? 1 : 0; return 0;
     // 1 when device-RNG encryption will use the fixed bases (tables resident, or not yet tried)
@@ -2934,6 +2947,12 @@ int pai_encrypt_dev(pai_ctx* c, int dtype, const void* d_x, size_t N, int exp_mo
   if (obf_mode == PAI_OBF_RNG && c->pfb_enabled && pfb_supported(c) && pfb_wanted(c, p.n) && ensure_pfb(c)) {
     const int rc = launch_pfb(c, p, st);
     return rc ? rc : guard_collect(c, st);
+  }
+  if (obf_mode != PAI_OBF_NONE && p.n <= c->crtw_max && c->d_pew_prog) {   // protocol-sized: k_pe_w on rows
+    stage_mark(c, 0, st);
+    HIPCHK(pew_launch(c->S_e, p, c->d_pew_prog, c->pew_nprog, st));
+    stage_mark(c, 1, st);
+    return 0;
   }
   if (obf_mode != PAI_OBF_NONE && c->pe_ok && c->ct_words == 2 * 64) return launch_pe(c, p, st);
   switch (c->tpi_e) {

@@ -16,6 +16,9 @@
 //                     c~^(p_h - 1) R^-1 mod p_h^2 (the op list over p_h - 1), x made canonical, then the pair of x that
 //                     k_dec_fin_pair takes: A = x mod p_h (0 or 1: x == 1 mod p_h unless p_h | c, when x == 0) and
 //                     B = (x - A) / p_h, an exact division by REDC's digits (Q = -(x - A) p_h^-1 mod R_A, B = -Q).
+//   k_pe_w<K>         a public-key-only party's encryption the same way (encryptor.py:71-114, raw_encrypt.py:37-45,
+//                     obfuscator.py:36): c0 = 1 + n M mod n^2 on the row, r R mod n^2, the op list over n with c0 as
+//                     the final multiplier, over the K = 74 / 148 limbs of n^2 (k_encrypt's R = 2^(28 K)).
 //
 // Layout: lane t of a row owns limbs [t LW, t LW + LW) of the accumulator (bn_group.hpp's rotating CIOS with L ->
 // LW); every multiplicand sits in LDS as plain limbs (limb j = word j of a slot), read by the row as a broadcast,
@@ -489,6 +492,102 @@ __global__ __launch_bounds__(BLOCK_W) void k_dec_w(DecParams p) {
           o[(size_t)limb * p.n] = limb == 0 ? A : 0u;
           o[(size_t)(KA + limb) * p.n] = Bv[j];
         }
+      }
+    }
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(BLOCK_W) void k_pe_w(EncParams p, const uint32_t* prog_, int nprog_) {
+  constexpr int LW = Geom<K>::LW, SW = Geom<K>::W;
+  constexpr int NS = LANE_NTILE + 3;                    // the tiles, the squaring operand, the multiplier, c0
+  static_assert(RBUF_WORDS <= LANE_NTILE * SW, "r staging must fit the tiles it aliases");
+  __shared__ __attribute__((aligned(16))) uint32_t sm[(GPW * NS + 1) * SW];
+  const int lane = threadIdx.x, tig = lane & (TPI - 1), g = lane / TPI;
+  uint32_t* T = sm + g * NS * SW;
+  uint32_t* SQ = T + LANE_NTILE * SW;
+  uint32_t* MU = SQ + SW;
+  uint32_t* C0 = MU + SW;
+  uint32_t* CR = sm + GPW * NS * SW;                    // R^2 mod n^2
+  for (int w = lane; w < SW; w += BLOCK_W) CR[w] = w < K ? p.R2[w] : 0u;
+  uint32_t m[LW];
+  load_const<LW>(p.N, K, m, tig);
+  const uint32_t mprime = p.mprime;
+  const uint32_t* prog = uniform_ptr(prog_);
+  const int nprog = __builtin_amdgcn_readfirstlane(nprog_);
+  const bool given = p.obf == 1;
+  const int nw = given ? p.r_words : p.rng_words;
+  for (long long base = (long long)blockIdx.x * GPW; base < p.n; base += (long long)gridDim.x * GPW) {
+    const long long i = base + g;
+    const bool valid = i < p.n;
+    const long long ii = valid ? i : p.n - 1;
+    int64_t M = 0;
+    int e = 0, st;
+    const bool fixed = p.exp_mode != 0;
+    if (p.dtype == 0) st = encode_float((double)((const float*)p.x)[ii], fixed, p.fexp, M, e);
+    else if (p.dtype == 1) st = encode_float(((const double*)p.x)[ii], fixed, p.fexp, M, e);
+    else st = encode_int(((const int64_t*)p.x)[ii], fixed, p.fexp, M, e);
+    {   // c0 = 1 + n M mod n^2 (n^2 - n |M| + 1 for M < 0: raw_encrypt.py's "sneaky inverse" gives the same value)
+      const bool neg = M < 0;
+      const uint64_t mag = neg ? (uint64_t)0 - (uint64_t)M : (uint64_t)M;
+      const uint32_t M0 = (uint32_t)mag & LMASK, M1 = (uint32_t)(mag >> LB) & LMASK, M2 = (uint32_t)(mag >> (2 * LB));
+      uint64_t P[LW];
+#pragma unroll
+      for (int j = 0; j < LW; ++j) {
+        const int k = tig * LW + j;
+        const uint64_t a0 = k < K ? p.nl[k] : 0u;
+        const uint64_t a1 = k >= 1 && k - 1 < K ? p.nl[k - 1] : 0u;
+        const uint64_t a2 = k >= 2 && k - 2 < K ? p.nl[k - 2] : 0u;
+        P[j] = a0 * M0 + a1 * M1 + a2 * M2;
+      }
+      uint32_t X[LW], D[LW];
+      normalize<LW, 0>(P, X, lane, tig);
+      (void)sub<LW>(m, X, D, lane, tig);
+#pragma unroll
+      for (int j = 0; j < LW; ++j) P[j] = (uint64_t)(neg ? D[j] : X[j]) + ((tig == 0 && j == 0) ? 1u : 0u);
+      normalize<LW, 0>(P, X, lane, tig);
+      put<LW, SW>(C0, X, tig);
+    }
+    // r: the caller's words or this element's ChaCha20 stream (k_encrypt's), staged in the tiles
+    uint32_t* RW = T;
+    wave_lds_fence();
+    if (given) {
+      const uint32_t* rg = p.r + ii * p.r_stride;
+      for (int w = tig; w < nw; w += TPI) RW[w] = rg[w];
+    } else {
+      const unsigned long long gi = p.index_base + (unsigned long long)ii;
+      for (int b = tig; b * 16 < nw; b += TPI) {
+        uint32_t blk[16];
+        chacha20_block(p.rng_key, (uint32_t)b, (uint32_t)gi, (uint32_t)(gi >> 32), 0x66786169u, blk);
+#pragma unroll
+        for (int w = 0; w < 16; ++w) RW[b * 16 + w] = blk[w];
+      }
+    }
+    wave_lds_fence();
+    uint32_t a[LW];
+#pragma unroll
+    for (int j = 0; j < LW; ++j) {
+      const int bit = (tig * LW + j) * LB, wi = bit >> 5, sh = bit & 31;
+      const uint64_t lo = wi < nw ? (uint64_t)RW[wi] : 0ull;
+      const uint64_t hi = wi + 1 < nw ? (uint64_t)RW[wi + 1] : 0ull;
+      a[j] = (uint32_t)(((hi << 32) | lo) >> sh) & LMASK;
+    }
+    mont<K>(a, CR, m, mprime, lane, tig);                         // r R (r < 4 n^2, R > 8 n^2)
+    put<LW, SW>(T, a, tig);
+    run<K, SW>(a, T, SQ, MU, C0, prog, nprog, m, mprime, lane, tig);   // r^n c0 (< 2 n^2)
+    {
+      uint32_t d[LW];
+      if (!sub<LW>(a, m, d, lane, tig)) {
+#pragma unroll
+        for (int j = 0; j < LW; ++j) a[j] = d[j];
+      }
+    }
+    put<LW, SW>(SQ, a, tig);
+    if (valid) {
+      for (int w = tig; w < p.ct_words; w += TPI) p.ct[ii * p.ct_words + w] = limbs_word(SQ, SW, w);
+      if (tig == 0) {
+        p.exp[ii] = e;
+        if (p.status) p.status[ii] = st;
       }
     }
   }

@@ -28,7 +28,7 @@ EL_OK, EL_INT, EL_INT_BIG, EL_OVERFLOW, EL_FLOAT_OVF, EL_ENC_RANGE = 0, 1, 2, 3,
 
 PAI_OPT_CRT_ENCRYPT, PAI_OPT_CRT_AVAILABLE, PAI_OPT_STAGE_TIMING, PAI_OPT_LANE_DECRYPT = 1, 2, 3, 4
 PAI_OPT_FIXED_BASE, PAI_OPT_FB_WINDOW, PAI_OPT_FB_READY, PAI_OPT_FB_PAIR, PAI_OPT_PAIR = 5, 6, 7, 8, 9
-PAI_OPT_SPLIT_SAMPLER, PAI_OPT_CRT_ROWS_MAX = 13, 14
+PAI_OPT_SPLIT_SAMPLER, PAI_OPT_ROWS_MAX = 13, 14
 PAI_OPT_PUBLIC_FB, PAI_OPT_PFB_READY, PAI_OPT_PFB_WINDOW = 10, 11, 12
 PFB_NBASES = 33
 
@@ -334,13 +334,13 @@ class Context:
         return [float(buf[i]) for i in range(cnt.value)]
 
     @property
-    def crt_rows_max(self) -> int:
+    def rows_max(self) -> int:
         """Largest CRT encryption / decryption call (elements) that runs on 16-lane rows (k_crt_w / k_dec_w)."""
-        return int(self._get_option(PAI_OPT_CRT_ROWS_MAX))
+        return int(self._get_option(PAI_OPT_ROWS_MAX))
 
-    def set_crt_rows_max(self, n: int):
+    def set_rows_max(self, n: int):
         """0 keeps every CRT encryption / decryption on the lane kernels (k_crt_a + k_crt_b_pair, k_dec_*_pair); same bits."""
-        self._chk(self.lib.pai_ctx_set_option(self._h, PAI_OPT_CRT_ROWS_MAX, int(n)))
+        self._chk(self.lib.pai_ctx_set_option(self._h, PAI_OPT_ROWS_MAX, int(n)))
 
     def set_crt(self, enabled: bool):
         """Encrypt through the private-key CRT kernels (default when available) or the public-key one.

@@ -140,10 +140,11 @@ typedef struct pai_comm pai_comm;
                                   * Shoup rows (kernels_sgs.hpp: k_sgs, the default where they price lower than the
                                   * factored rows at their window; $FLEXPAI_SGS=0 keeps k_sgp, =1 takes them
                                   * whenever they fit)                                                        */
-#define PAI_OPT_CRT_ROWS_MAX 14  /* CRT encryption and decryption calls of at most this many elements (default 4096) run
-                                  * their exponentiations with each residue on a 16-lane row (kernels_crtw.hpp: k_crt_w,
-                                  * k_dec_w; the latency of protocol-sized calls) instead of one lane / lane pair each;
-                                  * 0 disables. Same bits either way                                            */
+#define PAI_OPT_ROWS_MAX 14      /* calls of at most this many elements (default 4096) run their exponentiations with
+                                  * each residue on a 16-lane row (kernels_crtw.hpp: the key holder's CRT encryption
+                                  * k_crt_w and decryption k_dec_w, a public-key-only party's encryption k_pe_w at
+                                  * 1024/2048 bits; the latency of protocol-sized calls) instead of one lane / lane
+                                  * pair each; 0 disables. Same bits either way                                  */
 
 /* Number of visible GPUs (0 when there is none or the runtime cannot start). */
 int pai_device_count(int* count);

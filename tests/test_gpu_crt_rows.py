@@ -1,7 +1,8 @@
-"""GPU parity of the 16-lane-row CRT encryption (kernels_crtw.hpp, k_crt_w: calls of at most PAI_OPT_CRT_ROWS_MAX
-elements) against the lane kernels it stands in for (k_crt_a + k_crt_b_pair, forced with crt_rows_max = 0), the
-public-key kernel and the CPU oracle (oracle/paillier_oracle.py encrypt_value: raw_encrypt.py:22-49 and
-obfuscator.py:23-37 of the reference). Bit-exact on every obfuscator mode, ragged counts and edge obfuscators."""
+"""GPU parity of the 16-lane-row kernels (kernels_crtw.hpp: calls of at most PAI_OPT_ROWS_MAX elements) against the
+kernels they stand in for (forced with rows_max = 0) and the CPU oracle (oracle/paillier_oracle.py: raw_encrypt.py:22-49,
+obfuscator.py:23-37, decryptor.py:33-127 of the reference): the key holder's CRT encryption k_crt_w (against k_crt_a +
+k_crt_b_pair) and decryption k_dec_w (against k_dec_pre/pow_pair), and a public-key-only party's encryption k_pe_w
+(against k_pe_* at 2048 bits, k_encrypt at 1024). Bit-exact on every obfuscator mode, ragged counts and edge inputs."""
 import numpy as np
 import pytest
 
@@ -39,13 +40,13 @@ def _both(crt, *args, **kw):
     try:
         a = crt.encrypt(*args, **kw)
         ka = len(crt.stage_times())
-        old = crt.crt_rows_max
-        crt.set_crt_rows_max(0)
+        old = crt.rows_max
+        crt.set_rows_max(0)
         try:
             b = crt.encrypt(*args, **kw)
             kb = len(crt.stage_times())
         finally:
-            crt.set_crt_rows_max(old)
+            crt.set_rows_max(old)
     finally:
         crt.set_stage_timing(False)
     assert (ka, kb) == (2, 3), "k_crt_w + k_crt_fin against k_crt_a + k_crt_b_pair + k_crt_fin"
@@ -55,10 +56,10 @@ def _both(crt, *args, **kw):
 def test_rows_default_threshold(ctxs):
     N = _native()
     crt, _, _ = ctxs[2048]
-    assert crt.crt_rows_max == 4096
+    assert crt.rows_max == 4096
     with pytest.raises(N.NativeError):
-        crt.set_crt_rows_max(-1)
-    assert crt.crt_rows_max == 4096
+        crt.set_rows_max(-1)
+    assert crt.rows_max == 4096
 
 
 @pytest.mark.parametrize("nb", [1024, 2048])
@@ -126,21 +127,21 @@ def test_rows_scalar_r_and_dtypes(ctxs, nb):
 
 
 def test_rows_threshold_boundary(ctxs):
-    """crt_rows_max elements run on rows, one more on the lane kernels; the bits agree."""
+    """rows_max elements run on rows, one more on the lane kernels; the bits agree."""
     N = _native()
     crt, _, key = ctxs[1024]
-    old = crt.crt_rows_max
+    old = crt.rows_max
     rk = b"t" * 32
     x = np.random.default_rng(3).standard_normal(65).astype(np.float32)
     crt.set_stage_timing(True)
     try:
-        crt.set_crt_rows_max(64)
+        crt.set_rows_max(64)
         a = crt.encrypt(x[:64], obf_mode=N.PAI_OBF_RNG, rng_key=rk)
         assert len(crt.stage_times()) == 2
         b = crt.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk)
         assert len(crt.stage_times()) == 3
     finally:
-        crt.set_crt_rows_max(old)
+        crt.set_rows_max(old)
         crt.set_stage_timing(False)
     assert np.array_equal(a[0], b[0][:64])
 
@@ -152,13 +153,13 @@ def _dboth(ctx, ct, ex):
     try:
         a = ctx.decrypt(ct, ex, want_raw=True)
         ka = len(ctx.stage_times())
-        old = ctx.crt_rows_max
-        ctx.set_crt_rows_max(0)
+        old = ctx.rows_max
+        ctx.set_rows_max(0)
         try:
             b = ctx.decrypt(ct, ex, want_raw=True)
             kb = len(ctx.stage_times())
         finally:
-            ctx.set_crt_rows_max(old)
+            ctx.set_rows_max(old)
     finally:
         ctx.set_stage_timing(False)
     assert (ka, kb) == (2, 3), "k_dec_w + k_dec_fin_pair against k_dec_pre_pair + k_dec_pow_pair + k_dec_fin_pair"
@@ -210,3 +211,73 @@ def test_rows_decrypt_roundtrip(ctxs, nb, count):
     ct, ex, _ = crt.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=bytes(range(32)), index_base=11)
     val = _dboth(crt, ct, ex)[0]
     assert np.array_equal(val, x.astype(np.float64))
+
+
+# ---------------------------------------------------------------- public-key encryption on rows (k_pe_w)
+def _pboth(pub, *args, **kw):
+    """(rows, chain): a public-key-only party's call on k_pe_w and on k_pe_* (2048) / k_encrypt (1024)."""
+    pub.set_stage_timing(True)
+    try:
+        a = pub.encrypt(*args, **kw)
+        ka = len(pub.stage_times())
+        old = pub.rows_max
+        pub.set_rows_max(0)
+        try:
+            b = pub.encrypt(*args, **kw)
+        finally:
+            pub.set_rows_max(old)
+    finally:
+        pub.set_stage_timing(False)
+    assert ka == 1, "one k_pe_w launch"
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    return a
+
+
+@pytest.mark.parametrize("nb", [1024, 2048])
+@pytest.mark.parametrize("count", [1, 5, 17, 1000])
+def test_rows_public_rng_matches_chain_and_oracle(ctxs, nb, count):
+    N = _native()
+    _, pub, key = ctxs[nb]
+    x = (np.random.default_rng(31 + count).standard_normal(count) * 10.0 ** np.random.default_rng(count).integers(-20, 20, count)).astype(np.float32)
+    x[::6] = 0.0
+    rk = bytes(range(9, 41))
+    base = (1 << 32) + 5
+    ct, ex, _ = _pboth(pub, x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=base)
+    got = N.words_to_ints(ct)
+    rbytes = ((nb + 64 + 31) // 32) * 4
+    for i in sorted({0, count // 2, count - 1}):
+        c, e = O.encrypt_value(x[i], key, O.device_r(rk, base + i, rbytes))
+        assert got[i] == c and int(ex[i]) == e, f"element {i}"
+
+
+@pytest.mark.parametrize("nb", [1024, 2048])
+def test_rows_public_golden_and_edge_obfuscators(golden, ctxs, nb):
+    """The reference goldens (explicit r), then r = 0, 1, 2, n - 1, n, n + 1, 5 p, n^2 - 1 and the all-ones word vector."""
+    N = _native()
+    _, pub, key = ctxs[nb]
+    recs = golden["encrypt"][str(nb)]
+    x = np.array([r["bits"] for r in recs], dtype=np.uint32).view(np.float32)
+    ct, ex, _ = _pboth(pub, x, obf_mode=N.PAI_OBF_GIVEN, r=[int(r["r"], 16) for r in recs])
+    got = N.words_to_ints(ct)
+    for i, rec in enumerate(recs):
+        assert (hex(got[i]), int(ex[i])) == (rec["c"], rec["e"]), f"element {i}"
+    k = key
+    rs = [0, 1, 2, k.n - 1, k.n, k.n + 1, 5 * k.p, k.nsquare - 1, (1 << (32 * pub.ct_words)) - 1]
+    x = np.array([0.0, 1.0, -1.0, 3.5, -2.25, 1e-30, -1e30, 7.0, -0.0], dtype=np.float32)
+    ct, _, _ = _pboth(pub, x, obf_mode=N.PAI_OBF_GIVEN, r=rs)
+    got = N.words_to_ints(ct)
+    for i, r in enumerate(rs):
+        assert got[i] == O.encrypt_value(x[i], k, r)[0], f"r #{i}"
+
+
+@pytest.mark.parametrize("nb", [1024, 2048])
+def test_rows_public_dtypes_and_scalar_r(ctxs, nb):
+    N = _native()
+    crt, pub, key = ctxs[nb]
+    r = 0x1234567890ABCDEF1234567 % key.n
+    for x in (np.array([0.0, -0.0, 1.5, -2.25, 3e-30, -7e20], dtype=np.float64),
+              np.array([0, 1, -1, 2 ** 40, -(2 ** 50), 123456789], dtype=np.int64)):
+        a = _pboth(pub, x, obf_mode=N.PAI_OBF_GIVEN, r_scalar=r)
+        b = crt.encrypt(x, obf_mode=N.PAI_OBF_GIVEN, r_scalar=r)
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])

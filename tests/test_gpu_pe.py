@@ -37,6 +37,7 @@ def _pub(monkeypatch, key, pair):
     monkeypatch.setenv("FLEXPAI_PAIR", "1" if pair else "0")
     ctx = N.Context(key.n, 0, lib=None if pair else N.load_library(N.XCHECK_LIB_PATH))
     assert bool(ctx.pair_paths & 4) == pair
+    ctx.set_rows_max(0)   # the chains under test, not k_pe_w (tests/test_gpu_crt_rows.py)
     return ctx
 
 

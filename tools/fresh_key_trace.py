@@ -5,7 +5,7 @@ on the host clock with the device synchronised, with $FLEXPAI_SETUP_TRACE's per-
 
     python tools/fresh_key_trace.py [--keys 3] [--n 1048576] [--nb 2048] [--rows-max N]
 
---rows-max sets PAI_OPT_CRT_ROWS_MAX (0: the lane kernels k_crt_a + k_crt_b_pair for every call size).
+--rows-max sets PAI_OPT_ROWS_MAX (0: the lane kernels k_crt_a + k_crt_b_pair for every call size).
 """
 import argparse
 import os
@@ -46,7 +46,7 @@ def main():
         t1 = time.perf_counter()
         c.set_private(sk.p, sk.q)
         if a.rows_max is not None:
-            c.set_crt_rows_max(a.rows_max)
+            c.set_rows_max(a.rows_max)
         t2 = time.perf_counter()
         c.set_stage_timing(True)
         rc = lib.pai_encrypt_dev(c.handle, N.PAI_F32, x.data_ptr(), a.n, 0, 0, N.PAI_OBF_RNG, None, 0, 0, bytes(32), 0,

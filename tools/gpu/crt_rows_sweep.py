@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Call-size sweep of the key holder's generic CRT encryption (device RNG, fixed bases off): k_crt_w on 16-lane rows
 (kernels_crtw.hpp) against k_crt_a + k_crt_b_pair on lanes, and of decryption (k_dec_w against k_dec_pre/pow_pair), warm
-calls, median of --reps, one JSON line per size; where the rows stop winning is PAI_OPT_CRT_ROWS_MAX's default. Usage:
+calls, median of --reps, one JSON line per size; where the rows stop winning is PAI_OPT_ROWS_MAX's default. Usage:
     python tools/gpu/crt_rows_sweep.py [--nb 2048] [--sizes 256,1024,2048,4096,8192,16384] [--reps 3]"""
 import argparse
 import json
@@ -41,7 +41,7 @@ def main():
         row = {"nb": a.nb, "n": n}
         outs = {}
         for name, cap in (("rows", n), ("lanes", 0)):
-            c.set_crt_rows_max(cap)
+            c.set_rows_max(cap)
             wall, kern = [], []
             for rep in range(a.reps + 1):
                 torch.cuda.synchronize()
@@ -62,7 +62,7 @@ def main():
         dst = torch.empty(n, dtype=torch.int32, device=dev)
         dec = {}
         for name, cap in (("rows", n), ("pairs", 0)):
-            c.set_crt_rows_max(cap)
+            c.set_rows_max(cap)
             wall, kern = [], []
             for rep in range(a.reps + 1):
                 torch.cuda.synchronize()

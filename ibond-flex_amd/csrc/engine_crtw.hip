@@ -8,6 +8,7 @@ hipError_t crtw_launch(int sa, const crtw::Params& p, hipStream_t st) {
   const int gx = (int)std::min<long long>(blocks, 1ll << 20);
   if (sa == 19) hipLaunchKernelGGL((crtw::k_crt_w<19, 37>), dim3(gx, 2), dim3(crtw::BLOCK_W), 0, st, p);
   else if (sa == 37) hipLaunchKernelGGL((crtw::k_crt_w<37, 74>), dim3(gx, 2), dim3(crtw::BLOCK_W), 0, st, p);
+  else if (sa == 74) hipLaunchKernelGGL((crtw::k_crt_w<74, 148>), dim3(gx, 2), dim3(crtw::BLOCK_W), 0, st, p);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
@@ -17,6 +18,7 @@ hipError_t decw_launch(int sa, const crtw::DecParams& p, hipStream_t st) {
   const int gx = (int)std::min<long long>(blocks, 1ll << 20);
   if (sa == 19) hipLaunchKernelGGL((crtw::k_dec_w<19, 37>), dim3(gx, 2), dim3(crtw::BLOCK_W), 0, st, p);
   else if (sa == 37) hipLaunchKernelGGL((crtw::k_dec_w<37, 74>), dim3(gx, 2), dim3(crtw::BLOCK_W), 0, st, p);
+  else if (sa == 74) hipLaunchKernelGGL((crtw::k_dec_w<74, 148>), dim3(gx, 2), dim3(crtw::BLOCK_W), 0, st, p);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

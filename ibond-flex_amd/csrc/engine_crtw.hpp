@@ -6,7 +6,7 @@
 
 namespace fpai {
 
-// k_crt_w<sa, 2 sa> over p.n elements, both halves (grid blocks x 2); hipErrorInvalidValue for other sizes
+// k_crt_w<sa, 2 sa> (sa = 19, 37, 74) over p.n elements, both halves (grid blocks x 2); hipErrorInvalidValue for other sizes
 hipError_t crtw_launch(int sa, const crtw::Params& p, hipStream_t st);
 // k_dec_w<sa, 2 sa>: the pairs k_dec_fin_pair takes, for p.n elements, both halves
 hipError_t decw_launch(int sa, const crtw::DecParams& p, hipStream_t st);

@@ -23,6 +23,18 @@ int dec4_geometry(int cus, long long chunk, Dec4Geom* g) {
   return 0;
 }
 
+hipError_t dec4_launch_tail(const Dec4Params& p, const DecParams& f, const Dec4Geom& g, hipStream_t st) {
+  const long long lb = (p.n + LANE_BLOCK - 1) / LANE_BLOCK;
+  constexpr int GPB = BLOCK / 4;
+  const long long fb = (p.n + GPB - 1) / GPB;
+  hipLaunchKernelGGL(k_dec4_L<D4_S>, dim3((int)std::min<long long>(g.gx_L, lb), 2), dim3(LANE_BLOCK), 0, st, p);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_dec4_fin<4>, dim3((int)std::min<long long>(g.gx_fin, fb)), dim3(BLOCK), g.lds_fin, st, f,
+                     (const uint32_t*)p.mh);
+  return hipGetLastError();
+}
+
 hipError_t dec4_launch(const Dec4Params& p, const DecParams& f, const Dec4Geom& g, hipStream_t st, hipEvent_t* ev) {
   const long long pb = (p.n + D4_PAIRS - 1) / D4_PAIRS, lb = (p.n + LANE_BLOCK - 1) / LANE_BLOCK;
   constexpr int GPB = BLOCK / 4;

@@ -14,5 +14,7 @@ struct Dec4Geom {
 int dec4_geometry(int cus, long long chunk, Dec4Geom* g);
 // k_dec4_pre, k_dec4_pow, k_dec4_L (halves on blockIdx.y), k_dec4_fin on `st`; ev[0..3] nullable
 hipError_t dec4_launch(const Dec4Params& p, const DecParams& f, const Dec4Geom& g, hipStream_t st, hipEvent_t* ev);
+// k_dec4_L + k_dec4_fin alone, on pairs another kernel left in p.x (k_dec_w<74, 148>)
+hipError_t dec4_launch_tail(const Dec4Params& p, const DecParams& f, const Dec4Geom& g, hipStream_t st);
 
 }  // namespace fpai

@@ -104,6 +104,7 @@ struct pai_ctx {
   // protocol-sized calls); PAI_OPT_ROWS_MAX
   long long crtw_max = CRTW_DEFAULT_MAX;
   int crt_sa = 0, crt_sb = 0;
+  int rows_sa = 0;   // 74: a 4096-bit key's row-kernel constants (k_crt_w<74, 148>, k_dec_w<74, 148>; setup_rows4096)
   CrtHalf* d_crt_a = nullptr;   // [2] stage A halves
   CrtHalf* d_crt_b = nullptr;   // [2] stage B halves
   uint32_t *d_kq = nullptr, *d_kp = nullptr;
@@ -1732,6 +1733,58 @@ static int setup_fbg(pai_ctx* c, const HBig& p, const HBig& q) {
   return 0;
 }
 
+// A 4096-bit key's constants for the row kernels (kernels_crtw.hpp; the lane CRT kernels stop at 2048 bits): per
+// half, stage A over the 74 limbs of p_h (R^(K+1) mod p_h, the op list over q_h mod (p_h - 1)), stage B over the 148
+// limbs of p_h^2 (R^2, coef, the op list over p_h) and decryption (R^(K+1) mod p_h^2, the op list over p_h - 1); the
+// finish reuses setup_fbg's q^2 R^2 / p^2 R^2 mod n^2 and the k_dec4 halves. Soft: an unusable key leaves rows_sa = 0.
+static int setup_rows4096(pai_ctx* c, const HBig& p, const HBig& q) {
+  constexpr int SA = 74, SB = 148;
+  c->rows_sa = 0;
+  if (c->tpi_e != 8 || !c->d_kq || std::max(p.bits(), q.bits()) + 2 > (size_t)LB * SA) return 0;
+  const size_t RA = (size_t)LB * SA, RB = (size_t)LB * SB;
+  const int kd = (int)((32 * (size_t)c->ct_words + RB - 1) / RB);
+  if (kd > KMAX_CHUNKS) return 0;
+  SetupTrace tr("    rows 4096 consts");
+  const HBig primes[2] = {p, q};
+  const HBig sq[2] = {mul(p, p), mul(q, q)};
+  CrtHalf ha[2], hb[2], hd[2];
+  int rc;
+  for (int h = 0; h < 2; ++h) {
+    const HBig& ph = primes[h];
+    const HBig& m2 = sq[h];
+    std::vector<uint32_t> pa, pb, pd;
+    if (!build_lane_program(mod(primes[1 - h], sub(ph, HBig(1))), pa) || !build_lane_program(ph, pb) ||
+        !build_lane_program(sub(ph, HBig(1)), pd))
+      return 0;
+    const HBig coef = inv_mod(sq[1 - h], m2);
+    if (coef.is_zero()) return 0;
+    std::vector<uint32_t> ck;
+    for (int K = 1; K <= KMAX_CHUNKS; ++K) {
+      std::vector<uint32_t> v = mul_pow2_mod(HBig(1), RA * (K + 1), ph).limbs(SA, LB);
+      ck.insert(ck.end(), v.begin(), v.end());
+    }
+    std::vector<uint32_t> oneA(SA, 0), oneB(SB, 0);
+    oneA[0] = oneB[0] = 1;
+    uint32_t *dm, *dck, *done, *dpa, *dm2, *dr2, *dcoef, *dpb, *dck2, *done2, *dpd;
+    if ((rc = upload(c, ph.limbs(SA, LB), &dm)) || (rc = upload(c, ck, &dck)) || (rc = upload(c, oneA, &done)) ||
+        (rc = upload(c, pa, &dpa)) || (rc = upload(c, m2.limbs(SB, LB), &dm2)) ||
+        (rc = upload(c, mul_pow2_mod(HBig(1), 2 * RB, m2).limbs(SB, LB), &dr2)) ||
+        (rc = upload(c, coef.limbs(SB, LB), &dcoef)) || (rc = upload(c, pb, &dpb)) ||
+        (rc = upload(c, mul_pow2_mod(HBig(1), RB * (kd + 1), m2).limbs(SB, LB), &dck2)) ||
+        (rc = upload(c, oneB, &done2)) || (rc = upload(c, pd, &dpd)))
+      return rc;
+    ha[h] = CrtHalf{dm, dck, done, dpa, (int)pa.size(), mont_prime(ph, LB)};
+    hb[h] = CrtHalf{dm2, dr2, dcoef, dpb, (int)pb.size(), mont_prime(m2, LB)};
+    hd[h] = CrtHalf{dm2, dck2, done2, dpd, (int)pd.size(), mont_prime(m2, LB)};
+  }
+  std::vector<CrtHalf> va(ha, ha + 2), vb(hb, hb + 2), vd(hd, hd + 2);
+  if ((rc = upload(c, va, &c->d_crt_a)) || (rc = upload(c, vb, &c->d_crt_b)) || (rc = upload(c, vd, &c->d_decw)))
+    return rc;
+  c->decw_kchunks = kd;
+  c->rows_sa = SA;
+  return 0;
+}
+
 // CRT encryption constants (kernels_crt.hpp). p < q here (sorted like keypair.py:57-62).
 static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
   c->crt_ok = c->fbg_ok = c->dec_pair_ok = c->crt_pair_ok = c->dec4_ok = false;
@@ -1744,7 +1797,10 @@ static int setup_crt(pai_ctx* c, const HBig& p, const HBig& q) {
       break;
     }
   }
-  if (!sa) return setup_fbg(c, p, q);   // too large for the lane engine: fixed-base on the group engine
+  if (!sa) {   // too large for the lane engine: fixed-base on the group engine, protocol-sized calls on rows
+    int rc0 = setup_fbg(c, p, q);
+    return rc0 ? rc0 : setup_rows4096(c, p, q);
+  }
   const size_t RA = (size_t)LB * sa, RB = (size_t)LB * sb, RE = (size_t)LB * c->S_e;
   const HBig primes[2] = {p, q};
   const HBig sq[2] = {mul(p, p), mul(q, q)};
@@ -1910,6 +1966,7 @@ int pai_ctx_set_private(pai_ctx* c, const uint8_t* p_le, const uint8_t* q_le, si
     c->has_priv = c->crt_ok = c->fbg_ok = c->dec_lane_ok = c->dec_pair_ok = c->crt_pair_ok = c->dec4_ok = false;
     c->d_decw = nullptr;
     c->decw_kchunks = 0;
+    c->rows_sa = 0;
     c->fb_state = pai_ctx::FB_UNTRIED;
     g_last_error = msg;
   }
@@ -2800,6 +2857,7 @@ static int crt_finish(pai_ctx* c, const EncParams& e, const uint32_t* u, int sb,
   switch (c->tpi_e) {
     case 2: return launch_crt_fin<2>(c, f, st);
     case 4: return launch_crt_fin<4>(c, f, st);
+    case 8: return launch_crt_fin<8>(c, f, st);
   }
   return fail(PAI_ERR_KEY, "CRT finish: unsupported group size");
 }
@@ -2939,6 +2997,12 @@ int pai_encrypt_dev(pai_ctx* c, int dtype, const void* d_x, size_t N, int exp_mo
   if (obf_mode == PAI_OBF_RNG && c->fbg_ok && c->crt_enabled && c->fb_enabled && fb_wanted(c, p.n) && ensure_fb(c)) {
     const int rc = launch_fb(c, p, st);
     return rc ? rc : guard_collect(c, st);
+  }
+  if (obf_mode != PAI_OBF_NONE && c->rows_sa && c->crt_enabled && p.n <= c->crtw_max) {   // 4096 bits, protocol-sized
+    const int r_words = obf_mode == PAI_OBF_GIVEN ? p.r_words : p.rng_words;
+    const int kchunks = (32 * r_words + LB * c->rows_sa - 1) / (LB * c->rows_sa);
+    if (kchunks <= KMAX_CHUNKS && r_words <= crtw::RW_WORDS)
+      return launch_crtw(c, p, c->rows_sa, 2 * c->rows_sa, r_words, kchunks, st);
   }
   if (obf_mode != PAI_OBF_NONE && c->crt_ok && c->crt_enabled) {
     if (c->crt_sa == 19) return launch_crt<19, 37>(c, p, st);
@@ -3115,8 +3179,36 @@ static int launch_dec_pair(pai_ctx* c, const DecParams& d, hipStream_t st) {
 }
 
 // 4096-bit split-pair decryption (kernels_dec4.hpp, engine_dec4.hip), in chunks of CRT_CHUNK elements
+// A 4096-bit call of at most crtw_max ciphertexts: c^(p_h - 1) mod p_h^2 on rows (k_dec_w<74, 148>) into the pairs
+// k_dec4_L takes, then k_dec4_L and k_dec4_fin; stage times: k_dec_w, k_dec4_L + k_dec4_fin.
+static int launch_decw4(pai_ctx* c, const DecParams& d, hipStream_t st) {
+  const long long N = d.n;
+  Dec4Geom g;
+  dec4_geometry(c->cus, N, &g);
+  const size_t xbytes = (size_t)2 * 2 * D4_S * 4, mbytes = (size_t)2 * D4_S * 4;   // per element
+  int rc = ensure_work(c, (xbytes + mbytes) * N);
+  if (rc) return rc;
+  Dec4Params p{};
+  p.halves = c->d_dec4_halves;
+  p.n = N;
+  p.ct = d.ct;
+  p.ct_words = c->ct_words;
+  p.kchunks = c->dec4_kchunks;
+  p.x = (uint32_t*)c->d_work;
+  p.mh = (uint32_t*)((char*)c->d_work + xbytes * N);
+  p.scratch = (uint32_t*)c->d_scratch;
+  crtw::DecParams w{c->d_decw, c->d_crt_a, N, d.ct, c->ct_words, c->decw_kchunks, p.x};
+  stage_mark(c, 0, st);
+  HIPCHK(decw_launch(c->rows_sa, w, st));
+  stage_mark(c, 1, st);
+  HIPCHK(dec4_launch_tail(p, d, g, st));
+  stage_mark(c, 2, st);
+  return 0;
+}
+
 static int launch_dec4(pai_ctx* c, const DecParams& d, hipStream_t st) {
   const long long N = d.n;
+  if (N <= c->crtw_max && c->rows_sa && c->d_decw) return launch_decw4(c, d, st);
   const long long chunk = std::min(N, CRT_CHUNK);
   Dec4Geom g;
   dec4_geometry(c->cus, chunk, &g);

@@ -285,6 +285,7 @@ struct Params {
   uint32_t* out;                // u [2][KB][n]
 };
 
+constexpr int RW_WORDS = 256;          // staging of r / the ciphertext: up to 8192 bits (a 4096-bit key's ct_words)
 template <int KA, int KB>
 constexpr int slot_words() { return Geom<KB>::W > Geom<KA>::W ? Geom<KB>::W : Geom<KA>::W; }
 constexpr int NSLOT = LANE_NTILE + 2;   // the op list's tiles, the squaring operand, the multiplier
@@ -296,7 +297,7 @@ __global__ __launch_bounds__(BLOCK_W) void k_crt_w(Params p) {
   constexpr int LA = Geom<KA>::LW, LBW = Geom<KB>::LW;
   constexpr int SW = slot_words<KA, KB>();
   constexpr int CS = (KA + 3) & ~3;                     // stage A: one r chunk per CS words
-  static_assert(RBUF_WORDS + KMAX_CHUNKS * CS <= LANE_NTILE * SW, "r staging must fit the tiles it aliases");
+  static_assert(RW_WORDS + KMAX_CHUNKS * CS <= LANE_NTILE * SW, "r staging must fit the tiles it aliases");
   static_assert(SW % 4 == 0, "16-byte slots");
   __shared__ __attribute__((aligned(16))) uint32_t sm[lds_words<KA, KB>()];
   const int half = blockIdx.y;
@@ -329,7 +330,7 @@ __global__ __launch_bounds__(BLOCK_W) void k_crt_w(Params p) {
     const long long ii = i < p.n ? i : p.n - 1;
     // r words -> the row's staging words (aliasing the tiles), then r's 28-bit limbs chunk by chunk
     uint32_t* RW = T;
-    uint32_t* RL = T + RBUF_WORDS;
+    uint32_t* RL = T + RW_WORDS;
     wave_lds_fence();
     if (given) {
       const uint32_t* rg = p.r + ii * p.r_stride;
@@ -399,7 +400,7 @@ __global__ __launch_bounds__(BLOCK_W) void k_dec_w(DecParams p) {
   constexpr int LBW = Geom<KB>::LW;
   constexpr int SW = slot_words<KA, KB>();
   constexpr int CS = (KB + 3) & ~3;                     // one ciphertext chunk per CS words
-  static_assert(RBUF_WORDS + KMAX_CHUNKS * CS <= LANE_NTILE * SW, "ciphertext staging must fit the tiles it aliases");
+  static_assert(RW_WORDS + KMAX_CHUNKS * CS <= LANE_NTILE * SW, "ciphertext staging must fit the tiles it aliases");
   __shared__ __attribute__((aligned(16))) uint32_t sm[lds_words<KA, KB>()];
   const int half = blockIdx.y;
   const CrtHalf* HD = p.hd + half;
@@ -421,7 +422,7 @@ __global__ __launch_bounds__(BLOCK_W) void k_dec_w(DecParams p) {
     const long long i = base + g;
     const long long ii = i < p.n ? i : p.n - 1;
     uint32_t* RW = T;
-    uint32_t* RL = T + RBUF_WORDS;
+    uint32_t* RL = T + RW_WORDS;
     wave_lds_fence();
     {
       const uint32_t* cw = p.ct + ii * p.ct_words;
@@ -501,7 +502,7 @@ template <int K>
 __global__ __launch_bounds__(BLOCK_W) void k_pe_w(EncParams p, const uint32_t* prog_, int nprog_) {
   constexpr int LW = Geom<K>::LW, SW = Geom<K>::W;
   constexpr int NS = LANE_NTILE + 3;                    // the tiles, the squaring operand, the multiplier, c0
-  static_assert(RBUF_WORDS <= LANE_NTILE * SW, "r staging must fit the tiles it aliases");
+  static_assert(RW_WORDS <= LANE_NTILE * SW, "r staging must fit the tiles it aliases");
   __shared__ __attribute__((aligned(16))) uint32_t sm[(GPW * NS + 1) * SW];
   const int lane = threadIdx.x, tig = lane & (TPI - 1), g = lane / TPI;
   uint32_t* T = sm + g * NS * SW;

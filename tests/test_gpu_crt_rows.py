@@ -281,3 +281,96 @@ def test_rows_public_dtypes_and_scalar_r(ctxs, nb):
         a = _pboth(pub, x, obf_mode=N.PAI_OBF_GIVEN, r_scalar=r)
         b = crt.encrypt(x, obf_mode=N.PAI_OBF_GIVEN, r_scalar=r)
         assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+# ---------------------------------------------------------------- 4096-bit keys on rows (k_crt_w<74, 148>, k_dec_w<74, 148>)
+@pytest.fixture(scope="module")
+def ctx4096(golden):
+    N = _native()
+    key = _key(golden, 4096)
+    c = N.Context(key.n, 0, key.p, key.q)
+    c.set_fixed_base(False)
+    return c, key
+
+
+def _counts(ctx, fn):
+    ctx.set_stage_timing(True)
+    try:
+        r = fn()
+        return r, len(ctx.stage_times())
+    finally:
+        ctx.set_stage_timing(False)
+
+
+def _both4096(ctx, call):
+    a, ka = _counts(ctx, call)
+    old = ctx.rows_max
+    ctx.set_rows_max(0)
+    try:
+        b, kb = _counts(ctx, call)
+    finally:
+        ctx.set_rows_max(old)
+    return a, b, ka, kb
+
+
+def test_rows_4096_encrypt_golden_and_rng(golden, ctx4096):
+    """Against the reference goldens (explicit r) and, on the device stream, against the group engine's k_encrypt<8>
+    and the oracle."""
+    N = _native()
+    ctx, key = ctx4096
+    recs = golden["encrypt"]["4096"]
+    x = np.array([r["bits"] for r in recs], dtype=np.uint32).view(np.float32)
+    rs = [int(r["r"], 16) for r in recs]
+    a, b, ka, kb = _both4096(ctx, lambda: ctx.encrypt(x, obf_mode=N.PAI_OBF_GIVEN, r=rs))
+    assert (ka, kb) == (2, 1), "k_crt_w + k_crt_fin against k_encrypt<8>"
+    got = N.words_to_ints(a[0])
+    for i, rec in enumerate(recs):
+        assert (hex(got[i]), int(a[1][i])) == (rec["c"], rec["e"]), f"element {i}"
+    assert np.array_equal(a[0], b[0])
+    x = np.random.default_rng(4096).standard_normal(37).astype(np.float32)
+    rk = bytes(range(5, 37))
+    a, b, _, _ = _both4096(ctx, lambda: ctx.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=99))
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    got = N.words_to_ints(a[0])
+    rbytes = ((4096 + 64 + 31) // 32) * 4
+    for i in (0, 18, 36):
+        assert got[i] == O.encrypt_value(x[i], key, O.device_r(rk, 99 + i, rbytes))[0], f"element {i}"
+
+
+def test_rows_4096_edge_obfuscators(ctx4096):
+    N = _native()
+    ctx, key = ctx4096
+    k = key
+    rs = [1, 2, k.n - 1, k.n, k.n + 1, 5 * k.p, 3 * k.q, k.nsquare - 1, (1 << (32 * ctx.ct_words)) - 1]
+    x = np.linspace(-3, 3, len(rs)).astype(np.float32)
+    a, b, _, _ = _both4096(ctx, lambda: ctx.encrypt(x, obf_mode=N.PAI_OBF_GIVEN, r=rs))
+    assert np.array_equal(a[0], b[0])
+    got = N.words_to_ints(a[0])
+    for i, r in enumerate(rs):
+        assert got[i] == O.encrypt_value(x[i], k, r)[0], f"r #{i}"
+
+
+def test_rows_4096_decrypt_edges_and_roundtrip(ctx4096):
+    """k_dec_w<74, 148> + k_dec4_L + k_dec4_fin against the split-pair chain (k_dec4_pre/pow) and the oracle: c = 0,
+    multiples of p, q, p^2, q^2, c >= n^2, all-ones words, random words, and a round trip."""
+    N = _native()
+    ctx, key = ctx4096
+    W = ctx.ct_words
+    top = (1 << (32 * W)) - 1
+    cs = [0, 1, 2, key.p, key.q, 3 * key.p, key.p * key.q, key.psquare, key.qsquare, key.nsquare - 1, key.nsquare,
+          top, (key.n + 1) % key.nsquare, pow(key.n + 1, 5, key.nsquare)]
+    rng = np.random.default_rng(4097)
+    cs += [int.from_bytes(rng.bytes(4 * W), "little") for _ in range(10)]
+    ct = N.ints_to_words(cs, W)
+    ex = np.array([(i % 5) - 1 for i in range(len(cs))], dtype=np.int32)
+    a, b, ka, kb = _both4096(ctx, lambda: ctx.decrypt(ct, ex, want_raw=True))
+    assert (ka, kb) == (2, 3), "k_dec_w + (k_dec4_L, k_dec4_fin) against k_dec4_pre/pow/L + fin"
+    for u, v in zip(a, b):
+        assert np.array_equal(np.asarray(u).view(np.uint8), np.asarray(v).view(np.uint8))
+    raw = N.words_to_ints(a[3])
+    for i, c in enumerate(cs):
+        assert raw[i] == O.raw_decrypt(c, key), f"element {i}"
+    x = (rng.standard_normal(300) * 1e3).astype(np.float32)
+    ct, ex, _ = ctx.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=bytes(32), index_base=3)
+    (val, _, _, _), _, _, _ = _both4096(ctx, lambda: ctx.decrypt(ct, ex))
+    assert np.array_equal(val, x.astype(np.float64))

@@ -374,3 +374,18 @@ def test_rows_4096_decrypt_edges_and_roundtrip(ctx4096):
     ct, ex, _ = ctx.encrypt(x, obf_mode=N.PAI_OBF_RNG, rng_key=bytes(32), index_base=3)
     (val, _, _, _), _, _, _ = _both4096(ctx, lambda: ctx.decrypt(ct, ex))
     assert np.array_equal(val, x.astype(np.float64))
+
+
+def test_rows_largest_call_all_kernels(ctxs):
+    """rows_max elements (the largest call the rows take, 1024 of them per wave-row group of the grid) at nb = 1024:
+    holder encryption, decryption and public encryption against the kernels they stand in for."""
+    N = _native()
+    crt, pub, _ = ctxs[1024]
+    n = crt.rows_max
+    x = (np.random.default_rng(n).standard_normal(n) * 100).astype(np.float32)
+    kw = dict(obf_mode=N.PAI_OBF_RNG, rng_key=bytes(range(11, 43)), index_base=(1 << 40) - 7)
+    a, b = _both(crt, x, **kw)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    val = _dboth(crt, a[0], a[1])[0]
+    assert np.array_equal(val, x.astype(np.float64))
+    _pboth(pub, x, **kw)

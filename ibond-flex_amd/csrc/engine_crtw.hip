@@ -28,6 +28,7 @@ hipError_t pew_launch(int k, const EncParams& p, const uint32_t* prog, int nprog
   const int gx = (int)std::min<long long>(blocks, 1ll << 20);
   if (k == 74) hipLaunchKernelGGL((crtw::k_pe_w<74>), dim3(gx), dim3(crtw::BLOCK_W), 0, st, p, prog, nprog);
   else if (k == 148) hipLaunchKernelGGL((crtw::k_pe_w<148>), dim3(gx), dim3(crtw::BLOCK_W), 0, st, p, prog, nprog);
+  else if (k == 296) hipLaunchKernelGGL((crtw::k_pe_w<296>), dim3(gx), dim3(crtw::BLOCK_W), 0, st, p, prog, nprog);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

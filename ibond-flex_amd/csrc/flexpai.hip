@@ -782,7 +782,7 @@ int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** ou
     delete c;
     return rc;
   }
-  if (c->S_e == 74 || c->S_e == 148) {   // public-key encryption of protocol-sized calls on rows (k_pe_w)
+  if (c->S_e == 74 || c->S_e == 148 || c->S_e == 296) {   // public-key encryption of protocol-sized calls on rows (k_pe_w)
     std::vector<uint32_t> pw;
     if (build_lane_program(n, pw)) {
       if ((rc = upload(c, pw, &c->d_pew_prog))) {

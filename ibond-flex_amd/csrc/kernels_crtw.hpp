@@ -80,11 +80,27 @@ struct Digits {
   }
 };
 
+// LW consecutive steps from a digit index that is a multiple of LW (so step s has rotation s)
+template <int LW, int... Ss>
+__device__ __forceinline__ void step_group(uint64_t (&P)[LW], const uint32_t (&a)[LW], const uint32_t* Bg,
+                                           const uint32_t (&m)[LW], uint32_t mprime, std::integer_sequence<int, Ss...>) {
+  (step<LW, Ss>(P, a, Bg[Ss], m, mprime), ...);
+}
+// K steps: fully unrolled (the digits four per 16-byte read) up to K = 160; beyond that -- the 296 limbs of a
+// 4096-bit key's n^2, whose unrolled product would not fit the instruction cache -- a loop over groups of LW steps
+// (compile-time rotations inside a group) and an unrolled tail of K % LW steps
 template <int K, int LW, int... Js>
 __device__ __forceinline__ void steps(uint64_t (&P)[LW], const uint32_t (&a)[LW], const uint32_t* B,
                                       const uint32_t (&m)[LW], uint32_t mprime, std::integer_sequence<int, Js...>) {
-  Digits<K> d(B);
-  (step<LW, Js>(P, a, d.template get<Js>(), m, mprime), ...);
+  if constexpr (K <= 160) {
+    Digits<K> d(B);
+    (step<LW, Js>(P, a, d.template get<Js>(), m, mprime), ...);
+  } else {
+#pragma unroll 1
+    for (int g = 0; g < K / LW; ++g)
+      step_group<LW>(P, a, B + g * LW, m, mprime, std::make_integer_sequence<int, LW>{});
+    step_group<LW>(P, a, B + (K / LW) * LW, m, mprime, std::make_integer_sequence<int, K % LW>{});
+  }
 }
 
 // canonical limbs of the accumulator after K steps (rotation K % LW); bn_group.hpp normalize with L -> LW

@@ -389,3 +389,31 @@ def test_rows_largest_call_all_kernels(ctxs):
     val = _dboth(crt, a[0], a[1])[0]
     assert np.array_equal(val, x.astype(np.float64))
     _pboth(pub, x, **kw)
+
+
+def test_rows_public_4096(golden):
+    """k_pe_w<296> (the product loop rolled in groups of 19 steps) against k_encrypt<8>, the reference goldens and the
+    oracle: explicit r, edge obfuscators and the device stream."""
+    N = _native()
+    key = _key(golden, 4096)
+    pub = N.Context(key.n, 0)
+    recs = golden["encrypt"]["4096"]
+    x = np.array([r["bits"] for r in recs], dtype=np.uint32).view(np.float32)
+    ct, ex, _ = _pboth(pub, x, obf_mode=N.PAI_OBF_GIVEN, r=[int(r["r"], 16) for r in recs])
+    got = N.words_to_ints(ct)
+    for i, rec in enumerate(recs):
+        assert (hex(got[i]), int(ex[i])) == (rec["c"], rec["e"]), f"element {i}"
+    k = key
+    rs = [0, 1, k.n - 1, k.n, 5 * k.p, k.nsquare - 1, (1 << (32 * pub.ct_words)) - 1]
+    x = np.array([0.0, 1.0, -1.0, 3.5, -2.25, 1e-30, -1e30], dtype=np.float32)
+    ct, _, _ = _pboth(pub, x, obf_mode=N.PAI_OBF_GIVEN, r=rs)
+    got = N.words_to_ints(ct)
+    for i, r in enumerate(rs):
+        assert got[i] == O.encrypt_value(x[i], k, r)[0], f"r #{i}"
+    x = np.random.default_rng(296).standard_normal(9).astype(np.float32)
+    rk = bytes(range(2, 34))
+    ct, ex, _ = _pboth(pub, x, obf_mode=N.PAI_OBF_RNG, rng_key=rk, index_base=5)
+    got = N.words_to_ints(ct)
+    rbytes = ((4096 + 64 + 31) // 32) * 4
+    for i in (0, 4, 8):
+        assert got[i] == O.encrypt_value(x[i], key, O.device_r(rk, 5 + i, rbytes))[0], f"element {i}"

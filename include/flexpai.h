@@ -142,8 +142,9 @@ typedef struct pai_comm pai_comm;
                                   * whenever they fit)                                                        */
 #define PAI_OPT_ROWS_MAX 14      /* calls of at most this many elements (default 4096) run their exponentiations with
                                   * each residue on a 16-lane row (kernels_crtw.hpp: the key holder's CRT encryption
-                                  * k_crt_w and decryption k_dec_w, a public-key-only party's encryption k_pe_w; the latency of protocol-sized calls) instead of one lane / lane
-                                  * pair each; 0 disables. Same bits either way                                  */
+                                  * k_crt_w and decryption k_dec_w, a public-key-only party's encryption k_pe_w; the
+                                  * latency of protocol-sized calls) instead of one lane / lane pair each; 0
+                                  * disables. Same bits either way                                               */
 
 /* Number of visible GPUs (0 when there is none or the runtime cannot start). */
 int pai_device_count(int* count);

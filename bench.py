@@ -595,9 +595,11 @@ def nb1024_leg(args, dev, stream, lib, rng_key, x, local_rank, base, steps=5):
     wpe = float((_P(nb1) + 1) * _Mp(nb1 // 32)) if pe else work_enc_public(nb1)
     dom_ms = (pst[1] if pe else sum(pst)) if pst else tp * 1e3
     same_pub = bool(torch.equal(ctp[:nchk], ctg)) and bool(torch.equal(exp_[:nchk], exg))
+    pk_names = (("k_pe1_words + k_dec_pre_pair + k_pe1_pow + k_pe1_fin", "k_pe1_pow") if nb1 <= 1024 else
+                ("k_pe_pre + k_pe_pow + k_pe_fin", "k_pe_pow")) if pe else ("k_encrypt", "k_encrypt")
     leg["public_key_path"] = {"value": npub / tp, "unit": "encrypts/s", "elements": npub,
-                              "kernel": "k_pe_pre + k_pe_pow + k_pe_fin" if pe else "k_encrypt", "stages_ms": pst,
-                              "roofline": {"kernel": "k_pe_pow" if pe else "k_encrypt", "work_per_unit": wpe,
+                              "kernel": pk_names[0], "stages_ms": pst,
+                              "roofline": {"kernel": pk_names[1], "work_per_unit": wpe,
                                            "frac": npub * wpe / (dom_ms * 1e-3) / INT_MAC_PEAK},
                               "bit_identical_to_crt_on_prefix": same_pub}
     if not same_pub:

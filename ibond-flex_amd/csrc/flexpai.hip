@@ -53,6 +53,7 @@ static const char* xcheck_env(const char* name) {
 #include "engine_grp.hpp"
 #include "engine_mul.hpp"
 #include "engine_crtw.hpp"
+#include "engine_pe1.hpp"
 
 using namespace fpai;
 
@@ -128,6 +129,12 @@ struct pai_ctx {
   int dec4_kchunks = 0;
   // public-key encryption on split pairs (kernels_pe.hpp): 2048-bit n, the default ($FLEXPAI_PAIR=0: k_encrypt)
   bool pe_ok = false;
+  // public-key encryption of n <= 1024 bits on pairs over the 37 limbs of n (kernels_pe1.hpp)
+  bool pe1_ok = false;
+  DecPairHalf* d_pe1_half = nullptr;   // n, the pair of R^3 mod n^2 (k_dec_pre_pair's constants)
+  uint32_t *d_pe1_n = nullptr, *d_pe1_one = nullptr, *d_pe1_prog = nullptr, *d_pe1_r2n = nullptr;
+  int pe1_nprog = 0;
+  uint32_t pe1_mprime = 0;
   bool pef_ok = false;          // the factored public-key chain (k_pe_pow_f) is set up ($FLEXPAI_PEF=0, test build: off)
   PeConst* d_pe = nullptr;
   uint32_t *d_pe_n = nullptr, *d_pe_r2 = nullptr, *d_pe_oneR = nullptr;   // n, R^2, R mod n (R = 2^(28 74)): the batch
@@ -721,6 +728,7 @@ int pai_device_count(int* count) {
 }
 
 static int setup_pe(pai_ctx* c, const HBig& n);
+static int setup_pe1(pai_ctx* c, const HBig& n);
 
 int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** out) {
   if (!n_le || !out || n_bytes == 0) return fail(PAI_ERR_ARG, "pai_ctx_create: null argument");
@@ -778,7 +786,8 @@ int pai_ctx_create(const uint8_t* n_le, size_t n_bytes, int device, pai_ctx** ou
   if ((rc = upload(c, rs, &c->d_RS)) || (rc = upload(c, c->N.limbs(c->S_e, LB), &c->d_N)) ||
       (rc = upload(c, R2.limbs(c->S_e, LB), &c->d_R2)) ||
       (rc = upload(c, n.limbs(c->S_e, LB), &c->d_nl)) || (rc = upload(c, prog, &c->d_prog)) ||
-      (rc = upload(c, oneR.limbs(c->S_e, LB), &c->d_oneR)) || (rc = (SetupTrace("  setup_pe"), setup_pe(c, n)))) {
+      (rc = upload(c, oneR.limbs(c->S_e, LB), &c->d_oneR)) || (rc = (SetupTrace("  setup_pe"), setup_pe(c, n))) ||
+      (rc = setup_pe1(c, n))) {
     delete c;
     return rc;
   }
@@ -946,6 +955,39 @@ static int setup_pe(pai_ctx* c, const HBig& n) {
   }
   if ((rc = upload(c, pc, &c->d_pe))) return rc;
   c->pe_ok = true;
+  return 0;
+}
+
+// Public-key encryption on pairs over the S = 37 limbs of n for n <= 1024 bits (kernels_pe1.hpp; R = 2^1036 >= 2^12 n):
+// n, the pair of R^3 mod n^2 (r's two digit chunks, k_dec_pre_pair), the pair (1, 0), the op list over n, R^2 mod n.
+static int setup_pe1(pai_ctx* c, const HBig& n) {
+  bool pair = true;
+  if (const char* e = xcheck_env("FLEXPAI_PAIR")) pair = atoi(e) != 0;
+  const size_t RS = (size_t)LB * PE1_S;
+  if (!pair || n.bits() + 12 > RS || c->ct_words > 64) return 0;
+  std::vector<uint32_t> prog;
+  if (!build_lane_program(n, prog)) return 0;
+  const HBig n2 = mul(n, n);
+  const HBig r3 = mul_pow2_mod(HBig(1), 3 * RS, n2);
+  const HBig qt = div_big(r3, n), rm = sub(r3, mul(qt, n));
+  std::vector<uint32_t> ck = rm.limbs(PE1_S, LB), b = qt.limbs(PE1_S, LB), one(2 * PE1_S, 0);
+  ck.insert(ck.end(), b.begin(), b.end());
+  one[0] = 1;
+  uint32_t *dn, *dck, *done, *dprog, *dr2;
+  int rc;
+  if ((rc = upload(c, n.limbs(PE1_S, LB), &dn)) || (rc = upload(c, ck, &dck)) || (rc = upload(c, one, &done)) ||
+      (rc = upload(c, prog, &dprog)) || (rc = upload(c, mul_pow2_mod(HBig(1), 2 * RS, n).limbs(PE1_S, LB), &dr2)))
+    return rc;
+  const uint32_t mp = mont_prime(n, LB);
+  std::vector<DecPairHalf> h{DecPairHalf{dn, dck, nullptr, nullptr, mp, 0u}};
+  if ((rc = upload(c, h, &c->d_pe1_half))) return rc;
+  c->d_pe1_n = dn;
+  c->d_pe1_one = done;
+  c->d_pe1_prog = dprog;
+  c->pe1_nprog = (int)prog.size();
+  c->d_pe1_r2n = dr2;
+  c->pe1_mprime = mp;
+  c->pe1_ok = true;
   return 0;
 }
 
@@ -2099,7 +2141,7 @@ int pai_ctx_get_option(const pai_ctx* c, int option, int* value) {
       return 0;
     case PAI_OPT_PAIR:
       *value = ((c->dec_pair_ok || c->dec4_ok) && c->dec_lane_enabled ? 1 : 0) | (c->crt_pair_ok ? 2 : 0) |
-               (c->pe_ok ? 4 : 0);
+               (c->pe_ok || c->pe1_ok ? 4 : 0);
       return 0;
   }
   return fail(PAI_ERR_ARG, "pai_ctx_get_option: unknown option");
@@ -2777,6 +2819,60 @@ static long long pef_min_elems() {
   return 16384;
 }
 
+// public-key encryption for n <= 1024 bits on pairs (kernels_pe1.hpp, engine_pe1.hip), in chunks of CRT_CHUNK elements;
+// stage times: the obfuscator words + k_dec_pre_pair, k_pe1_pow, k_pe1_fin
+static int launch_pe1(pai_ctx* c, const EncParams& e, hipStream_t st) {
+  const long long N = e.n;
+  const long long chunk = std::min(N, CRT_CHUNK);
+  const int RW = e.obf == PAI_OBF_GIVEN ? e.r_words : e.rng_words;
+  const int kchunks = 2;   // r's digits in two chunks of S (zeros past its words): the constant is the pair of R^3
+  if (RW <= 0 || 32 * RW > kchunks * LB * PE1_S) return fail(PAI_ERR_ARG, "1024-bit pair encrypt: obfuscator too wide");
+  int occ = 1;
+  pe1_occupancy(&occ);
+  const long long lb = (chunk + LANE_BLOCK - 1) / LANE_BLOCK;
+  const int gx = (int)std::max<long long>(1, std::min<long long>(lb, (long long)occ * c->cus));
+  int rc = ensure_scratch(c, (size_t)gx * LANE_BLOCK * lane_scratch_words<2 * PE1_S>() * 4);
+  if (rc) return rc;
+  const size_t rwb = (size_t)RW * 4, xwb = (size_t)2 * PE1_S * 4;   // per element
+  if ((rc = ensure_work(c, (rwb + xwb) * chunk))) return rc;
+  const size_t esz = e.dtype == PAI_F32 ? 4 : 8;
+  for (long long off = 0; off < N; off += chunk) {
+    const long long n = std::min(chunk, N - off);
+    hipEvent_t* ev = stage_chunk(c);
+    if (ev) c->nev = 4;
+    Pe1Params p{};
+    p.x = (const char*)e.x + (size_t)off * esz;
+    p.dtype = e.dtype;
+    p.exp_mode = e.exp_mode;
+    p.fexp = e.fexp;
+    p.obf = e.obf;
+    p.r = e.r ? e.r + (size_t)off * e.r_stride : nullptr;
+    p.r_stride = e.r_stride;
+    p.r_words = e.r_words;
+    p.rng_words = e.rng_words;
+    std::memcpy(p.rng_key, e.rng_key, sizeof(p.rng_key));
+    p.index_base = e.index_base + (unsigned long long)off;
+    p.n = n;
+    p.nl = c->d_pe1_n;
+    p.one = c->d_pe1_one;
+    p.prog = c->d_pe1_prog;
+    p.nprog = c->pe1_nprog;
+    p.r2n = c->d_pe1_r2n;
+    p.mprime = c->pe1_mprime;
+    p.rw = (uint32_t*)c->d_work;
+    p.rw_words = RW;
+    p.xw = (uint32_t*)((char*)c->d_work + rwb * chunk);
+    p.scratch = (uint32_t*)c->d_scratch;
+    p.ct = e.ct + (size_t)off * c->ct_words;
+    p.exp = e.exp + off;
+    p.status = e.status ? e.status + off : nullptr;
+    p.ct_words = c->ct_words;
+    const DecPairPreParams pre{c->d_pe1_half, n, p.rw, RW, kchunks, p.xw};
+    HIPCHK(pe1_launch(p, pre, gx, c->cus, st, ev));
+  }
+  return 0;
+}
+
 static int launch_pe(pai_ctx* c, const EncParams& e, hipStream_t st) {
   const long long N = e.n;
   const long long chunk = std::min(N, CRT_CHUNK);
@@ -3019,6 +3115,7 @@ int pai_encrypt_dev(pai_ctx* c, int dtype, const void* d_x, size_t N, int exp_mo
     return 0;
   }
   if (obf_mode != PAI_OBF_NONE && c->pe_ok && c->ct_words == 2 * 64) return launch_pe(c, p, st);
+  if (obf_mode != PAI_OBF_NONE && c->pe1_ok) return launch_pe1(c, p, st);
   switch (c->tpi_e) {
     case 2: return launch_encrypt<2>(c, p, st);
     case 4: return launch_encrypt<4>(c, p, st);

@@ -120,9 +120,10 @@ typedef struct pai_comm pai_comm;
                                     kernels_grp_pair.hpp: the default; round 1's k_fb / k_fbg were retired in round 6),
                                     else 0                                                                     */
 #define PAI_OPT_PAIR 9           /* read-only: bit 0 = decryption, bit 1 = CRT encryption (stage B), bit 2 =
-                                    public-key encryption (2048-bit n) run on p-adic pairs (kernels_pair.hpp,
-                                    kernels_dec4.hpp, kernels_pe.hpp: the default; $FLEXPAI_PAIR=0 at context
-                                    creation selects the kernels they replace)                                */
+                                    public-key encryption (2048-bit n, and n of at most 1024 bits) run on
+                                    p-adic pairs (kernels_pair.hpp, kernels_dec4.hpp, kernels_pe.hpp,
+                                    kernels_pe1.hpp: the default; $FLEXPAI_PAIR=0 at context creation selects
+                                    the kernels they replace)                                                  */
 #define PAI_OPT_PUBLIC_FB 10     /* 1 (default): PAI_OBF_RNG encryption WITHOUT the private key (2048-bit n) samples
                                   * r^n through the public fixed bases (kernels_pfb.hpp) once the break-even count
                                   * is reached (pai_ctx_public_fb_policy); get: 1 when the path is enabled and not

@@ -372,8 +372,13 @@ __device__ __forceinline__ void decf_run(uint32_t (&A)[S], uint32_t (&B)[S], con
 // box, 443 -> 412 ms per 1M, 2.31 -> 2.48 M dec/s (profiles/r05_ab_dec_pair_occupancy.txt; k_crt_b_pair, with heavier
 // spills, lost 5 % the same way and keeps LANE_OCC).
 constexpr int DEC_PAIR_OCC = 2;
+// The 1024-bit key's chain (S = 19) at three waves (round 6): 168 VGPRs and 36 spilled against 237 at two waves;
+// same box, interleaved x3: 66.1-67.0 -> 63.1-63.5 ms per 1M, 15.5 -> 16.3 M dec/s (profiles/r06r_ab_dec19_occupancy.txt)
+#ifndef DEC_PAIR_OCC19
+#define DEC_PAIR_OCC19 3
+#endif
 template <int S, bool FACTORED>
-__global__ __launch_bounds__(LANE_BLOCK, DEC_PAIR_OCC) void k_dec_pow_pair(CrtParams p) {
+__global__ __launch_bounds__(LANE_BLOCK, S == 19 ? DEC_PAIR_OCC19 : DEC_PAIR_OCC) void k_dec_pow_pair(CrtParams p) {
   const int half = blockIdx.y;
   const CrtHalf* H = p.halves + half;
   uint32_t m[S];

@@ -487,3 +487,26 @@ def test_pack_numbers_checks_and_words_in_c():
     bad[4] = "x"
     with pytest.raises(TypeError, match="should be an PaillierEncryptedNumber"):
         pd.decrypt(bad)
+
+
+def test_option_numbers_match_the_header():
+    """Every PAI_OPT_* / PAI_OBF_* / PAI_F* number the Python binding uses is the one include/flexpai.h defines."""
+    import re
+    from flex.crypto.paillier import _native as N
+    with open(os.path.join(ROOT, "include", "flexpai.h")) as f:
+        defs = dict(re.findall(r"^#define (PAI_(?:OPT|OBF)_[A-Z_0-9]+)\s+(\d+)", f.read(), re.M))
+    used = {k: getattr(N, k) for k in dir(N) if re.fullmatch(r"PAI_(?:OPT|OBF)_[A-Z_0-9]+", k)}
+    assert "PAI_OPT_ROWS_MAX" in used and used
+    for k, v in used.items():
+        assert k in defs and int(defs[k]) == v, k
+
+
+def test_product_library_carries_the_row_and_pair_kernels():
+    """The row kernels (kernels_crtw.hpp) and the 1024-bit public pair path (kernels_pe1.hpp) are in the product."""
+    import subprocess
+    lib = os.path.join(ROOT, "ibond-flex_amd", "flex", "crypto", "paillier", "_native", "libflexpai.so")
+    if not os.path.exists(lib):
+        pytest.skip("library not built")
+    names = subprocess.run(["strings", lib], capture_output=True, text=True).stdout
+    for k in ("k_crt_w", "k_dec_w", "k_pe_w", "k_pe1_pow", "k_pe1_fin", "k_pe1_words"):
+        assert k in names, k
